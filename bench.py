@@ -1,0 +1,159 @@
+"""Headline benchmark: Solver env-steps/sec at 20x20, 4096 envs/GPU (BASELINE.json metric).
+
+One "step" = one heist_step launch over all envs of the rank: move, camera/guard
+update, raycast visibility, reward/termination, in-kernel auto-reset, and the
+[N,3,20,20] float32 observation write.  Inputs (layouts, per-step actions) are
+resident in HBM before the timed region.  Multi-GPU: one process per GPU (torchrun),
+envs sharded by rank with no data-path collective (weak scaling); the only RCCL
+calls are the barrier and the max-over-ranks of the elapsed time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 4096] [--no-cpu-baseline]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "rl-project-heist-architect-adversarial-reinforcement-learning-framework-cse4019_amd")
+sys.path[:0] = [ROOT, PKG]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "Solver env-steps/sec at 20×20, 4096 envs/GPU, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes_per_env_step(R, C, ncam, nguard):
+    """obs f32 write + grid u8 read + action i64 + reward f32 + done + status
+    + read and write of the dynamic per-env state (24 + 8*ncam + 12*nguard bytes)."""
+    return 12 * R * C + R * C + 8 + 4 + 1 + 1 + 2 * (24 + 8 * ncam + 12 * nguard)
+
+
+def cpu_baseline(layouts, cfg, budget, target_s=10.0, threads=1):
+    """The C oracle (restatement of the reference CPU path) on a bounded sample of the
+    same workload: env.step + get_state_tensor with random actions, auto-reset."""
+    from oracle import pyoracle as po
+    sample = layouts[:256]
+
+    def make():
+        envs = []
+        for lay in sample:
+            o = po.OracleEnv(cfg.grid_rows, cfg.grid_cols, cfg.max_steps, cfg.start_pos, cfg.vault_pos, budget)
+            o.set_layout(*lay)
+            o.reset()
+            envs.append(o)
+        return envs
+
+    envs = make()
+    t0 = time.perf_counter()
+    n = po.run_random(envs, 4, seed=1, n_threads=threads)
+    dt = time.perf_counter() - t0
+    steps = max(4, int(4 * target_s / max(dt, 1e-6)))
+    envs = make()
+    t0 = time.perf_counter()
+    n = po.run_random(envs, steps, seed=2, n_threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": "%d of the same synthetic 20x20 layouts x %d ticks (%d env-steps, %.1f s), random actions, "
+                      "auto-reset, state tensor each tick; C oracle (oracle/heist_oracle.c) with host libm"
+                      % (len(sample), steps, n, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--budget", type=int, default=15)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = torch.distributed
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from heist_amd import EnvironmentConfig, HeistEnv
+    from heist_amd.layouts import valid_synthetic_layouts
+
+    cfg = EnvironmentConfig(grid_rows=20, grid_cols=20, max_steps=200, architect_budget=args.budget)
+    N = args.envs
+    env = HeistEnv(N, cfg, max_cams=8, max_guards=4, max_path=16, device=dev, auto_reset=True)
+    layouts = valid_synthetic_layouts(env, args.budget, seed=1234 + rank)
+    env.reset()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(4321 + rank)
+    actions = torch.randint(0, 5, (args.warmup + args.steps, N), device=dev, generator=gen, dtype=torch.int64)
+    stream = torch.cuda.current_stream(dev)
+
+    for k in range(args.warmup):
+        env.step(actions[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        env.step(actions[args.warmup + k])
+        ev[k][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ncam = float(np.mean([len(c) for _, c, _ in layouts]))
+    ngu = float(np.mean([len(g) for _, _, g in layouts]))
+    b_step = algorithmic_bytes_per_env_step(20, 20, ncam, ngu)
+    achieved = b_step * N / (kern_ms * 1e-3) / 1e9  # GB/s, per launch / launch duration
+    total_steps = args.steps * N * world
+    value = total_steps / elapsed
+
+    if rank == 0:
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "heist_step_traffic.json")
+        if os.path.exists(tf) and N == 4096:
+            with open(tf) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        line = {
+            "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": "env-only heist_step, 20x20 grid, %d envs/GPU, synthetic budget-%d layouts "
+                                   "(mean %.2f cameras, %.2f guards/env), uniform random actions, auto-reset"
+                                   % (N, args.budget, ncam, ngu),
+                       "envs_per_gpu": N, "grid": "20x20", "parallelism": "env-sharded x%d" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "heist::step_kernel", "kernel_ms": kern_ms,
+                         "algorithmic_bytes_per_env_step": b_step},
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(layouts, cfg, args.budget, target_s=args.cpu_seconds, threads=1)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

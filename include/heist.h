@@ -1,0 +1,134 @@
+/* heist.h -- C ABI of the MI355X-native Heist Architect hot path (libheist_hip.so).
+ *
+ * The reference (a pure-Python package) has no FFI for this path; its boundary is the
+ * Python class API that training and the UI call.  Each entry point below replaces one
+ * reference interface (paths relative to the reference repository root) and is bound
+ * by the Python mirror package heist_amd (see INTEGRATION.md for the ctypes binding).
+ *
+ * Conventions
+ *  - All array pointers are DEVICE pointers owned by the caller (e.g. torch tensors on
+ *    the same HIP device), except `reward_consts` in heist_create (host).
+ *  - Every call is enqueued on `stream` and is asynchronous; nothing synchronises.
+ *  - Return 0 on success, HEIST_EINVAL for bad arguments, else a hipError_t value.
+ *    heist_last_error() gives a message for the calling thread's last failure.
+ *  - A heist_t handle is bound to the device that was current at heist_create and is
+ *    not thread-safe: use one handle per device/thread.
+ *  - Layouts are [env][...] row-major; grids are [env][row][col]; obs is [env][3][R][C].
+ */
+#ifndef HEIST_H
+#define HEIST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HEIST_ABI_VERSION 1
+#define HEIST_EINVAL 100000
+
+/* status_out codes of heist_step (environment.py:236-297 info["status"]). */
+#define HEIST_RUNNING 0
+#define HEIST_DETECTED 1
+#define HEIST_VAULT_REACHED 2
+#define HEIST_TIMEOUT 3
+#define HEIST_ALREADY_DONE 4
+
+typedef struct heist_env* heist_t;
+typedef struct ihipStream_t* heist_stream_t; /* == hipStream_t */
+
+int heist_abi_version(void);
+const char* heist_last_error(void);
+
+/* Replaces HeistEnvironment.__init__ / EnvironmentConfig (environment.py:18-97) for a
+ * batch of n_envs independent environments.  R, C <= 64.  reward_consts (host) =
+ * {reward_step, reward_detection, reward_vault}.  max_cams / max_guards / max_path bound
+ * the per-env layout capacity. */
+int heist_create(int rows, int cols, int max_steps, int start_r, int start_c, int vault_r, int vault_c,
+                 const double* reward_consts, int n_envs, int max_cams, int max_guards, int max_path,
+                 heist_t* out);
+int heist_destroy(heist_t h);
+
+/* Replaces HeistEnvironment.set_layout + _reset_layout + is_level_valid
+ * (environment.py:102-177) and BudgetManager.purchase (budget.py:48-58), per env:
+ *   wall_rc     [N][max_walls][2]      int32   walls in list order (first n_walls[e] used)
+ *   cam_params  [N][max_cams][6]       float64 row, col, fov_angle, heading, rotation_speed, vision_range
+ *   guard_paths [N][max_guards][max_path][2] int32 patrol_path points
+ *   guard_meta  [N][max_guards][3]     int32   path length, speed, vision_range
+ *   guard_fov   [N][max_guards]        float64 fov_angle
+ *   budget      [N]                    int32   BudgetManager.total_budget
+ *   valid_out   [N]                    uint8   bfs_path_exists(start, vault)
+ * Guard path points must lie inside the grid.  Solver state is left untouched (call
+ * heist_reset next, as training.py:516 does). */
+int heist_set_layout(heist_t h, int max_walls, const int32_t* wall_rc, const int32_t* n_walls,
+                     const double* cam_params, const int32_t* n_cams, const int32_t* guard_paths,
+                     const int32_t* guard_meta, const double* guard_fov, const int32_t* n_guards,
+                     const int32_t* budget, uint8_t* valid_out, heist_stream_t stream);
+
+/* Replaces HeistEnvironment.reset + get_state_tensor (environment.py:183-214, :347-374)
+ * for envs with mask[e] != 0 (mask == NULL: all).  obs_out [N][3][R][C] float32; rows of
+ * unmasked envs are not written. */
+int heist_reset(heist_t h, const uint8_t* mask, float* obs_out, heist_stream_t stream);
+
+/* Replaces HeistEnvironment.step + get_state_tensor (environment.py:216-299, :347-374).
+ *   actions [N] int64 in 0..4;  obs_out [N][3][R][C] float32;  reward_out [N] float32
+ *   (the float64 reward rounded, as agents/solver.py:138 stores it); reward64_out [N]
+ *   float64 or NULL; done_out [N] uint8; status_out [N] int8 (HEIST_* codes).
+ * auto_reset != 0: an env that finishes this tick is reset in the same launch and its
+ * obs row holds the reset observation (training.py:515-520 next attempt), while reward,
+ * done and status describe the finishing tick.  auto_reset == 0: finished envs answer
+ * later steps with reward 0 / HEIST_ALREADY_DONE (environment.py:232-233). */
+int heist_step(heist_t h, const int64_t* actions, float* obs_out, float* reward_out, double* reward64_out,
+               uint8_t* done_out, int8_t* status_out, int auto_reset, heist_stream_t stream);
+
+/* Copies per-env state out for get_environment_state / the single-env compatibility
+ * class (environment.py:388-417).  Any pointer may be NULL.
+ *   scalars [N][12] int32: pos_r, pos_c, tick, done, detected, vault_reached, prev_dist,
+ *                          initial_dist, n_cams, n_guards, n_walls, budget_spent
+ *   grid [N][R][C] int8;  cam_heading [N][max_cams] f64;  guard_idx [N][max_guards] int32;
+ *   guard_heading [N][max_guards] f64 */
+int heist_export(heist_t h, int32_t* scalars, int8_t* grid, double* cam_heading, int32_t* guard_idx,
+                 double* guard_heading, heist_stream_t stream);
+
+/* Replaces bfs_path_exists (utils.py:52-85) on a batch of grids [N][R][C] int32. */
+int heist_bfs_valid(const int32_t* grid, int n, int rows, int cols, int start_r, int start_c, int goal_r,
+                    int goal_c, uint8_t* valid_out, heist_stream_t stream);
+
+/* Replaces Camera.get_vision_cone_tiles (security.py:53-101, kind 0) and
+ * Guard.get_visible_tiles (security.py:161-192, kind 1) for n independent emitters:
+ *   walls [n][R][C] uint8 (nonzero = wall); meta [n][4] int32 = kind, row, col, range;
+ *   params [n][2] f64 = fov_angle, heading;  tiles_out [n][R][C] uint8 (1 = visible). */
+int heist_cones(int n, int rows, int cols, const uint8_t* walls, const int32_t* meta, const double* params,
+                uint8_t* tiles_out, heist_stream_t stream);
+
+/* Replaces SolverAgent._compute_gae + returns (agents/solver.py:142-143, :228-244) on a
+ * [T][N] rollout (column e = env e's concatenated episodes).  dones [T][N] uint8.
+ * last_value [N] bootstraps t = T-1 (NULL = 0, the reference's buffer-end rule).  gamma and
+ * lam are taken in float64 because the reference forms gamma*lam in Python floats. */
+int heist_gae(const float* rewards, const float* values, const uint8_t* dones, const float* last_value,
+              int T, int n, double gamma, double lam, float* adv_out, float* ret_out, heist_stream_t stream);
+
+/* Advantage normalisation (agents/solver.py:146-147): x <- (x - mean) / (std + eps),
+ * unbiased std; skipped when the global count is <= 1.  acc is a device float64[3] the
+ * caller zeroes.  Phases (multi-GPU callers all-reduce acc between them):
+ *   phase 0: acc[0] += sum(x), acc[1] += n            -> all-reduce acc[0..1]
+ *   phase 1: acc[2] += sum((x - acc[0]/acc[1])^2)     -> all-reduce acc[2]
+ *   heist_adv_apply(x, n, acc, eps)
+ * heist_adv_normalize runs both phases and the apply on one device (acc = scratch3). */
+int heist_adv_moments(const float* x, int64_t n, int phase, double* acc, heist_stream_t stream);
+int heist_adv_apply(float* x, int64_t n, const double* acc, float eps, heist_stream_t stream);
+int heist_adv_normalize(float* x, int64_t n, double* scratch3, float eps, heist_stream_t stream);
+
+/* Clipped PPO loss of SolverAgent.update (agents/solver.py:172-193) over M samples with
+ * Categorical(probs=softmax(logits)) semantics, fused forward + backward:
+ *   logits [M][A] f32 (A <= 16), values [M] f32, actions [M] int64, old_logp/adv/ret [M] f32;
+ *   loss_parts [4] f32 = total, policy, value, entropy (means over M);
+ *   dlogits [M][A], dvalues [M] = d(total)/d(input);  scratch >= 3*ceil(M/256) float64. */
+int heist_ppo_loss(const float* logits, const float* values, const int64_t* actions, const float* old_logp,
+                   const float* adv, const float* ret, int M, int A, double clip, double vcoef, double ecoef,
+                   float* loss_parts, float* dlogits, float* dvalues, double* scratch, heist_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,302 @@
+// heist_capi.hip -- extern "C" entry points of libheist_hip.so (declared in include/heist.h).
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "heist.h"
+#include "heist_device.h"
+
+#pragma clang fp contract(off)
+
+namespace heist {
+hipError_t launch_init(const EnvParams& p, hipStream_t st);
+hipError_t launch_set_layout(const EnvParams& p, int max_walls, const int32_t* wall_rc, const int32_t* n_walls,
+                             const double* cam_params, const int32_t* n_cams, const int32_t* guard_paths,
+                             const int32_t* guard_meta, const double* guard_fov, const int32_t* n_guards,
+                             const int32_t* budget, uint8_t* valid_out, hipStream_t st);
+hipError_t launch_reset(const EnvParams& p, const uint8_t* mask, float* obs, hipStream_t st);
+hipError_t launch_step(const EnvParams& p, const int64_t* actions, float* obs, float* rew, double* rew64,
+                       uint8_t* done_out, int8_t* status_out, int auto_reset, hipStream_t st);
+hipError_t launch_export(const EnvParams& p, int32_t* scalars, int8_t* grid, double* cam_heading, int32_t* guard_idx,
+                         double* guard_heading, hipStream_t st);
+hipError_t launch_bfs(const int32_t* grid, int n, int R, int C, int sr, int sc, int gr, int gc, uint8_t* out,
+                      hipStream_t st);
+hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
+                        uint8_t* out, hipStream_t st);
+hipError_t launch_gae(const float* r, const float* v, const uint8_t* d, const float* last_value, int T, int N,
+                      double gamma, double lam, float* adv, float* ret, hipStream_t st);
+hipError_t launch_adv_moments(const float* x, int64_t n, int phase, double* acc, hipStream_t st);
+hipError_t launch_adv_apply(float* x, int64_t n, const double* acc, float eps, hipStream_t st);
+hipError_t launch_ppo_loss(const float* logits, const float* values, const int64_t* actions, const float* old_logp,
+                           const float* adv, const float* ret, int M, int A, double clip, double vcoef, double ecoef,
+                           float* parts, float* dlogits, float* dvalues, double* scratch, hipStream_t st);
+}  // namespace heist
+
+using heist::EnvParams;
+
+struct heist_env {
+  int device;
+  EnvParams p;
+  void* allocs[8];
+  int n_allocs;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int check_hip(hipError_t e, const char* what) {
+  if (e == hipSuccess) return 0;
+  return fail((int)e, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HEIST_REQUIRE(cond, msg) \
+  do {                           \
+    if (!(cond)) return fail(HEIST_EINVAL, msg); \
+  } while (0)
+
+int check_handle(heist_t h) {
+  HEIST_REQUIRE(h != nullptr, "null heist_t handle");
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev != h->device)
+    return fail(HEIST_EINVAL, "heist_t used on device " + std::to_string(dev) + " but created on device " +
+                                  std::to_string(h->device));
+  return 0;
+}
+
+double py_mod(double x, double m) {  // Python float %
+  double r = std::fmod(x, m);
+  if (r != 0.0) {
+    if ((m < 0) != (r < 0)) r += m;
+  } else {
+    r = std::copysign(0.0, m);
+  }
+  return r;
+}
+
+// Guard heading after a move by (dr, dc): math.degrees(math.atan2(-dr, dc)) % 360.0
+// (security.py:159), evaluated with the host libm exactly as CPython does.
+std::vector<double> heading_table(int R, int C) {
+  const double rad_to_deg = 180.0 / 3.141592653589793;  // CPython math.degrees factor
+  std::vector<double> t((size_t)(2 * R - 1) * (2 * C - 1), 0.0);
+  for (int dr = -(R - 1); dr <= R - 1; ++dr)
+    for (int dc = -(C - 1); dc <= C - 1; ++dc) {
+      if (dr == 0 && dc == 0) continue;
+      const double y = (double)(-dr), x = (double)dc;
+      double a;
+      if (y == 0.0) a = std::copysign(1.0, x) == 1.0 ? std::copysign(0.0, y) : std::copysign(3.141592653589793, y);
+      else a = std::atan2(y, x);  // CPython m_atan2 for finite, nonzero y
+      t[(size_t)(dr + R - 1) * (2 * C - 1) + (dc + C - 1)] = py_mod(a * rad_to_deg, 360.0);
+    }
+  return t;
+}
+
+}  // namespace
+
+extern "C" {
+
+int heist_abi_version(void) { return HEIST_ABI_VERSION; }
+
+const char* heist_last_error(void) { return g_err.c_str(); }
+
+int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, const double* reward_consts, int n_envs,
+                 int max_cams, int max_guards, int max_path, heist_t* out) {
+  HEIST_REQUIRE(out != nullptr, "heist_create: out is null");
+  *out = nullptr;
+  HEIST_REQUIRE(R >= 3 && C >= 3 && R <= heist::kMaxDim && C <= heist::kMaxDim, "heist_create: need 3 <= rows, cols <= 64");
+  HEIST_REQUIRE(sr >= 0 && sr < R && sc >= 0 && sc < C && vr >= 0 && vr < R && vc >= 0 && vc < C,
+                "heist_create: start/vault outside the grid");
+  HEIST_REQUIRE(n_envs >= 1, "heist_create: n_envs must be >= 1");
+  HEIST_REQUIRE(max_cams >= 0 && max_guards >= 0 && max_cams + max_guards <= heist::kMaxEmitters,
+                "heist_create: need max_cams + max_guards <= 64");
+  HEIST_REQUIRE(max_path >= 1 && max_path <= 4096, "heist_create: need 1 <= max_path <= 4096");
+  HEIST_REQUIRE(max_steps >= 1, "heist_create: max_steps must be >= 1");
+  HEIST_REQUIRE(reward_consts != nullptr, "heist_create: reward_consts is null");
+
+  heist_env* h = new heist_env();
+  if (hipGetDevice(&h->device) != hipSuccess) {
+    delete h;
+    return fail(HEIST_EINVAL, "heist_create: no HIP device");
+  }
+  EnvParams& p = h->p;
+  p.R = R; p.C = C; p.RC = R * C; p.max_steps = max_steps;
+  p.sr = sr; p.sc = sc; p.vr = vr; p.vc = vc;
+  p.r_step = reward_consts[0]; p.r_detect = reward_consts[1]; p.r_vault = reward_consts[2];
+  p.n_envs = n_envs; p.max_cams = max_cams; p.max_guards = max_guards; p.max_path = max_path;
+
+  const size_t n = (size_t)n_envs;
+  const std::vector<double> htab = heading_table(R, C);
+  std::vector<float> planes((size_t)2 * R * C);
+  for (int r = 0; r < R; ++r)
+    for (int c = 0; c < C; ++c) {  // environment.py:356-365 with NumPy-2 float32 adds
+      const int d = std::abs(r - vr) + std::abs(c - vc);
+      const float g = (float)(-0.3 * ((double)d / (double)(R + C)));
+      planes[(size_t)r * C + c] = 0.0f + g;
+      planes[(size_t)R * C + (size_t)r * C + c] = 1.0f + g;
+    }
+  p.vault_val = -1.0f + (float)(-0.3 * (0.0 / (double)(R + C)));
+  for (int k = 0; k < 8; ++k) p.tile_lut[k] = k <= 5 ? (float)k / 5.0f : 0.0f;  // environment.py:319
+
+  const size_t sizes[] = {
+      sizeof(heist::EnvScalars) * n,
+      n * p.RC,
+      sizeof(heist::Cam) * n * (max_cams > 0 ? max_cams : 1),
+      sizeof(heist::Guard) * n * (max_guards > 0 ? max_guards : 1),
+      sizeof(uint16_t) * n * (max_guards > 0 ? max_guards : 1) * max_path,
+      sizeof(double) * htab.size(),
+      sizeof(float) * planes.size(),
+  };
+  h->n_allocs = 0;
+  for (size_t k = 0; k < sizeof(sizes) / sizeof(sizes[0]); ++k) {
+    void* ptr = nullptr;
+    hipError_t e = hipMalloc(&ptr, sizes[k]);
+    if (e != hipSuccess) {
+      for (int j = 0; j < h->n_allocs; ++j) (void)hipFree(h->allocs[j]);
+      delete h;
+      return check_hip(e, "heist_create: hipMalloc");
+    }
+    h->allocs[h->n_allocs++] = ptr;
+  }
+  p.scal = (heist::EnvScalars*)h->allocs[0];
+  p.grid = (uint8_t*)h->allocs[1];
+  p.cams = (heist::Cam*)h->allocs[2];
+  p.guards = (heist::Guard*)h->allocs[3];
+  p.paths = (uint16_t*)h->allocs[4];
+  p.heading_tab = (const double*)h->allocs[5];
+  p.plane0 = (const float*)h->allocs[6];
+  p.plane1 = p.plane0 + (size_t)R * C;
+
+  int rc = check_hip(hipMemcpy(h->allocs[5], htab.data(), sizes[5], hipMemcpyHostToDevice), "heist_create: upload");
+  if (!rc) rc = check_hip(hipMemcpy(h->allocs[6], planes.data(), sizes[6], hipMemcpyHostToDevice), "heist_create: upload");
+  if (!rc) rc = check_hip(hipMemset(h->allocs[2], 0, sizes[2]), "heist_create: memset");
+  if (!rc) rc = check_hip(hipMemset(h->allocs[3], 0, sizes[3]), "heist_create: memset");
+  if (!rc) rc = check_hip(hipMemset(h->allocs[4], 0, sizes[4]), "heist_create: memset");
+  if (!rc) rc = check_hip(heist::launch_init(p, nullptr), "heist_create: init");
+  if (!rc) rc = check_hip(hipDeviceSynchronize(), "heist_create: init");
+  if (rc) {
+    heist_destroy(h);
+    return rc;
+  }
+  *out = h;
+  return 0;
+}
+
+int heist_destroy(heist_t h) {
+  if (!h) return 0;
+  for (int j = 0; j < h->n_allocs; ++j) (void)hipFree(h->allocs[j]);
+  delete h;
+  return 0;
+}
+
+int heist_set_layout(heist_t h, int max_walls, const int32_t* wall_rc, const int32_t* n_walls, const double* cam_params,
+                     const int32_t* n_cams, const int32_t* guard_paths, const int32_t* guard_meta,
+                     const double* guard_fov, const int32_t* n_guards, const int32_t* budget, uint8_t* valid_out,
+                     heist_stream_t stream) {
+  if (int rc = check_handle(h)) return rc;
+  HEIST_REQUIRE(max_walls >= 0, "heist_set_layout: max_walls < 0");
+  HEIST_REQUIRE(n_walls && n_cams && n_guards && budget && valid_out, "heist_set_layout: null counts/budget/valid_out");
+  HEIST_REQUIRE(max_walls == 0 || wall_rc, "heist_set_layout: wall_rc is null");
+  HEIST_REQUIRE(h->p.max_cams == 0 || cam_params, "heist_set_layout: cam_params is null");
+  HEIST_REQUIRE(h->p.max_guards == 0 || (guard_paths && guard_meta && guard_fov), "heist_set_layout: guard arrays null");
+  return check_hip(heist::launch_set_layout(h->p, max_walls, wall_rc, n_walls, cam_params, n_cams, guard_paths,
+                                            guard_meta, guard_fov, n_guards, budget, valid_out, (hipStream_t)stream),
+                   "heist_set_layout");
+}
+
+int heist_reset(heist_t h, const uint8_t* mask, float* obs_out, heist_stream_t stream) {
+  if (int rc = check_handle(h)) return rc;
+  HEIST_REQUIRE(obs_out != nullptr, "heist_reset: obs_out is null");
+  return check_hip(heist::launch_reset(h->p, mask, obs_out, (hipStream_t)stream), "heist_reset");
+}
+
+int heist_step(heist_t h, const int64_t* actions, float* obs_out, float* reward_out, double* reward64_out,
+               uint8_t* done_out, int8_t* status_out, int auto_reset, heist_stream_t stream) {
+  if (int rc = check_handle(h)) return rc;
+  HEIST_REQUIRE(actions && obs_out && reward_out && done_out && status_out, "heist_step: null output/input");
+  return check_hip(heist::launch_step(h->p, actions, obs_out, reward_out, reward64_out, done_out, status_out,
+                                      auto_reset, (hipStream_t)stream),
+                   "heist_step");
+}
+
+int heist_export(heist_t h, int32_t* scalars, int8_t* grid, double* cam_heading, int32_t* guard_idx,
+                 double* guard_heading, heist_stream_t stream) {
+  if (int rc = check_handle(h)) return rc;
+  return check_hip(heist::launch_export(h->p, scalars, grid, cam_heading, guard_idx, guard_heading, (hipStream_t)stream),
+                   "heist_export");
+}
+
+int heist_bfs_valid(const int32_t* grid, int n, int rows, int cols, int sr, int sc, int gr, int gc, uint8_t* valid_out,
+                    heist_stream_t stream) {
+  HEIST_REQUIRE(grid && valid_out, "heist_bfs_valid: null pointer");
+  HEIST_REQUIRE(rows >= 1 && cols >= 1 && rows <= heist::kMaxDim && cols <= heist::kMaxDim,
+                "heist_bfs_valid: need 1 <= rows, cols <= 64");
+  HEIST_REQUIRE(sr >= 0 && sr < rows && sc >= 0 && sc < cols && gr >= 0 && gr < rows && gc >= 0 && gc < cols,
+                "heist_bfs_valid: start/goal outside the grid");
+  if (n <= 0) return 0;
+  return check_hip(heist::launch_bfs(grid, n, rows, cols, sr, sc, gr, gc, valid_out, (hipStream_t)stream),
+                   "heist_bfs_valid");
+}
+
+int heist_cones(int n, int rows, int cols, const uint8_t* walls, const int32_t* meta, const double* params,
+                uint8_t* tiles_out, heist_stream_t stream) {
+  HEIST_REQUIRE(walls && meta && params && tiles_out, "heist_cones: null pointer");
+  HEIST_REQUIRE(rows >= 1 && cols >= 1 && rows <= heist::kMaxDim && cols <= heist::kMaxDim,
+                "heist_cones: need 1 <= rows, cols <= 64");
+  if (n <= 0) return 0;
+  return check_hip(heist::launch_cones(n, rows, cols, walls, meta, params, tiles_out, (hipStream_t)stream),
+                   "heist_cones");
+}
+
+int heist_gae(const float* rewards, const float* values, const uint8_t* dones, const float* last_value, int T, int n,
+              double gamma, double lam, float* adv_out, float* ret_out, heist_stream_t stream) {
+  HEIST_REQUIRE(rewards && values && dones && adv_out && ret_out, "heist_gae: null pointer");
+  HEIST_REQUIRE(T >= 0 && n >= 0, "heist_gae: negative size");
+  if (T == 0 || n == 0) return 0;
+  return check_hip(heist::launch_gae(rewards, values, dones, last_value, T, n, gamma, lam, adv_out, ret_out,
+                                     (hipStream_t)stream),
+                   "heist_gae");
+}
+
+int heist_adv_moments(const float* x, int64_t n, int phase, double* acc, heist_stream_t stream) {
+  HEIST_REQUIRE(x && acc, "heist_adv_moments: null pointer");
+  HEIST_REQUIRE(phase == 0 || phase == 1, "heist_adv_moments: phase must be 0 or 1");
+  HEIST_REQUIRE(n >= 0, "heist_adv_moments: negative size");
+  return check_hip(heist::launch_adv_moments(x, n, phase, acc, (hipStream_t)stream), "heist_adv_moments");
+}
+
+int heist_adv_apply(float* x, int64_t n, const double* acc, float eps, heist_stream_t stream) {
+  HEIST_REQUIRE(x && acc, "heist_adv_apply: null pointer");
+  if (n <= 0) return 0;
+  return check_hip(heist::launch_adv_apply(x, n, acc, eps, (hipStream_t)stream), "heist_adv_apply");
+}
+
+int heist_adv_normalize(float* x, int64_t n, double* scratch3, float eps, heist_stream_t stream) {
+  HEIST_REQUIRE(x && scratch3, "heist_adv_normalize: null pointer");
+  if (n <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (int rc = check_hip(hipMemsetAsync(scratch3, 0, 3 * sizeof(double), st), "heist_adv_normalize")) return rc;
+  if (int rc = check_hip(heist::launch_adv_moments(x, n, 0, scratch3, st), "heist_adv_normalize")) return rc;
+  if (int rc = check_hip(heist::launch_adv_moments(x, n, 1, scratch3, st), "heist_adv_normalize")) return rc;
+  return check_hip(heist::launch_adv_apply(x, n, scratch3, eps, st), "heist_adv_normalize");
+}
+
+int heist_ppo_loss(const float* logits, const float* values, const int64_t* actions, const float* old_logp,
+                   const float* adv, const float* ret, int M, int A, double clip, double vcoef, double ecoef,
+                   float* loss_parts, float* dlogits, float* dvalues, double* scratch, heist_stream_t stream) {
+  HEIST_REQUIRE(logits && values && actions && old_logp && adv && ret && loss_parts && dlogits && dvalues && scratch,
+                "heist_ppo_loss: null pointer");
+  HEIST_REQUIRE(M >= 1, "heist_ppo_loss: M must be >= 1");
+  HEIST_REQUIRE(A >= 1 && A <= 16, "heist_ppo_loss: need 1 <= A <= 16");
+  return check_hip(heist::launch_ppo_loss(logits, values, actions, old_logp, adv, ret, M, A, clip, vcoef, ecoef,
+                                          loss_parts, dlogits, dvalues, scratch, (hipStream_t)stream),
+                   "heist_ppo_loss");
+}
+
+}  // extern "C"

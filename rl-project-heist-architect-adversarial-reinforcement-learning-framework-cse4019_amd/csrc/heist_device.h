@@ -1,0 +1,78 @@
+// heist_device.h -- device-side data layout of the batched Heist environment.
+//
+// HBM layout (all [env]-major, one env is handled by one 64-lane wavefront):
+//   EnvScalars [N]                 48 B  solver state + layout counters
+//   grid       [N][R*C]            u8    tile types (utils.py:31-37), static per layout
+//   Cam        [N][max_cams]       32 B  fov, heading, speed (f64), row, col, range, num_rays
+//   Guard      [N][max_guards]     32 B  fov, heading (f64), idx, speed, len, range, num_rays
+//   paths      [N][max_guards][max_path] u16 (row | col << 8)
+// Per-handle constant tables: guard heading by (dr, dc) (host libm atan2), the two
+// static position-channel planes, the tile->float LUT.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace heist {
+
+enum : int { kEmpty = 0, kWall = 1, kStart = 2, kVault = 3, kCamera = 4, kGuard = 5 };
+enum : int { kRunning = 0, kDetected = 1, kVaultReached = 2, kTimeout = 3, kAlreadyDone = 4 };
+
+constexpr int kMaxDim = 64;          // R, C <= 64
+constexpr int kMaxEmitters = 64;     // max_cams + max_guards per env
+constexpr double kDegToRad = 3.141592653589793 / 180.0;  // CPython math.radians factor
+
+struct EnvScalars {
+  int32_t pos_r, pos_c, tick, done;
+  int32_t detected, vault_reached, prev_dist, initial_dist;
+  int32_t n_cams, n_guards, n_walls, spent;
+};
+static_assert(sizeof(EnvScalars) == 48, "EnvScalars layout");
+
+struct Cam {
+  double fov, heading, speed;
+  int16_t row, col, range, num_rays;
+};
+static_assert(sizeof(Cam) == 32, "Cam layout");
+
+struct Guard {
+  double fov, heading;
+  int32_t idx, speed;
+  int16_t len, range, num_rays, pad;
+};
+static_assert(sizeof(Guard) == 32, "Guard layout");
+
+// One ray emitter as the raycaster sees it (a camera or a guard at its current pose).
+struct Emit {
+  double hmh;     // heading - fov / 2.0  (security.py:64, :70)
+  double fov;
+  int32_t row, col, range, num_rays;
+  int32_t first;  // index of this emitter's ray 0 in the env's flattened ray list
+  int32_t kind;   // 0 camera (half-tile sub-steps), 1 guard (whole-tile steps)
+};
+
+struct EnvParams {
+  int R, C, RC, max_steps;
+  int sr, sc, vr, vc;
+  double r_step, r_detect, r_vault;
+  int n_envs, max_cams, max_guards, max_path;
+  EnvScalars* scal;
+  uint8_t* grid;
+  Cam* cams;
+  Guard* guards;
+  uint16_t* paths;
+  const double* heading_tab;  // [(2R-1)*(2C-1)]
+  const float* plane0;        // [RC] position channel without the solver
+  const float* plane1;        // [RC] position channel value if the solver is on that cell
+  float vault_val;            // position channel value on the vault cell
+  float tile_lut[8];          // float32(tile) / 5  (environment.py:319)
+};
+
+// security.py:67 max(int(fov * 2), 30); capped at 32000 rays (fov 16000 deg) so the
+// count fits the int16 fields and a bad fov cannot blow up a launch.
+__host__ __device__ inline int num_rays_for(double fov) {
+  if (!(fov * 2 < 32000.0)) return 32000;
+  int n = (int)(fov * 2);
+  return n > 30 ? n : 30;
+}
+
+}  // namespace heist

@@ -1,0 +1,80 @@
+"""Builds libheist_hip.so (the C ABI of include/heist.h) for gfx950, in-tree.
+
+hipcc compiles each csrc/*.hip with -ffp-contract=off (the env kernels must not fuse
+multiplies into adds: the reference's raycast relies on separately rounded IEEE
+operations) and the library is linked against the HIP runtime that torch ships, so
+that torch tensors' device pointers and streams are valid inside it.
+"""
+import os
+import subprocess
+import sys
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+CSRC = os.path.join(PKG_ROOT, "csrc")
+INCLUDE = os.path.join(REPO_ROOT, "include")
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libheist_hip.so")
+BUILD_DIR = os.path.join(PKG_ROOT, "build")
+ARCH = os.environ.get("HEIST_OFFLOAD_ARCH", "gfx950")
+SOURCES = ["heist_env.hip", "heist_ppo.hip", "heist_capi.hip"]
+HEADERS = ["heist_device.h", "heist_trig.h", "heist_sincos_table.h"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
+          "--offload-arch=" + ARCH, "-I", INCLUDE, "-I", CSRC]
+
+
+def _torch_lib_dir():
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return None
+    d = os.path.join(list(spec.submodule_search_locations)[0], "lib")
+    return d if os.path.exists(os.path.join(d, "libamdhip64.so")) else None
+
+
+def _mtime(p):
+    return os.path.getmtime(p) if os.path.exists(p) else -1.0
+
+
+def needs_build():
+    if not os.path.exists(LIB_PATH):
+        return True
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(INCLUDE, "heist.h"), __file__]
+    return max(_mtime(d) for d in deps) > _mtime(LIB_PATH)
+
+
+def build(force=False, verbose=False, jobs=4):
+    if not force and not needs_build():
+        return LIB_PATH
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    procs, objs = [], []
+    for src in SOURCES:
+        obj = os.path.join(BUILD_DIR, src.replace(".hip", ".o"))
+        cmd = [HIPCC] + CFLAGS + ["-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+        objs.append(obj)
+        if len([p for _, p in procs if p.poll() is None]) >= jobs:
+            procs[0][1].wait()
+    for src, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            raise RuntimeError("hipcc failed on %s:\n%s" % (src, out.decode(errors="replace")))
+        if verbose and out:
+            print(out.decode(errors="replace"), file=sys.stderr)
+    tl = _torch_lib_dir()
+    link = ["g++", "-shared", "-o", LIB_PATH + ".tmp"] + objs
+    if tl:
+        link += ["-L" + tl, "-l:libamdhip64.so", "-Wl,-rpath," + tl]
+    else:
+        link += ["-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"]
+    r = subprocess.run(link, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("link failed:\n" + r.stdout + r.stderr)
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,93 @@
+"""ctypes binding of libheist_hip.so (include/heist.h).
+
+torch is imported first on purpose: the library is linked against the HIP runtime
+that torch ships (same soname), so torch tensors' device pointers and streams are
+valid inside it.  There is no CPU fallback: if the library or the GPU is missing,
+the calls raise.
+"""
+import ctypes
+import os
+import re
+
+import torch
+
+from . import _build
+
+_lib = None
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_i64 = ctypes.c_int64
+_d = ctypes.c_double
+_f = ctypes.c_float
+
+# name -> (restype, argtypes); pointers are passed as c_void_p (device addresses).
+SIGNATURES = {
+    "heist_abi_version": (_i, []),
+    "heist_last_error": (ctypes.c_char_p, []),
+    "heist_create": (_i, [_i, _i, _i, _i, _i, _i, _i, ctypes.POINTER(_d), _i, _i, _i, _i, ctypes.POINTER(_vp)]),
+    "heist_destroy": (_i, [_vp]),
+    "heist_set_layout": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "heist_reset": (_i, [_vp, _vp, _vp, _vp]),
+    "heist_step": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
+    "heist_export": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "heist_bfs_valid": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    "heist_cones": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
+    "heist_gae": (_i, [_vp, _vp, _vp, _vp, _i, _i, _d, _d, _vp, _vp, _vp]),
+    "heist_adv_moments": (_i, [_vp, _i64, _i, _vp, _vp]),
+    "heist_adv_apply": (_i, [_vp, _i64, _vp, _f, _vp]),
+    "heist_adv_normalize": (_i, [_vp, _i64, _vp, _f, _vp]),
+    "heist_ppo_loss": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _d, _d, _d, _vp, _vp, _vp, _vp, _vp]),
+}
+
+
+class HeistError(RuntimeError):
+    pass
+
+
+def header_functions():
+    """Function names declared in include/heist.h (the ABI contract)."""
+    with open(os.path.join(_build.INCLUDE, "heist.h")) as f:
+        txt = f.read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(heist_\w+)\s*\(", txt, re.M)))
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_build.LIB_PATH):
+            raise HeistError("libheist_hip.so is not built (%s); run __graft_entry__.build()" % _build.LIB_PATH)
+        L = ctypes.CDLL(_build.LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().heist_last_error()
+        raise HeistError("%s failed (code %d): %s" % (what, rc, msg.decode() if msg else ""))
+
+
+def ptr(t):
+    """Device address of a tensor (None -> NULL).  Tensors must be contiguous."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise HeistError("expected a device tensor, got %s" % t.device)
+    if not t.is_contiguous():
+        raise HeistError("expected a contiguous tensor")
+    return _vp(t.data_ptr())
+
+
+def stream(device=None):
+    return _vp(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_gpu(device=None):
+    if not torch.cuda.is_available():
+        raise HeistError("no HIP device: heist_amd has no CPU fallback")
+    return torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())

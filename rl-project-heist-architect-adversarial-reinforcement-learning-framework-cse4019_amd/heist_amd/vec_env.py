@@ -1,0 +1,196 @@
+"""HeistEnv -- N independent Heist environments stepped by one HIP launch.
+
+This is the batched form of the reference's HeistEnvironment (environment.py:40-426):
+set_layout / reset / step have the same semantics per env, the observation is the
+reference's get_state_tensor() stacked as [N, 3, R, C] float32, and all state stays
+in HBM.  Layout lists in the reference's dict format are packed by LayoutBatch.
+"""
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+import torch
+
+from . import _native as nat
+
+STATUS_NAMES = {0: "running", 1: "detected", 2: "vault_reached", 3: "timeout", 4: "already_done"}
+STATUS_CODES = {v: k for k, v in STATUS_NAMES.items()}
+
+Layout = Tuple[Sequence[Tuple[int, int]], Sequence[dict], Sequence[dict]]
+
+
+@dataclass
+class LayoutBatch:
+    """Padded device arrays for heist_set_layout (see include/heist.h)."""
+    wall_rc: torch.Tensor      # [N, max_walls, 2] int32
+    n_walls: torch.Tensor      # [N] int32
+    cam_params: torch.Tensor   # [N, max_cams, 6] float64
+    n_cams: torch.Tensor       # [N] int32
+    guard_paths: torch.Tensor  # [N, max_guards, max_path, 2] int32
+    guard_meta: torch.Tensor   # [N, max_guards, 3] int32
+    guard_fov: torch.Tensor    # [N, max_guards] float64
+    n_guards: torch.Tensor     # [N] int32
+    budget: torch.Tensor       # [N] int32
+
+    @property
+    def max_walls(self) -> int:
+        return int(self.wall_rc.shape[1])
+
+    @staticmethod
+    def from_lists(layouts: Sequence[Layout], budget: Union[int, Sequence[int]], max_cams: int, max_guards: int,
+                   max_path: int, device, rows: int = 64, cols: int = 64) -> "LayoutBatch":
+        n = len(layouts)
+        mw = max(1, max((len(w) for w, _, _ in layouts), default=0))
+        W = np.zeros((n, mw, 2), np.int32)
+        nw = np.zeros(n, np.int32)
+        CP = np.zeros((n, max(1, max_cams), 6), np.float64)
+        nc = np.zeros(n, np.int32)
+        GP = np.zeros((n, max(1, max_guards), max_path, 2), np.int32)
+        GM = np.zeros((n, max(1, max_guards), 3), np.int32)
+        GF = np.zeros((n, max(1, max_guards)), np.float64)
+        ng = np.zeros(n, np.int32)
+        for e, (walls, cams, guards) in enumerate(layouts):
+            if len(cams) > max_cams or len(guards) > max_guards:
+                raise ValueError("env %d: %d cameras / %d guards exceed capacity %d / %d"
+                                 % (e, len(cams), len(guards), max_cams, max_guards))
+            nw[e] = len(walls)
+            for i, (r, c) in enumerate(walls):
+                W[e, i] = (r, c)
+            nc[e] = len(cams)
+            for i, cd in enumerate(cams):  # environment.py:127-133 defaults
+                CP[e, i] = (cd["row"], cd["col"], cd.get("fov_angle", 60.0), cd.get("heading", 0.0),
+                            cd.get("rotation_speed", 15.0), cd.get("vision_range", 6))
+            ng[e] = len(guards)
+            for i, gd in enumerate(guards):  # environment.py:141-146 defaults
+                path = list(gd["patrol_path"])
+                if len(path) > max_path:
+                    raise ValueError("env %d guard %d: patrol path of %d points exceeds max_path %d"
+                                     % (e, i, len(path), max_path))
+                for k, (r, c) in enumerate(path):
+                    if not (0 <= r < rows and 0 <= c < cols):
+                        raise ValueError("env %d guard %d: patrol point %s outside the %dx%d grid"
+                                         % (e, i, (r, c), rows, cols))
+                    GP[e, i, k] = (r, c)
+                GM[e, i] = (len(path), gd.get("speed", 1), gd.get("vision_range", 4))
+                GF[e, i] = gd.get("fov_angle", 90.0)
+        b = np.broadcast_to(np.asarray(budget, np.int32), (n,)).copy()
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+        return LayoutBatch(t(W), t(nw), t(CP), t(nc), t(GP), t(GM), t(GF), t(ng), t(b))
+
+
+class HeistEnv:
+    """Batched HeistEnvironment on one HIP device.
+
+    step(actions) returns (obs, reward, done, status) as device tensors: obs [N,3,R,C]
+    float32 (get_state_tensor, environment.py:347-374), reward [N] float32, done [N]
+    bool, status [N] int8 (STATUS_NAMES).  With auto_reset=True an env that finishes is
+    reset in the same launch (headings carry over, environment.py:204-208) and its obs
+    row is the next attempt's first observation.
+    """
+
+    def __init__(self, n_envs: int, config=None, max_cams: int = 8, max_guards: int = 4, max_path: int = 16,
+                 device=None, auto_reset: bool = True):
+        from .environment import EnvironmentConfig
+        self.config = config or EnvironmentConfig()
+        cfg = self.config
+        self.device = nat.require_gpu(device)
+        self.n_envs = int(n_envs)
+        self.rows, self.cols = cfg.grid_rows, cfg.grid_cols
+        self.max_cams, self.max_guards, self.max_path = max_cams, max_guards, max_path
+        self.auto_reset = auto_reset
+        consts = (ctypes.c_double * 3)(cfg.reward_step, cfg.reward_detection, cfg.reward_vault)
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().heist_create(cfg.grid_rows, cfg.grid_cols, cfg.max_steps, cfg.start_pos[0],
+                                             cfg.start_pos[1], cfg.vault_pos[0], cfg.vault_pos[1], consts, self.n_envs,
+                                             max_cams, max_guards, max_path, ctypes.byref(h)), "heist_create")
+        self._h = h
+        kw = dict(device=self.device)
+        self.obs = torch.zeros((self.n_envs, 3, self.rows, self.cols), dtype=torch.float32, **kw)
+        self.reward = torch.zeros(self.n_envs, dtype=torch.float32, **kw)
+        self.reward64 = torch.zeros(self.n_envs, dtype=torch.float64, **kw)
+        self.done = torch.zeros(self.n_envs, dtype=torch.uint8, **kw)
+        self.status = torch.zeros(self.n_envs, dtype=torch.int8, **kw)
+        self.valid = torch.zeros(self.n_envs, dtype=torch.uint8, **kw)
+
+    # -- lifecycle ---------------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            with torch.cuda.device(self.device):
+                torch.cuda.synchronize(self.device)
+                nat.lib().heist_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self):
+        return nat.stream(self.device)
+
+    # -- layout ------------------------------------------------------------------
+    def set_layout_batch(self, lb: LayoutBatch) -> torch.Tensor:
+        """heist_set_layout on pre-packed device arrays; returns valid [N] bool."""
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().heist_set_layout(
+                self._h, lb.max_walls, nat.ptr(lb.wall_rc), nat.ptr(lb.n_walls), nat.ptr(lb.cam_params),
+                nat.ptr(lb.n_cams), nat.ptr(lb.guard_paths), nat.ptr(lb.guard_meta), nat.ptr(lb.guard_fov),
+                nat.ptr(lb.n_guards), nat.ptr(lb.budget), nat.ptr(self.valid), self._stream()), "heist_set_layout")
+        return self.valid.bool()
+
+    def set_layouts(self, layouts: Sequence[Layout], budget: Union[int, Sequence[int]] = None) -> torch.Tensor:
+        """HeistEnvironment.set_layout (environment.py:102-152) for every env."""
+        if len(layouts) != self.n_envs:
+            raise ValueError("expected %d layouts, got %d" % (self.n_envs, len(layouts)))
+        if budget is None:
+            budget = self.config.architect_budget
+        lb = LayoutBatch.from_lists(layouts, budget, self.max_cams, self.max_guards, self.max_path, self.device,
+                                    self.rows, self.cols)
+        return self.set_layout_batch(lb)
+
+    # -- episode -----------------------------------------------------------------
+    def reset(self, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """HeistEnvironment.reset + get_state_tensor for envs with mask (None: all)."""
+        m = None if mask is None else mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().heist_reset(self._h, nat.ptr(m), nat.ptr(self.obs), self._stream()), "heist_reset")
+        return self.obs
+
+    def step(self, actions: torch.Tensor, auto_reset: Optional[bool] = None, obs_out: torch.Tensor = None):
+        """HeistEnvironment.step + get_state_tensor for all envs (environment.py:216-299)."""
+        a = actions.to(device=self.device, dtype=torch.int64).contiguous()
+        ar = self.auto_reset if auto_reset is None else auto_reset
+        obs = self.obs if obs_out is None else obs_out
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().heist_step(self._h, nat.ptr(a), nat.ptr(obs), nat.ptr(self.reward),
+                                           nat.ptr(self.reward64), nat.ptr(self.done), nat.ptr(self.status),
+                                           1 if ar else 0, self._stream()), "heist_step")
+        return obs, self.reward, self.done.bool(), self.status
+
+    # -- introspection -------------------------------------------------------------
+    def export(self, grid: bool = False) -> dict:
+        """Per-env state (get_environment_state source) as device tensors."""
+        kw = dict(device=self.device)
+        sc = torch.empty((self.n_envs, 12), dtype=torch.int32, **kw)
+        ch = torch.empty((self.n_envs, max(1, self.max_cams)), dtype=torch.float64, **kw)
+        gi = torch.empty((self.n_envs, max(1, self.max_guards)), dtype=torch.int32, **kw)
+        gh = torch.empty((self.n_envs, max(1, self.max_guards)), dtype=torch.float64, **kw)
+        gr = torch.empty((self.n_envs, self.rows, self.cols), dtype=torch.int8, **kw) if grid else None
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().heist_export(self._h, nat.ptr(sc), nat.ptr(gr), nat.ptr(ch), nat.ptr(gi), nat.ptr(gh),
+                                             self._stream()), "heist_export")
+        keys = ("pos_r", "pos_c", "tick", "done", "detected", "vault_reached", "prev_dist", "initial_dist",
+                "n_cams", "n_guards", "n_walls", "spent")
+        out = {k: sc[:, i] for i, k in enumerate(keys)}
+        out.update(cam_heading=ch, guard_idx=gi, guard_heading=gh)
+        if grid:
+            out["grid"] = gr
+        return out
+
+    @property
+    def visibility(self) -> torch.Tensor:
+        """Current visibility plane [N, R, C] (obs channel 1)."""
+        return self.obs[:, 1]

@@ -1,0 +1,172 @@
+"""GPU parity of the environment path (heist_set_layout / heist_reset / heist_step /
+heist_cones / heist_bfs_valid) against the reference's golden vectors and the C oracle.
+
+Bar: bit-exact.  Integer state, visibility and the float32 observation must match
+byte for byte; the float64 reward must match exactly (reward64_out).  The golden
+vectors come from the Python reference (tests/golden/make_golden.py); the oracle
+(oracle/heist_oracle.c) is pinned to them by tests/test_oracle_golden.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_data as gd
+from oracle import pyoracle as po
+from heist_amd import EnvironmentConfig, HeistEnv
+from heist_amd.layouts import synthetic_layouts, valid_synthetic_layouts
+
+pytestmark = pytest.mark.gpu
+
+STATUS_RESET = 5
+
+
+def _cfg(tr):
+    return EnvironmentConfig(grid_rows=tr["R"], grid_cols=tr["C"], max_steps=tr["max_steps"], start_pos=tr["start"],
+                             vault_pos=tr["vault"], architect_budget=tr["budget"])
+
+
+@pytest.mark.parametrize("tr", list(gd.env_traces()), ids=lambda t: t["name"])
+def test_golden_trace_bit_exact(tr, gpu_device):
+    env = HeistEnv(1, _cfg(tr), max_cams=16, max_guards=8, max_path=64, device=gpu_device, auto_reset=False)
+    valid = env.set_layouts([(tr["walls"], tr["cams"], tr["guards"])], budget=tr["budget"])
+    assert bool(valid[0]) == tr["valid"]
+    st = env.export(grid=True)
+    np.testing.assert_array_equal(st["grid"][0].cpu().numpy(), tr["grid"])
+    acc = [int(st[k][0]) for k in ("n_walls", "n_cams", "n_guards", "spent")]
+    assert acc == tr["accepted"]
+    nc, ng = tr["accepted"][1], tr["accepted"][2]
+    for k, op in enumerate(tr["ops"]):
+        ctx = "%s op#%d" % (tr["name"], k)
+        if op == -1:
+            obs = env.reset()
+            r, d, s = 0.0, None, STATUS_RESET
+        else:
+            obs, _, dn, stt = env.step(torch.tensor([op]))
+            r, d, s = float(env.reward64[0]), bool(dn[0]), int(stt[0])
+        st = env.export()
+        assert r == tr["reward"][k], ctx
+        if d is not None:
+            assert d == tr["done"][k], ctx
+        assert s == tr["status"][k], ctx
+        assert (int(st["pos_r"][0]), int(st["pos_c"][0])) == tuple(tr["pos"][k]), ctx
+        assert int(st["tick"][0]) == tr["tick"][k], ctx
+        assert bool(st["done"][0]) == tr["done"][k], ctx
+        np.testing.assert_array_equal(st["cam_heading"][0, :nc].cpu().numpy(), tr["cam_h"][k], err_msg=ctx)
+        np.testing.assert_array_equal(st["guard_idx"][0, :ng].cpu().numpy(), tr["g_idx"][k], err_msg=ctx)
+        np.testing.assert_array_equal(st["guard_heading"][0, :ng].cpu().numpy(), tr["g_h"][k], err_msg=ctx)
+        o = obs[0].cpu().numpy()
+        np.testing.assert_array_equal(o[1] > 0.5, tr["vis"][k], err_msg=ctx)
+        if k < len(tr["state"]):
+            assert o.tobytes() == tr["state"][k].tobytes(), ctx
+
+
+def test_cones_bit_exact(gpu_device):
+    groups = {}
+    for c in gd.cones():
+        groups.setdefault((c["R"], c["C"]), []).append(c)
+    n = 0
+    for (R, C), cs in groups.items():
+        walls = torch.tensor(np.stack([c["walls"] for c in cs]).astype(np.uint8), device=gpu_device)
+        meta = torch.tensor([[1 if c["kind"] == 2 else 0, c["row"], c["col"], c["range"]] for c in cs],
+                            dtype=torch.int32, device=gpu_device)
+        par = torch.tensor([[c["fov"], c["heading"]] for c in cs], dtype=torch.float64, device=gpu_device)
+        out = torch.empty((len(cs), R, C), dtype=torch.uint8, device=gpu_device)
+        from heist_amd import _native as nat
+        nat.check(nat.lib().heist_cones(len(cs), R, C, nat.ptr(walls), nat.ptr(meta), nat.ptr(par), nat.ptr(out),
+                                        nat.stream(gpu_device)), "heist_cones")
+        got = out.bool().cpu().numpy()
+        for i, c in enumerate(cs):
+            np.testing.assert_array_equal(got[i], c["tiles"], err_msg=str((c["kind"], c["fov"], c["heading"])))
+            n += 1
+    assert n >= 1000
+
+
+def test_bfs_bit_exact(gpu_device):
+    from heist_amd.utils import bfs_valid_batch
+    groups = {}
+    for c in gd.bfs_cases():
+        key = (c["grid"].shape, c["start"], c["goal"])
+        groups.setdefault(key, []).append(c)
+    n = 0
+    for (shape, start, goal), cs in groups.items():
+        g = torch.tensor(np.stack([c["grid"] for c in cs]).astype(np.int32), device=gpu_device)
+        got = bfs_valid_batch(g, start, goal).cpu().numpy()
+        np.testing.assert_array_equal(got, np.array([c["valid"] for c in cs]))
+        n += len(cs)
+    assert n >= 1000
+
+
+def _oracle_envs(cfg, layouts, budget):
+    envs = []
+    for lay in layouts:
+        o = po.OracleEnv(cfg.grid_rows, cfg.grid_cols, cfg.max_steps, cfg.start_pos, cfg.vault_pos, budget)
+        o.set_layout(*lay)
+        o.reset()
+        envs.append(o)
+    return envs
+
+
+@pytest.mark.parametrize("R,C,budget,n,T", [(20, 20, 15, 192, 260), (32, 32, 40, 64, 120), (13, 17, 25, 64, 150)])
+def test_batched_auto_reset_vs_oracle(R, C, budget, n, T, gpu_device):
+    """Every env of a batch, with in-kernel auto-reset, equals its own oracle replay."""
+    cfg = EnvironmentConfig(grid_rows=R, grid_cols=C, max_steps=60 if R != 20 else 200)
+    env = HeistEnv(n, cfg, max_cams=16, max_guards=8, max_path=16, device=gpu_device, auto_reset=True)
+    lays = synthetic_layouts(n, R, C, budget, seed=R * 1000 + C)
+    env.set_layouts(lays, budget=budget)
+    obs = env.reset().cpu().numpy()
+    oracles = _oracle_envs(cfg, lays, budget)
+    for i, o in enumerate(oracles):
+        assert obs[i].tobytes() == o.state_tensor().tobytes()
+    rng = np.random.default_rng(7)
+    for t in range(T):
+        acts = rng.integers(0, 5, n)
+        acts[rng.random(n) < 0.4] = rng.choice([2, 4])
+        obs, rew, done, status = env.step(torch.from_numpy(acts))
+        obs, r64, done, status = (x.cpu().numpy() for x in (obs, env.reward64, done, status))
+        for i, o in enumerate(oracles):
+            r, d, s = o.step(int(acts[i]))
+            if d:
+                o.reset()
+            assert (r64[i], bool(done[i]), int(status[i])) == (r, d, s), "env %d t %d" % (i, t)
+            assert obs[i].tobytes() == o.state_tensor().tobytes(), "env %d t %d" % (i, t)
+
+
+def test_full_size_sampled_vs_oracle(gpu_device):
+    """BASELINE config size (4096 envs, 20x20): a sample of envs matches the oracle exactly
+    and batch-wide invariants hold for every env."""
+    n, R = 4096, 20
+    cfg = EnvironmentConfig()
+    env = HeistEnv(n, cfg, device=gpu_device)
+    lays = valid_synthetic_layouts(env, 15, seed=1234)
+    assert bool(env.valid.bool().all())
+    env.reset()
+    pick = np.random.default_rng(3).choice(n, 48, replace=False)
+    oracles = _oracle_envs(cfg, [lays[i] for i in pick], 15)
+    grid = env.export(grid=True)["grid"].float() / 5.0
+    g = torch.Generator(device="cpu").manual_seed(11)
+    for t in range(120):
+        acts = torch.randint(0, 5, (n,), generator=g)
+        obs, rew, done, status = env.step(acts)
+        assert torch.equal(obs[:, 0], grid)  # occupancy channel is static
+        assert bool(((obs[:, 1] == 0) | (obs[:, 1] == 1)).all())
+        o_np = obs[torch.from_numpy(pick).to(gpu_device)].cpu().numpy()
+        r64 = env.reward64.cpu().numpy()
+        for j, i in enumerate(pick):
+            r, d, s = oracles[j].step(int(acts[i]))
+            if d:
+                oracles[j].reset()
+            assert r64[i] == r
+            assert o_np[j].tobytes() == oracles[j].state_tensor().tobytes()
+
+
+def test_step_after_done_without_auto_reset(gpu_device):
+    cfg = EnvironmentConfig(grid_rows=6, grid_cols=6, max_steps=3)
+    env = HeistEnv(2, cfg, device=gpu_device, auto_reset=False)
+    env.set_layouts([([], [], []), ([], [], [])])
+    env.reset()
+    for _ in range(3):
+        env.step(torch.zeros(2, dtype=torch.int64))
+    obs_before = env.obs.clone()
+    _, rew, done, status = env.step(torch.zeros(2, dtype=torch.int64))
+    assert bool(done.all()) and (status == 4).all() and float(rew.abs().sum()) == 0.0
+    assert torch.equal(env.obs, obs_before)

@@ -1,0 +1,33 @@
+#!/bin/bash
+# One GPU-box session: build check, GPU parity tests, smoke, bench, rocprof kernel trace.
+# Each GPU step has its own time limit; a fault-like exit (abort, segfault, timeout)
+# ends the script immediately -- no GPU work after a fault.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+OUT=gpurun_out/${TAG:-run}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+step() {  # step NAME SECONDS CMD...
+  local name=$1 secs=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 5 "$OUT/$name.log"
+  if fatal $rc; then echo "FATAL exit in $name; stopping"; exit $rc; fi
+  return 0
+}
+rocm-smi --showproductname > "$OUT/gpu.txt" 2>&1 || true
+nproc > "$OUT/nproc.txt"; lscpu > "$OUT/lscpu.txt" 2>&1
+for s in ${STEPS:-pytest smoke bench prof}; do
+  case $s in
+    pytest) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    pytestall) step pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py ;;
+    prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o heist --output-format csv -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline ;;
+    pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline
+         step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline ;;
+  esac
+done
+echo "== all done"

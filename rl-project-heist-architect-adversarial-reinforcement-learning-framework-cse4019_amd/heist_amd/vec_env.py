@@ -139,7 +139,7 @@ class HeistEnv:
                 self._h, lb.max_walls, nat.ptr(lb.wall_rc), nat.ptr(lb.n_walls), nat.ptr(lb.cam_params),
                 nat.ptr(lb.n_cams), nat.ptr(lb.guard_paths), nat.ptr(lb.guard_meta), nat.ptr(lb.guard_fov),
                 nat.ptr(lb.n_guards), nat.ptr(lb.budget), nat.ptr(self.valid), self._stream()), "heist_set_layout")
-        return self.valid.bool()
+        return self.valid.view(torch.bool)
 
     def set_layouts(self, layouts: Sequence[Layout], budget: Union[int, Sequence[int]] = None) -> torch.Tensor:
         """HeistEnvironment.set_layout (environment.py:102-152) for every env."""
@@ -168,7 +168,7 @@ class HeistEnv:
             nat.check(nat.lib().heist_step(self._h, nat.ptr(a), nat.ptr(obs), nat.ptr(self.reward),
                                            nat.ptr(self.reward64), nat.ptr(self.done), nat.ptr(self.status),
                                            1 if ar else 0, self._stream()), "heist_step")
-        return obs, self.reward, self.done.bool(), self.status
+        return obs, self.reward, self.done.view(torch.bool), self.status
 
     # -- introspection -------------------------------------------------------------
     def export(self, grid: bool = False) -> dict:

@@ -1,6 +1,7 @@
 // heist_capi.hip -- extern "C" entry points of libheist_hip.so (declared in include/heist.h).
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -142,6 +143,18 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
       planes[(size_t)R * C + (size_t)r * C + c] = 1.0f + g;
     }
   p.vault_val = -1.0f + (float)(-0.3 * (0.0 / (double)(R + C)));
+  {  // axis-aligned guard moves: heading depends only on the direction
+    const int W2 = 2 * C - 1;
+    p.axis_heading[0] = htab[(size_t)(-1 + R - 1) * W2 + (C - 1)];
+    p.axis_heading[1] = htab[(size_t)(1 + R - 1) * W2 + (C - 1)];
+    p.axis_heading[2] = htab[(size_t)(R - 1) * W2 + (-1 + C - 1)];
+    p.axis_heading[3] = htab[(size_t)(R - 1) * W2 + (1 + C - 1)];
+  }
+  p.step_waves = 2;
+  if (const char* w = getenv("HEIST_STEP_WAVES")) {
+    const int v = atoi(w);
+    if (v == 1 || v == 2 || v == 4) p.step_waves = v;
+  }
   for (int k = 0; k < 8; ++k) p.tile_lut[k] = k <= 5 ? (float)k / 5.0f : 0.0f;  // environment.py:319
 
   const size_t sizes[] = {

@@ -36,10 +36,16 @@ static_assert(sizeof(Cam) == 32, "Cam layout");
 
 struct Guard {
   double fov, heading;
-  int32_t idx, speed;
-  int16_t len, range, num_rays, pad;
+  int16_t idx;       // current_idx
+  int16_t step;      // speed mod len (Python %), so idx' = (idx + step) % len
+  int16_t len, range, num_rays;
+  uint16_t pos;      // patrol_path[idx] packed row | col << 8
+  uint16_t pos0;     // patrol_path[0]
+  int16_t pad;
 };
 static_assert(sizeof(Guard) == 32, "Guard layout");
+
+__host__ __device__ inline int pack_rc(int r, int c) { return r | (c << 8); }
 
 // One ray emitter as the raycaster sees it (a camera or a guard at its current pose).
 struct Emit {
@@ -65,6 +71,8 @@ struct EnvParams {
   const float* plane1;        // [RC] position channel value if the solver is on that cell
   float vault_val;            // position channel value on the vault cell
   float tile_lut[8];          // float32(tile) / 5  (environment.py:319)
+  double axis_heading[4];     // heading_tab at (dr,dc) = (-1,0), (1,0), (0,-1), (0,1)
+  int step_waves;             // wavefronts per env in step/reset (1, 2 or 4)
 };
 
 // security.py:67 max(int(fov * 2), 30); capped at 32000 rays (fov 16000 deg) so the

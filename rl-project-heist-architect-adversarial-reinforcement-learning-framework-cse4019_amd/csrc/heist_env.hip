@@ -1,13 +1,15 @@
 // heist_env.hip -- CDNA4 kernels for the batched Heist environment.
 //
-// One 64-lane wavefront (= one workgroup) owns one environment:
-//   * the env's tile grid and its visibility plane live in LDS as bytes;
-//   * cameras and guards are flattened into one ray list; lane l casts rays
-//     l, l+64, ... (security.py:53-101, :161-192) and marks visible tiles with
-//     idempotent byte stores (no atomics);
-//   * the solver/reward logic (environment.py:216-299) runs wave-uniform;
-//   * the [3][R][C] float32 observation (environment.py:347-374) leaves in
-//     16-byte coalesced stores.
+// step/reset: one workgroup of W wavefronts (W = 1, 2, 4) owns one environment.
+//   * Prefetch first: the env's tile grid, guard paths and the glibc sin/cos table
+//     go to LDS, cameras/guards and the observation's static position plane to
+//     registers -- all issued together, so the env costs one HBM round trip.
+//   * Cameras and guards are updated in registers (no store -> reload) and flattened
+//     into one ray list; thread t casts rays t, t + 64W, ... (security.py:53-101,
+//     :161-192) with the samples of a ray computed in blocks of four so the wall
+//     lookups in LDS overlap; visible tiles are idempotent byte stores (no atomics).
+//   * The solver/reward logic (environment.py:216-299) runs block-uniform; the
+//     [3][R][C] float32 observation (environment.py:347-374) leaves in 16-byte stores.
 // Arithmetic follows the reference's IEEE double semantics exactly: no FMA
 // contraction, half-to-even rint(), glibc-exact sin/cos (heist_trig.h).
 #include "heist_device.h"
@@ -18,10 +20,13 @@
 namespace heist {
 
 __constant__ double kSinCosTab[4 * HEIST_SINCOS_TAB_ROWS] = HEIST_SINCOS_TAB_INIT;
+constexpr int kTabDoubles = 4 * HEIST_SINCOS_TAB_ROWS;
 __constant__ int kActDR[5] = {0, -1, 1, 0, 0};  // environment.py:52-58
 __constant__ int kActDC[5] = {0, 0, 0, -1, 1};
 
 __device__ __forceinline__ int iabs_(int a) { return a < 0 ? -a : a; }
+__device__ __forceinline__ int unpack_r(uint16_t v) { return v & 0xff; }
+__device__ __forceinline__ int unpack_c(uint16_t v) { return v >> 8; }
 
 // Python float % 360.0 (floatobject.c float_rem: remainder takes the divisor's sign).
 __device__ __forceinline__ double py_mod360(double x) {
@@ -34,31 +39,37 @@ __device__ __forceinline__ double py_mod360(double x) {
   return r;
 }
 
-__device__ __forceinline__ int py_imod(int a, int m) {
-  int r = a % m;
-  return (r != 0 && ((r < 0) != (m < 0))) ? r + m : r;
-}
-
-// Dynamic LDS carve-up for one env: grid bytes, visibility bytes, emitter table.
-struct EnvLds {
-  uint8_t* grid;
-  uint8_t* vis;
-  Emit* em;
-  int* meta;  // [0] = number of emitters, [1] = total rays
-};
-
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
-__host__ inline size_t env_lds_bytes(int RC, int n_emit) {
-  return align16(RC) * 2 + align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) + 16;
+// ---------------------------------------------------------------------------
+// LDS carve-up for one env
+// ---------------------------------------------------------------------------
+
+struct EnvLds {
+  double* tab;     // [440] glibc sin/cos table
+  uint8_t* grid;   // [RC]
+  uint8_t* vis;    // [RC]
+  Emit* em;        // [n_emit]
+  uint16_t* path;  // [max_guards][max_path]
+  float* plane;    // [RC] static position channel (plane0)
+  int* meta;       // [0] emitters, [1] total rays
+};
+
+__host__ __device__ inline size_t env_lds_bytes(int RC, int n_emit, int path_words) {
+  return align16(sizeof(double) * kTabDoubles) + 2 * align16(RC) + align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) +
+         align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1)) + align16(sizeof(float) * RC) + 16;
 }
 
-__device__ __forceinline__ EnvLds carve(unsigned char* smem, int RC, int n_emit) {
+__device__ __forceinline__ EnvLds carve(unsigned char* smem, int RC, int n_emit, int path_words) {
   EnvLds L;
-  L.grid = smem;
-  L.vis = smem + align16(RC);
-  L.em = reinterpret_cast<Emit*>(smem + 2 * align16(RC));
-  L.meta = reinterpret_cast<int*>(smem + 2 * align16(RC) + align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)));
+  size_t o = 0;
+  L.tab = reinterpret_cast<double*>(smem + o); o += align16(sizeof(double) * kTabDoubles);
+  L.grid = smem + o; o += align16(RC);
+  L.vis = smem + o; o += align16(RC);
+  L.em = reinterpret_cast<Emit*>(smem + o); o += align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1));
+  L.path = reinterpret_cast<uint16_t*>(smem + o); o += align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1));
+  L.plane = reinterpret_cast<float*>(smem + o); o += align16(sizeof(float) * RC);
+  L.meta = reinterpret_cast<int*>(smem + o);
   return L;
 }
 
@@ -71,39 +82,55 @@ __device__ __forceinline__ EnvLds carve(unsigned char* smem, int RC, int n_emit)
 // duplicated integer samples of security.py:78-82 are idempotent and skipped); guard
 // rays sample dist = 1..range.  A wall or the grid edge ends the ray; the emitter's own
 // tile is never marked by its rays.
+template <int NT>
 __device__ void cast_rays(const EnvLds& L, int R, int C) {
-  const int lane = threadIdx.x & 63;
   const int n_em = L.meta[0];
   const int total = L.meta[1];
   int k = 0;
-  for (int j = lane; j < total; j += 64) {
+  for (int j = threadIdx.x; j < total; j += NT) {
     while (k + 1 < n_em && L.em[k + 1].first <= j) ++k;
     const Emit E = L.em[k];
     const int i = j - E.first;
     const double angle = E.hmh + (E.fov * (double)i) / (double)E.num_rays;  // security.py:70
     const double rad = angle * kDegToRad;                                   // math.radians
-    const double dx = heist_trig::cos(rad, kSinCosTab);
-    const double dy = -heist_trig::sin(rad, kSinCosTab);
+    const double dx = heist_trig::cos(rad, L.tab);
+    const double dy = -heist_trig::sin(rad, L.tab);
     const double stride = E.kind == 0 ? 0.5 : 1.0;
     const int n_samp = E.kind == 0 ? 2 * E.range : E.range;
     const double col = (double)E.col, row = (double)E.row;
-    for (int s = 1; s <= n_samp; ++s) {
-      const double dist = stride * (double)s;  // exact
-      const double fx = col + dx * dist;
-      const double fy = row + dy * dist;
-      const int c = (int)rint(fx);  // Python round(): half to even
-      const int r = (int)rint(fy);
-      if ((unsigned)r >= (unsigned)R || (unsigned)c >= (unsigned)C) break;
-      const int cell = r * C + c;
-      if (L.grid[cell] == kWall) break;
-      if (r != E.row || c != E.col) L.vis[cell] = 1;
+    for (int s0 = 1; s0 <= n_samp; s0 += 4) {
+      int cell[4];
+      bool own[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double dist = stride * (double)(s0 + u);  // exact
+        const double fx = col + dx * dist;
+        const double fy = row + dy * dist;
+        const int c = (int)rint(fx);  // Python round(): half to even
+        const int r = (int)rint(fy);
+        const bool in = s0 + u <= n_samp && (unsigned)r < (unsigned)R && (unsigned)c < (unsigned)C;
+        cell[u] = in ? r * C + c : -1;
+        own[u] = r == E.row && c == E.col;
+      }
+      int w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) w[u] = cell[u] >= 0 ? (int)L.grid[cell[u]] : kWall;
+      bool stop = false;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (!stop) {
+          if (w[u] == kWall) stop = true;
+          else if (!own[u]) L.vis[cell[u]] = 1;
+        }
+      }
+      if (stop) break;
     }
   }
 }
 
-// Lane 0 turns per-emitter ray counts into the flattened ray index (call between barriers).
+// One thread turns per-emitter ray counts into the flattened ray index.
 __device__ __forceinline__ void index_rays(const EnvLds& L, int n_em) {
-  if ((threadIdx.x & 63) == 0) {
+  if (threadIdx.x == 0) {
     int t = 0;
     for (int k = 0; k < n_em; ++k) {
       L.em[k].first = t;
@@ -114,115 +141,147 @@ __device__ __forceinline__ void index_rays(const EnvLds& L, int n_em) {
   }
 }
 
-__device__ __forceinline__ void guard_pos(const EnvParams& p, int e, int g, int idx, int* r, int* c) {
-  const uint16_t pt = p.paths[((size_t)e * p.max_guards + g) * p.max_path + idx];
-  *r = pt & 0xff;
-  *c = pt >> 8;
+__device__ __forceinline__ Emit cam_emit(const Cam& cm) {
+  Emit E;
+  E.hmh = cm.heading - cm.fov / 2.0;  // security.py:64, :70
+  E.fov = cm.fov;
+  E.row = cm.row; E.col = cm.col; E.range = cm.range; E.num_rays = cm.num_rays;
+  E.first = 0; E.kind = 0;
+  return E;
 }
 
-// Build the emitter table from the env's cameras and guards at their current pose.
-// Lanes [0, n_cams) take cameras, [n_cams, n_cams + n_guards) guards.
-__device__ __forceinline__ void build_emitters(const EnvParams& p, int e, const EnvScalars& s, const EnvLds& L) {
-  const int lane = threadIdx.x & 63;
-  if (lane < s.n_cams) {
-    const Cam cm = p.cams[(size_t)e * p.max_cams + lane];
-    Emit E;
-    E.hmh = cm.heading - cm.fov / 2.0;
-    E.fov = cm.fov;
-    E.row = cm.row; E.col = cm.col; E.range = cm.range; E.num_rays = cm.num_rays;
-    E.first = 0; E.kind = 0;
-    L.em[lane] = E;
-  } else if (lane < s.n_cams + s.n_guards) {
-    const int g = lane - s.n_cams;
-    const Guard gd = p.guards[(size_t)e * p.max_guards + g];
-    int r, c;
-    guard_pos(p, e, g, gd.idx, &r, &c);
-    Emit E;
-    E.hmh = gd.heading - gd.fov / 2.0;
-    E.fov = gd.fov;
-    E.row = r; E.col = c; E.range = gd.range; E.num_rays = gd.num_rays;
-    E.first = 0; E.kind = 1;
-    L.em[lane] = E;
-  }
+__device__ __forceinline__ Emit guard_emit(const Guard& gd) {
+  Emit E;
+  E.hmh = gd.heading - gd.fov / 2.0;
+  E.fov = gd.fov;
+  E.row = unpack_r(gd.pos); E.col = unpack_c(gd.pos); E.range = gd.range; E.num_rays = gd.num_rays;
+  E.first = 0; E.kind = 1;
+  return E;
 }
 
-// Full visibility recompute (visibility.py:31-65) for the env's current pose.
-// Must be entered by the whole (single-wave) workgroup.
-__device__ __forceinline__ void compute_visibility(const EnvParams& p, int e, const EnvScalars& s, const EnvLds& L) {
-  const int lane = threadIdx.x & 63;
-  for (int i = lane; i < p.RC; i += 64) L.vis[i] = 0;
-  build_emitters(p, e, s, L);
+// Visibility (visibility.py:31-65) once the emitter table is in LDS and vis is zeroed.
+template <int NT>
+__device__ __forceinline__ void raycast_pass(const EnvParams& p, const EnvLds& L, int n_em, int n_cams) {
   __syncthreads();
-  index_rays(L, s.n_cams + s.n_guards);
+  index_rays(L, n_em);
   __syncthreads();
-  cast_rays(L, p.R, p.C);
+  cast_rays<NT>(L, p.R, p.C);
   __syncthreads();
-  if (lane >= s.n_cams && lane < s.n_cams + s.n_guards) {  // a guard's own tile (visibility.py:59)
-    const Emit E = L.em[lane];
+  const int t = threadIdx.x;
+  if (t >= n_cams && t < n_em) {  // a guard's own tile (visibility.py:59)
+    const Emit E = L.em[t];
     L.vis[E.row * p.C + E.col] = 1;
   }
   __syncthreads();
 }
 
-__device__ __forceinline__ void load_grid(const EnvParams& p, int e, const EnvLds& L) {
-  const int lane = threadIdx.x & 63;
+template <int NT>
+__device__ __forceinline__ void clear_vis(const EnvParams& p, const EnvLds& L) {
+  uint32_t* v4 = reinterpret_cast<uint32_t*>(L.vis);
+  for (int i = threadIdx.x; i < (p.RC + 3) / 4; i += NT) v4[i] = 0u;
+}
+
+// ---------------------------------------------------------------------------
+// Prefetch / observation
+// ---------------------------------------------------------------------------
+
+// A camera or a guard as two 16-byte register loads; the destination is fixed and the
+// type is chosen afterwards by bit-cast (selecting a destination struct member instead
+// would defeat SROA and put the whole prefetch in scratch).
+struct EmitterRaw {
+  uint4 a, b;
+};
+static_assert(sizeof(EmitterRaw) == sizeof(Cam) && sizeof(EmitterRaw) == sizeof(Guard), "emitter records");
+
+__device__ __forceinline__ Cam as_cam(const EmitterRaw& r) { return __builtin_bit_cast(Cam, r); }
+__device__ __forceinline__ Guard as_guard(const EmitterRaw& r) { return __builtin_bit_cast(Guard, r); }
+
+// Issue every per-env HBM read before the first barrier: sin/cos table, grid, guard
+// paths and the static position plane into LDS; this thread's camera/guard record into
+// registers.  EnvScalars come in through scalar loads.
+template <int NT>
+__device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds& L, int n_cams, int n_em,
+                                         EmitterRaw& raw) {
+  const int t = threadIdx.x;
+  const double2* tab2 = reinterpret_cast<const double2*>(kSinCosTab);
+  double2* ltab2 = reinterpret_cast<double2*>(L.tab);
+  for (int i = t; i < kTabDoubles / 2; i += NT) ltab2[i] = tab2[i];
   const uint8_t* src = p.grid + (size_t)e * p.RC;
   if ((p.RC & 3) == 0) {
     const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
     uint32_t* d4 = reinterpret_cast<uint32_t*>(L.grid);
-    for (int i = lane; i < p.RC / 4; i += 64) d4[i] = s4[i];
+    for (int i = t; i < p.RC / 4; i += NT) d4[i] = s4[i];
   } else {
-    for (int i = lane; i < p.RC; i += 64) L.grid[i] = src[i];
+    for (int i = t; i < p.RC; i += NT) L.grid[i] = src[i];
+  }
+  const int pw = p.max_guards * p.max_path;
+  const uint16_t* ps = p.paths + (size_t)e * pw;
+  for (int i = t; i < pw; i += NT) L.path[i] = ps[i];
+  raw.a = make_uint4(0u, 0u, 0u, 0u);
+  raw.b = raw.a;
+  if (t < n_em) {
+    const uint4* rs = t < n_cams ? reinterpret_cast<const uint4*>(p.cams + (size_t)e * p.max_cams + t)
+                                 : reinterpret_cast<const uint4*>(p.guards + (size_t)e * p.max_guards + (t - n_cams));
+    raw.a = rs[0];
+    raw.b = rs[1];
+  }
+  if ((p.RC & 3) == 0) {
+    const float4* pl0 = reinterpret_cast<const float4*>(p.plane0);
+    float4* lp = reinterpret_cast<float4*>(L.plane);
+    for (int i = t; i < p.RC / 4; i += NT) lp[i] = pl0[i];
+  } else {
+    for (int i = t; i < p.RC; i += NT) L.plane[i] = p.plane0[i];
   }
 }
 
+// Set lane m (0..3) of v; m outside 0..3 leaves v unchanged (no dynamic indexing:
+// that would put the vector in scratch).
+__device__ __forceinline__ void patch4(float4& v, int m, float val) {
+  if (m == 0) v.x = val;
+  else if (m == 1) v.y = val;
+  else if (m == 2) v.z = val;
+  else if (m == 3) v.w = val;
+}
+
 // Observation row [3][R][C] (environment.py:347-374): occupancy / 5, visibility, and the
-// position channel (static planes with the solver and vault cells patched).
+// position channel (static plane with the solver and vault cells patched; the vault
+// wins if the solver stands on it).
+template <int NT>
 __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvScalars& s, const EnvLds& L,
                                           float* __restrict__ obs) {
-  const int lane = threadIdx.x & 63;
+  const int t = threadIdx.x;
   const int RC = p.RC;
   float* o = obs + (size_t)e * 3 * RC;
   const int solver = s.pos_r * p.C + s.pos_c;
   const int vault = p.vr * p.C + p.vc;
+  const float sv = p.plane1[solver];
   if ((RC & 3) == 0) {
-    const int n4 = 3 * RC / 4;
-    for (int q = lane; q < n4; q += 64) {
-      const int o4 = q * 4;
-      const int ch = o4 / RC;
-      const int cell = o4 - ch * RC;
-      float4 v;
-      if (ch == 0) {
-        const uint32_t b = *reinterpret_cast<const uint32_t*>(L.grid + cell);
-        v.x = p.tile_lut[b & 7]; v.y = p.tile_lut[(b >> 8) & 7];
-        v.z = p.tile_lut[(b >> 16) & 7]; v.w = p.tile_lut[(b >> 24) & 7];
-      } else if (ch == 1) {
-        const uint32_t b = *reinterpret_cast<const uint32_t*>(L.vis + cell);
-        v.x = (b & 0xff) ? 1.0f : 0.0f; v.y = (b & 0xff00) ? 1.0f : 0.0f;
-        v.z = (b & 0xff0000) ? 1.0f : 0.0f; v.w = (b & 0xff000000u) ? 1.0f : 0.0f;
-      } else {
-        v = *reinterpret_cast<const float4*>(p.plane0 + cell);
-        if ((unsigned)(solver - cell) < 4u) {
-          const int k = solver - cell;
-          const float sv = p.plane1[solver];
-          if (k == 0) v.x = sv; else if (k == 1) v.y = sv; else if (k == 2) v.z = sv; else v.w = sv;
-        }
-        if ((unsigned)(vault - cell) < 4u) {  // vault wins if the solver stands on it
-          const int k = vault - cell;
-          if (k == 0) v.x = p.vault_val; else if (k == 1) v.y = p.vault_val;
-          else if (k == 2) v.z = p.vault_val; else v.w = p.vault_val;
-        }
-      }
-      *reinterpret_cast<float4*>(o + o4) = v;
+    const int n4 = RC / 4;
+    float4* o0 = reinterpret_cast<float4*>(o);
+    float4* o1 = o0 + n4;
+    float4* o2 = o1 + n4;
+    for (int q = t; q < n4; q += NT) {
+      const uint32_t b = *reinterpret_cast<const uint32_t*>(L.grid + 4 * q);
+      o0[q] = make_float4(p.tile_lut[b & 7], p.tile_lut[(b >> 8) & 7], p.tile_lut[(b >> 16) & 7],
+                          p.tile_lut[(b >> 24) & 7]);
+      const uint32_t v = *reinterpret_cast<const uint32_t*>(L.vis + 4 * q);
+      o1[q] = make_float4((v & 0xff) ? 1.0f : 0.0f, (v & 0xff00) ? 1.0f : 0.0f, (v & 0xff0000) ? 1.0f : 0.0f,
+                          (v & 0xff000000u) ? 1.0f : 0.0f);
+    }
+    for (int q = t; q < n4; q += NT) {
+      float4 v = reinterpret_cast<const float4*>(L.plane)[q];
+      patch4(v, solver - 4 * q, sv);
+      patch4(v, vault - 4 * q, p.vault_val);
+      o2[q] = v;
     }
   } else {
-    for (int q = lane; q < 3 * RC; q += 64) {
+    for (int q = t; q < 3 * RC; q += NT) {
       const int ch = q / RC;
       const int cell = q - ch * RC;
       float v;
       if (ch == 0) v = p.tile_lut[L.grid[cell] & 7];
       else if (ch == 1) v = L.vis[cell] ? 1.0f : 0.0f;
-      else v = cell == vault ? p.vault_val : (cell == solver ? p.plane1[cell] : p.plane0[cell]);
+      else v = cell == vault ? p.vault_val : (cell == solver ? sv : L.plane[cell]);
       o[q] = v;
     }
   }
@@ -234,64 +293,75 @@ __device__ __forceinline__ void reset_solver(const EnvParams& p, EnvScalars& s) 
   s.prev_dist = s.initial_dist = iabs_(p.sr - p.vr) + iabs_(p.sc - p.vc);
 }
 
-// Same lane -> guard mapping as build_emitters, so each lane re-reads only its own store.
-__device__ __forceinline__ void reset_guards(const EnvParams& p, int e, const EnvScalars& s) {
-  const int lane = threadIdx.x & 63;
-  if (lane >= s.n_cams && lane < s.n_cams + s.n_guards)
-    p.guards[(size_t)e * p.max_guards + (lane - s.n_cams)].idx = 0;  // headings carry over
+__device__ __forceinline__ double guard_heading_after(const EnvParams& p, int dr, int dc, double cur) {
+  if (dr == 0 && dc == 0) return cur;  // security.py:158: heading only changes if it moved
+  if (dc == 0) return dr < 0 ? p.axis_heading[0] : p.axis_heading[1];
+  if (dr == 0) return dc < 0 ? p.axis_heading[2] : p.axis_heading[3];
+  return p.heading_tab[(dr + p.R - 1) * (2 * p.C - 1) + (dc + p.C - 1)];
 }
 
 // ---------------------------------------------------------------------------
 // step / reset
 // ---------------------------------------------------------------------------
 
-__global__ __launch_bounds__(64) void step_kernel(EnvParams p, const int64_t* __restrict__ actions,
-                                                   float* __restrict__ obs, float* __restrict__ rew,
-                                                   double* __restrict__ rew64, uint8_t* __restrict__ done_out,
-                                                   int8_t* __restrict__ status_out, int auto_reset) {
+template <int W>
+__global__ __launch_bounds__(64 * W) void step_kernel(EnvParams p, const int64_t* __restrict__ actions,
+                                                       float* __restrict__ obs, float* __restrict__ rew,
+                                                       double* __restrict__ rew64, uint8_t* __restrict__ done_out,
+                                                       int8_t* __restrict__ status_out, int auto_reset) {
+  constexpr int NT = 64 * W;
   extern __shared__ __align__(16) unsigned char smem[];
   const int e = blockIdx.x;
-  const int lane = threadIdx.x;
-  const EnvLds L = carve(smem, p.RC, p.max_cams + p.max_guards);
-  load_grid(p, e, L);
+  const int t = threadIdx.x;
+  const EnvLds L = carve(smem, p.RC, p.max_cams + p.max_guards, p.max_guards * p.max_path);
   EnvScalars s = p.scal[e];
+  const int n_cams = s.n_cams, n_em = s.n_cams + s.n_guards;
+  EmitterRaw raw;
+  prefetch<NT>(p, e, L, n_cams, n_em, raw);
+  const int a_raw = (int)actions[e];
+  clear_vis<NT>(p, L);
   const bool act = !s.done;
-  __syncthreads();
+  __syncthreads();  // grid, paths, table in LDS
 
   double reward = 0.0;
   int status = kAlreadyDone;
   if (act) {
     // 1. move (environment.py:239-246)
-    int a = (int)actions[e];
-    if (a < 0 || a > 4) a = 0;
+    const int a = (a_raw < 0 || a_raw > 4) ? 0 : a_raw;
     const int nr = s.pos_r + kActDR[a], nc = s.pos_c + kActDC[a];
     if (nr >= 0 && nr < p.R && nc >= 0 && nc < p.C && L.grid[nr * p.C + nc] != kWall) {
       s.pos_r = nr;
       s.pos_c = nc;
     }
-    // 2. cameras rotate, guards patrol (security.py:49-51, :145-159)
-    if (lane < s.n_cams) {
-      Cam* cm = p.cams + (size_t)e * p.max_cams + lane;
-      cm->heading = py_mod360(cm->heading + cm->speed * 1.0);
-    } else if (lane < s.n_cams + s.n_guards) {
-      const int g = lane - s.n_cams;
-      Guard* gd = p.guards + (size_t)e * p.max_guards + g;
-      const int len = gd->len;
-      if (len >= 2) {
-        const int old = gd->idx;
-        const int nidx = py_imod(old + gd->speed * 1, len);
-        int r0, c0, r1, c1;
-        guard_pos(p, e, g, old, &r0, &c0);
-        guard_pos(p, e, g, nidx, &r1, &c1);
-        const int dr = r1 - r0, dc = c1 - c0;
-        if (dr != 0 || dc != 0) gd->heading = p.heading_tab[(dr + p.R - 1) * (2 * p.C - 1) + (dc + p.C - 1)];
-        gd->idx = nidx;
-      }
-    }
   }
-  __syncthreads();
+  // 2. cameras rotate, guards patrol (security.py:49-51, :145-159) -- in registers
+  Guard gd = as_guard(raw);  // meaningful on guard threads only
+  if (t < n_cams) {
+    Cam cm = as_cam(raw);
+    if (act) {
+      cm.heading = py_mod360(cm.heading + cm.speed * 1.0);
+      p.cams[(size_t)e * p.max_cams + t].heading = cm.heading;
+    }
+    L.em[t] = cam_emit(cm);
+  } else if (t < n_em) {
+    const int g = t - n_cams;
+    if (act && gd.len >= 2) {
+      int nidx = gd.idx + gd.step;
+      if (nidx >= gd.len) nidx -= gd.len;
+      const uint16_t np = L.path[g * p.max_path + nidx];
+      gd.heading = guard_heading_after(p, unpack_r(np) - unpack_r(gd.pos), unpack_c(np) - unpack_c(gd.pos),
+                                       gd.heading);
+      gd.idx = (int16_t)nidx;
+      gd.pos = np;
+      Guard* gp = p.guards + (size_t)e * p.max_guards + g;
+      gp->heading = gd.heading;
+      gp->idx = gd.idx;
+      gp->pos = gd.pos;
+    }
+    L.em[t] = guard_emit(gd);
+  }
   // 3. visibility (environment.py:257-258); an already-done env recomputes the same plane
-  compute_visibility(p, e, s, L);
+  raycast_pass<NT>(p, L, n_em, n_cams);
 
   if (act) {
     // 4-5. shaping, detection, vault, timeout (environment.py:235, :261-297)
@@ -323,14 +393,21 @@ __global__ __launch_bounds__(64) void step_kernel(EnvParams p, const int64_t* __
     }
   }
   const int done_now = s.done;
-  if (auto_reset && done_now) {  // wave-uniform: the barriers inside are safe
+  if (auto_reset && done_now) {  // block-uniform: the barriers inside are safe
     reset_solver(p, s);
-    reset_guards(p, e, s);
-    __syncthreads();
-    compute_visibility(p, e, s, L);
+    if (t >= n_cams && t < n_em) {  // guards back to patrol point 0, headings carry over (environment.py:204-208)
+      gd.idx = 0;
+      gd.pos = gd.pos0;
+      Guard* gp = p.guards + (size_t)e * p.max_guards + (t - n_cams);
+      gp->idx = 0;
+      gp->pos = gd.pos0;
+      L.em[t] = guard_emit(gd);
+    }
+    clear_vis<NT>(p, L);
+    raycast_pass<NT>(p, L, n_em, n_cams);
   }
-  write_obs(p, e, s, L, obs);
-  if (lane == 0) {
+  write_obs<NT>(p, e, s, L, obs);
+  if (t == 0) {
     rew[e] = (float)reward;
     if (rew64) rew64[e] = reward;
     done_out[e] = (uint8_t)done_now;
@@ -339,20 +416,35 @@ __global__ __launch_bounds__(64) void step_kernel(EnvParams p, const int64_t* __
   }
 }
 
-__global__ __launch_bounds__(64) void reset_kernel(EnvParams p, const uint8_t* __restrict__ mask,
-                                                    float* __restrict__ obs) {
+template <int W>
+__global__ __launch_bounds__(64 * W) void reset_kernel(EnvParams p, const uint8_t* __restrict__ mask,
+                                                        float* __restrict__ obs) {
+  constexpr int NT = 64 * W;
   extern __shared__ __align__(16) unsigned char smem[];
   const int e = blockIdx.x;
+  const int t = threadIdx.x;
   if (mask && !mask[e]) return;
-  const EnvLds L = carve(smem, p.RC, p.max_cams + p.max_guards);
-  load_grid(p, e, L);
+  const EnvLds L = carve(smem, p.RC, p.max_cams + p.max_guards, p.max_guards * p.max_path);
   EnvScalars s = p.scal[e];
+  const int n_cams = s.n_cams, n_em = s.n_cams + s.n_guards;
+  EmitterRaw raw;
+  prefetch<NT>(p, e, L, n_cams, n_em, raw);
+  clear_vis<NT>(p, L);
   reset_solver(p, s);
-  reset_guards(p, e, s);
-  __syncthreads();
-  compute_visibility(p, e, s, L);
-  write_obs(p, e, s, L, obs);
-  if (threadIdx.x == 0) p.scal[e] = s;
+  if (t < n_cams) {
+    L.em[t] = cam_emit(as_cam(raw));
+  } else if (t < n_em) {
+    Guard gd = as_guard(raw);
+    gd.idx = 0;
+    gd.pos = gd.pos0;
+    Guard* gp = p.guards + (size_t)e * p.max_guards + (t - n_cams);
+    gp->idx = 0;
+    gp->pos = gd.pos0;
+    L.em[t] = guard_emit(gd);
+  }
+  raycast_pass<NT>(p, L, n_em, n_cams);
+  write_obs<NT>(p, e, s, L, obs);
+  if (t == 0) p.scal[e] = s;
 }
 
 // ---------------------------------------------------------------------------
@@ -380,15 +472,6 @@ __device__ bool bfs_wave(uint64_t pass, int sr, int sc, int gr, int gc) {
   return false;
 }
 
-__device__ __forceinline__ uint64_t row_pass_mask(const uint8_t* g, int R, int C) {
-  const int lane = threadIdx.x & 63;
-  uint64_t m = 0;
-  if (lane < R)
-    for (int c = 0; c < C; ++c)
-      if (g[lane * C + c] != kWall) m |= 1ull << c;
-  return m;
-}
-
 __global__ __launch_bounds__(64) void set_layout_kernel(EnvParams p, int max_walls, const int32_t* __restrict__ wall_rc,
                                                          const int32_t* __restrict__ n_walls,
                                                          const double* __restrict__ cam_params,
@@ -399,31 +482,31 @@ __global__ __launch_bounds__(64) void set_layout_kernel(EnvParams p, int max_wal
                                                          const int32_t* __restrict__ n_guards,
                                                          const int32_t* __restrict__ budget,
                                                          uint8_t* __restrict__ valid_out) {
-  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ uint8_t g[kMaxDim * kMaxDim];
+  __shared__ int cnt[4];
   const int e = blockIdx.x;
   const int lane = threadIdx.x;
   const int R = p.R, C = p.C;
-  const EnvLds L = carve(smem, p.RC, p.max_cams + p.max_guards);
   // _reset_layout + create_empty_grid (environment.py:169-177, utils.py:131-139)
   for (int i = lane; i < p.RC; i += 64) {
     const int r = i / C, c = i - (i / C) * C;
-    L.grid[i] = (r == 0 || r == R - 1 || c == 0 || c == C - 1) ? kWall : kEmpty;
+    g[i] = (r == 0 || r == R - 1 || c == 0 || c == C - 1) ? kWall : kEmpty;
   }
   __syncthreads();
   if (lane == 0) {
-    L.grid[p.sr * C + p.sc] = kStart;
-    L.grid[p.vr * C + p.vc] = kVault;
+    g[p.sr * C + p.sc] = kStart;
+    g[p.vr * C + p.vc] = kVault;
     const int total = budget[e];
     int spent = 0, nw = 0, nc = 0, ng = 0;
     auto placeable = [&](int r, int c) {  // environment.py:160-167
-      return r > 0 && r < R - 1 && c > 0 && c < C - 1 && L.grid[r * C + c] == kEmpty;
+      return r > 0 && r < R - 1 && c > 0 && c < C - 1 && g[r * C + c] == kEmpty;
     };
     const int wn = min(n_walls[e], max_walls);
     for (int i = 0; i < wn; ++i) {  // :118-121
       const int r = wall_rc[((size_t)e * max_walls + i) * 2], c = wall_rc[((size_t)e * max_walls + i) * 2 + 1];
       if (placeable(r, c) && total - spent >= 1) {
         spent += 1;
-        L.grid[r * C + c] = kWall;
+        g[r * C + c] = kWall;
         ++nw;
       }
     }
@@ -438,7 +521,7 @@ __global__ __launch_bounds__(64) void set_layout_kernel(EnvParams p, int max_wal
         cm.row = (int16_t)r; cm.col = (int16_t)c; cm.range = (int16_t)cp[5];
         cm.num_rays = (int16_t)num_rays_for(cm.fov);
         p.cams[(size_t)e * p.max_cams + nc] = cm;
-        L.grid[r * C + c] = kCamera;
+        g[r * C + c] = kCamera;
         ++nc;
       }
     }
@@ -452,34 +535,42 @@ __global__ __launch_bounds__(64) void set_layout_kernel(EnvParams p, int max_wal
         uint16_t* dst = p.paths + ((size_t)e * p.max_guards + ng) * p.max_path;
         for (int k = 0; k < len; ++k) {  // points outside the grid are clamped onto it
           const int pr = min(max(src[2 * k], 0), R - 1), pc = min(max(src[2 * k + 1], 0), C - 1);
-          dst[k] = (uint16_t)(pr | (pc << 8));
+          dst[k] = (uint16_t)pack_rc(pr, pc);
         }
         Guard gd;
         gd.fov = guard_fov[(size_t)e * p.max_guards + i];
         gd.heading = 0.0;
         gd.idx = 0;
-        gd.speed = gm[1];
+        int st = gm[1] % len;  // Python % (non-negative for len > 0)
+        if (st < 0) st += len;
+        gd.step = (int16_t)st;
         gd.len = (int16_t)len;
         gd.range = (int16_t)gm[2];
         gd.num_rays = (int16_t)num_rays_for(gd.fov);
+        gd.pos = dst[0];
+        gd.pos0 = dst[0];
         gd.pad = 0;
         p.guards[(size_t)e * p.max_guards + ng] = gd;
-        L.grid[(dst[0] & 0xff) * C + (dst[0] >> 8)] = kGuard;
+        g[unpack_r(dst[0]) * C + unpack_c(dst[0])] = kGuard;
         ++ng;
       }
     }
-    L.meta[0] = nw; L.meta[1] = nc; L.meta[2] = ng; L.meta[3] = spent;
+    cnt[0] = nw; cnt[1] = nc; cnt[2] = ng; cnt[3] = spent;
   }
   __syncthreads();
-  const bool ok = bfs_wave(row_pass_mask(L.grid, R, C), p.sr, p.sc, p.vr, p.vc);
+  uint64_t m = 0;
+  if (lane < R)
+    for (int c = 0; c < C; ++c)
+      if (g[lane * C + c] != kWall) m |= 1ull << c;
+  const bool ok = bfs_wave(m, p.sr, p.sc, p.vr, p.vc);
   uint8_t* dst = p.grid + (size_t)e * p.RC;
-  for (int i = lane; i < p.RC; i += 64) dst[i] = L.grid[i];
+  for (int i = lane; i < p.RC; i += 64) dst[i] = g[i];
   if (lane == 0) {
     EnvScalars* s = p.scal + e;
-    s->n_walls = L.meta[0];
-    s->n_cams = L.meta[1];
-    s->n_guards = L.meta[2];
-    s->spent = L.meta[3];
+    s->n_walls = cnt[0];
+    s->n_cams = cnt[1];
+    s->n_guards = cnt[2];
+    s->spent = cnt[3];
     valid_out[e] = ok ? 1 : 0;
   }
 }
@@ -504,7 +595,9 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
   const int e = blockIdx.x;
   const int lane = threadIdx.x;
   const int RC = R * C;
-  const EnvLds L = carve(smem, RC, 1);
+  const EnvLds L = carve(smem, RC, 1, 0);
+  const double2* tab2 = reinterpret_cast<const double2*>(kSinCosTab);
+  for (int i = lane; i < kTabDoubles / 2; i += 64) reinterpret_cast<double2*>(L.tab)[i] = tab2[i];
   for (int i = lane; i < RC; i += 64) {
     L.grid[i] = walls[(size_t)e * RC + i] ? kWall : kEmpty;
     L.vis[i] = 0;
@@ -522,7 +615,7 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
     L.meta[1] = E.num_rays + 1;
   }
   __syncthreads();
-  cast_rays(L, R, C);
+  cast_rays<64>(L, R, C);
   __syncthreads();
   for (int i = lane; i < RC; i += 64) out[(size_t)e * RC + i] = L.vis[i];
 }
@@ -570,6 +663,10 @@ __global__ void export_kernel(EnvParams p, int32_t* scalars, int8_t* grid, doubl
 // host launchers
 // ---------------------------------------------------------------------------
 
+static size_t env_lds(const EnvParams& p) {
+  return env_lds_bytes(p.RC, p.max_cams + p.max_guards, p.max_guards * p.max_path);
+}
+
 hipError_t launch_init(const EnvParams& p, hipStream_t st) {
   hipLaunchKernelGGL(init_kernel, dim3((p.n_envs + 255) / 256), dim3(256), 0, st, p);
   return hipGetLastError();
@@ -579,23 +676,38 @@ hipError_t launch_set_layout(const EnvParams& p, int max_walls, const int32_t* w
                              const double* cam_params, const int32_t* n_cams, const int32_t* guard_paths,
                              const int32_t* guard_meta, const double* guard_fov, const int32_t* n_guards,
                              const int32_t* budget, uint8_t* valid_out, hipStream_t st) {
-  const size_t lds = env_lds_bytes(p.RC, p.max_cams + p.max_guards);
-  hipLaunchKernelGGL(set_layout_kernel, dim3(p.n_envs), dim3(64), lds, st, p, max_walls, wall_rc, n_walls, cam_params,
+  hipLaunchKernelGGL(set_layout_kernel, dim3(p.n_envs), dim3(64), 0, st, p, max_walls, wall_rc, n_walls, cam_params,
                      n_cams, guard_paths, guard_meta, guard_fov, n_guards, budget, valid_out);
   return hipGetLastError();
 }
 
 hipError_t launch_reset(const EnvParams& p, const uint8_t* mask, float* obs, hipStream_t st) {
-  const size_t lds = env_lds_bytes(p.RC, p.max_cams + p.max_guards);
-  hipLaunchKernelGGL(reset_kernel, dim3(p.n_envs), dim3(64), lds, st, p, mask, obs);
+  const size_t lds = env_lds(p);
+  switch (p.step_waves) {
+    case 1: hipLaunchKernelGGL(reset_kernel<1>, dim3(p.n_envs), dim3(64), lds, st, p, mask, obs); break;
+    case 4: hipLaunchKernelGGL(reset_kernel<4>, dim3(p.n_envs), dim3(256), lds, st, p, mask, obs); break;
+    default: hipLaunchKernelGGL(reset_kernel<2>, dim3(p.n_envs), dim3(128), lds, st, p, mask, obs); break;
+  }
   return hipGetLastError();
 }
 
 hipError_t launch_step(const EnvParams& p, const int64_t* actions, float* obs, float* rew, double* rew64,
                        uint8_t* done_out, int8_t* status_out, int auto_reset, hipStream_t st) {
-  const size_t lds = env_lds_bytes(p.RC, p.max_cams + p.max_guards);
-  hipLaunchKernelGGL(step_kernel, dim3(p.n_envs), dim3(64), lds, st, p, actions, obs, rew, rew64, done_out, status_out,
-                     auto_reset);
+  const size_t lds = env_lds(p);
+  switch (p.step_waves) {
+    case 1:
+      hipLaunchKernelGGL(step_kernel<1>, dim3(p.n_envs), dim3(64), lds, st, p, actions, obs, rew, rew64, done_out,
+                         status_out, auto_reset);
+      break;
+    case 4:
+      hipLaunchKernelGGL(step_kernel<4>, dim3(p.n_envs), dim3(256), lds, st, p, actions, obs, rew, rew64, done_out,
+                         status_out, auto_reset);
+      break;
+    default:
+      hipLaunchKernelGGL(step_kernel<2>, dim3(p.n_envs), dim3(128), lds, st, p, actions, obs, rew, rew64, done_out,
+                         status_out, auto_reset);
+      break;
+  }
   return hipGetLastError();
 }
 
@@ -614,7 +726,7 @@ hipError_t launch_bfs(const int32_t* grid, int n, int R, int C, int sr, int sc, 
 
 hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
                         uint8_t* out, hipStream_t st) {
-  const size_t lds = env_lds_bytes(R * C, 1);
+  const size_t lds = env_lds_bytes(R * C, 1, 0);
   hipLaunchKernelGGL(cones_kernel, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, out);
   return hipGetLastError();
 }

@@ -57,13 +57,14 @@ int heist_destroy(heist_t h);
  *   guard_meta  [N][max_guards][3]     int32   path length, speed, vision_range
  *   guard_fov   [N][max_guards]        float64 fov_angle
  *   budget      [N]                    int32   BudgetManager.total_budget
- *   valid_out   [N]                    uint8   bfs_path_exists(start, vault)
+ *   mask        [N]                    uint8   only envs with mask[e] != 0 are re-laid out (NULL: all)
+ *   valid_out   [N]                    uint8   bfs_path_exists(start, vault) (written for masked envs)
  * Guard path points must lie inside the grid.  Solver state is left untouched (call
  * heist_reset next, as training.py:516 does). */
 int heist_set_layout(heist_t h, int max_walls, const int32_t* wall_rc, const int32_t* n_walls,
                      const double* cam_params, const int32_t* n_cams, const int32_t* guard_paths,
                      const int32_t* guard_meta, const double* guard_fov, const int32_t* n_guards,
-                     const int32_t* budget, uint8_t* valid_out, heist_stream_t stream);
+                     const int32_t* budget, const uint8_t* mask, uint8_t* valid_out, heist_stream_t stream);
 
 /* Replaces HeistEnvironment.reset + get_state_tensor (environment.py:183-214, :347-374)
  * for envs with mask[e] != 0 (mask == NULL: all).  obs_out [N][3][R][C] float32; rows of
@@ -100,6 +101,19 @@ int heist_bfs_valid(const int32_t* grid, int n, int rows, int cols, int start_r,
  *   params [n][2] f64 = fov_angle, heading;  tiles_out [n][R][C] uint8 (1 = visible). */
 int heist_cones(int n, int rows, int cols, const uint8_t* walls, const int32_t* meta, const double* params,
                 uint8_t* tiles_out, heist_stream_t stream);
+
+/* Replaces the decode half of ArchitectNetwork.generate_layout (networks.py:283-335) and
+ * the curriculum filter of training.py:464-467 for n sampled layouts:
+ *   asset_map [n][R][C] int64 per-cell class (0 none, 1 wall, 2 camera, 3 guard);
+ *   cam_params [3] or [n][3] float32 = fov, speed, heading (cam_stride 0 or 3);
+ *   budget [n] int32.  Outputs are the heist_set_layout input arrays with capacities
+ *   max_walls / max_cams / max_guards / max_path (max_path >= 8); lists longer than a
+ *   capacity are truncated, so size capacities from the budget (budget, /3, /5). */
+int heist_architect_decode(const int64_t* asset_map, int n, int rows, int cols, const float* cam_params,
+                           int cam_stride, const int32_t* budget, int allow_cams, int allow_guards, int max_walls,
+                           int max_cams, int max_guards, int max_path, int32_t* wall_rc, int32_t* n_walls,
+                           double* cam_out, int32_t* n_cams, int32_t* guard_paths, int32_t* guard_meta,
+                           double* guard_fov, int32_t* n_guards, heist_stream_t stream);
 
 /* Replaces SolverAgent._compute_gae + returns (agents/solver.py:142-143, :228-244) on a
  * [T][N] rollout (column e = env e's concatenated episodes).  dones [T][N] uint8.

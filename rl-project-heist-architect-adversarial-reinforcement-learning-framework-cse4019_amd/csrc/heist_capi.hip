@@ -16,7 +16,7 @@ hipError_t launch_init(const EnvParams& p, hipStream_t st);
 hipError_t launch_set_layout(const EnvParams& p, int max_walls, const int32_t* wall_rc, const int32_t* n_walls,
                              const double* cam_params, const int32_t* n_cams, const int32_t* guard_paths,
                              const int32_t* guard_meta, const double* guard_fov, const int32_t* n_guards,
-                             const int32_t* budget, uint8_t* valid_out, hipStream_t st);
+                             const int32_t* budget, const uint8_t* mask, uint8_t* valid_out, hipStream_t st);
 hipError_t launch_reset(const EnvParams& p, const uint8_t* mask, float* obs, hipStream_t st);
 hipError_t launch_step(const EnvParams& p, const int64_t* actions, float* obs, float* rew, double* rew64,
                        uint8_t* done_out, int8_t* status_out, int auto_reset, hipStream_t st);
@@ -26,6 +26,11 @@ hipError_t launch_bfs(const int32_t* grid, int n, int R, int C, int sr, int sc, 
                       hipStream_t st);
 hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
                         uint8_t* out, hipStream_t st);
+hipError_t launch_arch_decode(const int64_t* amap, int n, int R, int C, const float* cam, int cam_stride,
+                              const int32_t* budget, int allow_cams, int allow_guards, int max_walls, int max_cams,
+                              int max_guards, int max_path, int32_t* wall_rc, int32_t* n_walls, double* cam_out,
+                              int32_t* n_cams, int32_t* guard_paths, int32_t* guard_meta, double* guard_fov,
+                              int32_t* n_guards, hipStream_t st);
 hipError_t launch_gae(const float* r, const float* v, const uint8_t* d, const float* last_value, int T, int N,
                       double gamma, double lam, float* adv, float* ret, hipStream_t st);
 hipError_t launch_adv_moments(const float* x, int64_t n, int phase, double* acc, hipStream_t st);
@@ -150,7 +155,7 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
     p.axis_heading[2] = htab[(size_t)(R - 1) * W2 + (-1 + C - 1)];
     p.axis_heading[3] = htab[(size_t)(R - 1) * W2 + (1 + C - 1)];
   }
-  p.step_waves = 2;
+  p.step_waves = 4;
   if (const char* w = getenv("HEIST_STEP_WAVES")) {
     const int v = atoi(w);
     if (v == 1 || v == 2 || v == 4) p.step_waves = v;
@@ -210,8 +215,8 @@ int heist_destroy(heist_t h) {
 
 int heist_set_layout(heist_t h, int max_walls, const int32_t* wall_rc, const int32_t* n_walls, const double* cam_params,
                      const int32_t* n_cams, const int32_t* guard_paths, const int32_t* guard_meta,
-                     const double* guard_fov, const int32_t* n_guards, const int32_t* budget, uint8_t* valid_out,
-                     heist_stream_t stream) {
+                     const double* guard_fov, const int32_t* n_guards, const int32_t* budget, const uint8_t* mask,
+                     uint8_t* valid_out, heist_stream_t stream) {
   if (int rc = check_handle(h)) return rc;
   HEIST_REQUIRE(max_walls >= 0, "heist_set_layout: max_walls < 0");
   HEIST_REQUIRE(n_walls && n_cams && n_guards && budget && valid_out, "heist_set_layout: null counts/budget/valid_out");
@@ -219,7 +224,8 @@ int heist_set_layout(heist_t h, int max_walls, const int32_t* wall_rc, const int
   HEIST_REQUIRE(h->p.max_cams == 0 || cam_params, "heist_set_layout: cam_params is null");
   HEIST_REQUIRE(h->p.max_guards == 0 || (guard_paths && guard_meta && guard_fov), "heist_set_layout: guard arrays null");
   return check_hip(heist::launch_set_layout(h->p, max_walls, wall_rc, n_walls, cam_params, n_cams, guard_paths,
-                                            guard_meta, guard_fov, n_guards, budget, valid_out, (hipStream_t)stream),
+                                            guard_meta, guard_fov, n_guards, budget, mask, valid_out,
+                                            (hipStream_t)stream),
                    "heist_set_layout");
 }
 
@@ -265,6 +271,28 @@ int heist_cones(int n, int rows, int cols, const uint8_t* walls, const int32_t* 
   if (n <= 0) return 0;
   return check_hip(heist::launch_cones(n, rows, cols, walls, meta, params, tiles_out, (hipStream_t)stream),
                    "heist_cones");
+}
+
+int heist_architect_decode(const int64_t* asset_map, int n, int rows, int cols, const float* cam_params,
+                           int cam_stride, const int32_t* budget, int allow_cams, int allow_guards, int max_walls,
+                           int max_cams, int max_guards, int max_path, int32_t* wall_rc, int32_t* n_walls,
+                           double* cam_out, int32_t* n_cams, int32_t* guard_paths, int32_t* guard_meta,
+                           double* guard_fov, int32_t* n_guards, heist_stream_t stream) {
+  HEIST_REQUIRE(asset_map && cam_params && budget && n_walls && n_cams && n_guards, "heist_architect_decode: null pointer");
+  HEIST_REQUIRE(rows >= 3 && cols >= 3 && rows <= heist::kMaxDim && cols <= heist::kMaxDim,
+                "heist_architect_decode: need 3 <= rows, cols <= 64");
+  HEIST_REQUIRE(cam_stride == 0 || cam_stride == 3, "heist_architect_decode: cam_stride must be 0 or 3");
+  HEIST_REQUIRE(max_walls >= 0 && max_cams >= 0 && max_guards >= 0 && max_path >= 8,
+                "heist_architect_decode: bad capacities (max_path >= 8)");
+  HEIST_REQUIRE((max_walls == 0 || wall_rc) && (max_cams == 0 || cam_out) &&
+                    (max_guards == 0 || (guard_paths && guard_meta && guard_fov)),
+                "heist_architect_decode: null output array");
+  if (n <= 0) return 0;
+  return check_hip(heist::launch_arch_decode(asset_map, n, rows, cols, cam_params, cam_stride, budget, allow_cams,
+                                             allow_guards, max_walls, max_cams, max_guards, max_path, wall_rc, n_walls,
+                                             cam_out, n_cams, guard_paths, guard_meta, guard_fov, n_guards,
+                                             (hipStream_t)stream),
+                   "heist_architect_decode");
 }
 
 int heist_gae(const float* rewards, const float* values, const uint8_t* dones, const float* last_value, int T, int n,

@@ -481,10 +481,12 @@ __global__ __launch_bounds__(64) void set_layout_kernel(EnvParams p, int max_wal
                                                          const double* __restrict__ guard_fov,
                                                          const int32_t* __restrict__ n_guards,
                                                          const int32_t* __restrict__ budget,
+                                                         const uint8_t* __restrict__ mask,
                                                          uint8_t* __restrict__ valid_out) {
   __shared__ uint8_t g[kMaxDim * kMaxDim];
   __shared__ int cnt[4];
   const int e = blockIdx.x;
+  if (mask && !mask[e]) return;
   const int lane = threadIdx.x;
   const int R = p.R, C = p.C;
   // _reset_layout + create_empty_grid (environment.py:169-177, utils.py:131-139)
@@ -675,9 +677,9 @@ hipError_t launch_init(const EnvParams& p, hipStream_t st) {
 hipError_t launch_set_layout(const EnvParams& p, int max_walls, const int32_t* wall_rc, const int32_t* n_walls,
                              const double* cam_params, const int32_t* n_cams, const int32_t* guard_paths,
                              const int32_t* guard_meta, const double* guard_fov, const int32_t* n_guards,
-                             const int32_t* budget, uint8_t* valid_out, hipStream_t st) {
+                             const int32_t* budget, const uint8_t* mask, uint8_t* valid_out, hipStream_t st) {
   hipLaunchKernelGGL(set_layout_kernel, dim3(p.n_envs), dim3(64), 0, st, p, max_walls, wall_rc, n_walls, cam_params,
-                     n_cams, guard_paths, guard_meta, guard_fov, n_guards, budget, valid_out);
+                     n_cams, guard_paths, guard_meta, guard_fov, n_guards, budget, mask, valid_out);
   return hipGetLastError();
 }
 

@@ -27,12 +27,14 @@ SIGNATURES = {
     "heist_last_error": (ctypes.c_char_p, []),
     "heist_create": (_i, [_i, _i, _i, _i, _i, _i, _i, ctypes.POINTER(_d), _i, _i, _i, _i, ctypes.POINTER(_vp)]),
     "heist_destroy": (_i, [_vp]),
-    "heist_set_layout": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "heist_set_layout": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "heist_reset": (_i, [_vp, _vp, _vp, _vp]),
     "heist_step": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
     "heist_export": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "heist_bfs_valid": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "heist_cones": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
+    "heist_architect_decode": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp,
+                                    _vp, _vp, _vp, _vp]),
     "heist_gae": (_i, [_vp, _vp, _vp, _vp, _i, _i, _d, _d, _vp, _vp, _vp]),
     "heist_adv_moments": (_i, [_vp, _i64, _i, _vp, _vp]),
     "heist_adv_apply": (_i, [_vp, _i64, _vp, _f, _vp]),

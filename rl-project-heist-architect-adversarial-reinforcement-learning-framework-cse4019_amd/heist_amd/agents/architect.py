@@ -1,0 +1,122 @@
+"""Architect agent (reference: agents/architect.py).
+
+generate_layout / store_reward / update / save / load keep the reference semantics,
+including its "simplified PPO": the log-probabilities are recorded under no_grad, so
+the policy term carries no gradient and only the encoder, fc_global and value head
+train (agents/architect.py:75-81, :105, :133).  generate_layouts() draws N layouts
+from one forward of the (constant-input) network and decodes them on the GPU.
+"""
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..architect_decode import decode_layouts
+from ..networks import ArchitectNetwork
+from ..utils import DEVICE, TileType
+from .solver import allreduce_grads
+
+
+class ArchitectAgent:  # agents/architect.py:16-170
+    def __init__(self, grid_rows: int = 20, grid_cols: int = 20, budget: int = 15, lr: float = 3e-4,
+                 gamma: float = 0.99, clip_epsilon: float = 0.2, entropy_coeff: float = 0.01,
+                 value_coeff: float = 0.5, device=None):
+        self.grid_rows = grid_rows
+        self.grid_cols = grid_cols
+        self.budget = budget
+        self.gamma = gamma
+        self.clip_epsilon = clip_epsilon
+        self.entropy_coeff = entropy_coeff
+        self.value_coeff = value_coeff
+        self.device = torch.device(device) if device is not None else DEVICE
+        self.network = ArchitectNetwork(grid_rows=grid_rows, grid_cols=grid_cols).to(self.device)
+        self.optimizer = torch.optim.Adam(self.network.parameters(), lr=lr)
+        self.log_probs: List[torch.Tensor] = []
+        self.values: List[torch.Tensor] = []
+        self.rewards: List[float] = []
+        self.episode_count = 0
+        self.total_reward = 0.0
+
+    def grid_state(self) -> torch.Tensor:
+        """The constant Architect input: start and vault markers (agents/architect.py:67-71)."""
+        g = torch.zeros((1, 1, self.grid_rows, self.grid_cols), dtype=torch.float32)
+        g[0, 0, 1, 1] = TileType.START / 5.0
+        g[0, 0, self.grid_rows - 2, self.grid_cols - 2] = TileType.VAULT / 5.0
+        return g.to(self.device)
+
+    def generate_layout(self, temperature: float = 1.0):  # agents/architect.py:53-83
+        self.network.eval()
+        with torch.no_grad():
+            walls, cams, guards, log_prob, value = self.network.generate_layout(self.grid_state(), self.budget,
+                                                                                 temperature)
+        self.log_probs.append(log_prob)
+        self.values.append(value)
+        return walls, cams, guards
+
+    @torch.no_grad()
+    def generate_layouts(self, n: int, temperature: float = 1.0, allow_cameras: bool = True,
+                         allow_guards: bool = True, env=None, generator: Optional[torch.Generator] = None,
+                         record: bool = True):
+        """n layouts as a device LayoutBatch sized for `env` (a HeistEnv), plus per-layout
+        log-probs [n] and the (shared) value."""
+        self.network.eval()
+        amap, total_logp, value, cam = self.network.sample_assets(self.grid_state(), n, temperature, generator)
+        kw = {}
+        if env is not None:
+            kw = dict(max_cams=env.max_cams, max_guards=env.max_guards, max_path=env.max_path)
+        lb = decode_layouts(amap, cam, self.budget, allow_cameras, allow_guards, **kw)
+        if record:
+            self.log_probs.extend(total_logp.unbind(0))
+            self.values.extend([value] * n)
+        return lb, total_logp, value
+
+    def store_reward(self, reward: float):
+        self.rewards.append(reward)
+        self.total_reward += reward
+        self.episode_count += 1
+
+    def store_rewards(self, rewards):
+        for r in (rewards.tolist() if torch.is_tensor(rewards) else list(rewards)):
+            self.store_reward(float(r))
+
+    def update(self) -> Dict[str, float]:  # agents/architect.py:91-155
+        if len(self.rewards) == 0:
+            return {"architect_loss": 0.0}
+        self.network.train()
+        n = min(len(self.rewards), len(self.log_probs))
+        rewards = torch.tensor(self.rewards[:n], dtype=torch.float32, device=self.device)
+        old_log_probs = torch.stack(self.log_probs[:n]).to(self.device).detach().float()
+        old_values = torch.stack([v.squeeze() for v in self.values[:n]]).to(self.device).detach()
+        if len(rewards) > 1:
+            rewards = (rewards - rewards.mean()) / (rewards.std() + 1e-8)
+        advantages = rewards - old_values
+        _, new_values, _ = self.network(self.grid_state())
+        new_value = new_values.squeeze()
+        value_loss = F.mse_loss(new_value, rewards.mean())
+        policy_loss = -(old_log_probs * advantages.detach()).mean()  # no gradient path, as in the reference
+        total_loss = policy_loss + self.value_coeff * value_loss
+        self.optimizer.zero_grad()
+        total_loss.backward()
+        params = list(self.network.parameters())
+        allreduce_grads(params)
+        nn.utils.clip_grad_norm_(params, 0.5)
+        self.optimizer.step()
+        metrics = {"architect_policy_loss": float(policy_loss.item()), "architect_value_loss": float(value_loss.item()),
+                   "architect_total_loss": float(total_loss.item()),
+                   "architect_avg_reward": self.total_reward / max(self.episode_count, 1)}
+        self.log_probs.clear()
+        self.values.clear()
+        self.rewards.clear()
+        return metrics
+
+    def save(self, path: str):  # agents/architect.py:157-163
+        torch.save({"network": self.network.state_dict(), "optimizer": self.optimizer.state_dict(),
+                    "episode_count": self.episode_count}, path)
+
+    def load(self, path: str):
+        ck = torch.load(path, map_location=self.device, weights_only=True)
+        self.network.load_state_dict(ck["network"])
+        self.optimizer.load_state_dict(ck["optimizer"])
+        self.episode_count = ck.get("episode_count", 0)

@@ -1,0 +1,203 @@
+"""Solver agent: PPO with GAE on the HIP kernels (reference: agents/solver.py).
+
+The reference API (select_action / store_transition / end_episode / update /
+_compute_gae / save / load) is kept for single-env use.  Batched training uses
+act() on [N,3,R,C] observations and update_rollout() on [T,N] rollouts; both paths
+compute GAE (heist_gae), advantage normalisation (heist_adv_*) and the clipped loss
+and its gradient (heist_ppo_loss) on the GPU.  With torch.distributed initialised the
+gradients of every optimizer step are averaged with ONE flat all-reduce.
+"""
+from collections import deque
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..networks import SolverNetwork
+from ..ppo import compute_gae, normalize_advantages, ppo_loss
+from ..utils import DEVICE
+
+
+def allreduce_grads(params, group=None):
+    """Average .grad over ranks with one flat all-reduce (a single RCCL call)."""
+    dist = torch.distributed
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return
+    grads = [p.grad for p in params if p.grad is not None]
+    if not grads:
+        return
+    flat = torch.cat([g.reshape(-1) for g in grads])
+    dist.all_reduce(flat, group=group)
+    flat.div_(dist.get_world_size(group))
+    o = 0
+    for g in grads:
+        n = g.numel()
+        g.copy_(flat[o:o + n].view_as(g))
+        o += n
+
+
+@dataclass
+class Rollout:
+    """[T, N] time-major rollout of the batched environment."""
+    obs: torch.Tensor       # [T, N, 3, R, C] float32
+    actions: torch.Tensor   # [T, N] int64
+    logp: torch.Tensor      # [T, N] float32
+    values: torch.Tensor    # [T, N] float32
+    rewards: torch.Tensor   # [T, N] float32
+    dones: torch.Tensor     # [T, N] uint8
+    mask: Optional[torch.Tensor] = None        # [N] bool: envs whose samples train (valid layouts)
+    last_value: Optional[torch.Tensor] = None  # [N] bootstrap (None: the reference's buffer-end 0)
+
+
+class SolverAgent:  # agents/solver.py:18-259
+    def __init__(self, grid_rows: int = 20, grid_cols: int = 20, num_actions: int = 5, lr: float = 3e-4,
+                 gamma: float = 0.99, gae_lambda: float = 0.95, clip_epsilon: float = 0.2,
+                 entropy_coeff: float = 0.05, value_coeff: float = 0.5, max_grad_norm: float = 0.5,
+                 ppo_epochs: int = 3, batch_size: int = 64, device=None):
+        self.grid_rows = grid_rows
+        self.grid_cols = grid_cols
+        self.num_actions = num_actions
+        self.gamma = gamma
+        self.gae_lambda = gae_lambda
+        self.clip_epsilon = clip_epsilon
+        self.entropy_coeff = entropy_coeff
+        self.value_coeff = value_coeff
+        self.max_grad_norm = max_grad_norm
+        self.ppo_epochs = ppo_epochs
+        self.batch_size = batch_size
+        self.device = torch.device(device) if device is not None else DEVICE
+        self.network = SolverNetwork(grid_rows=grid_rows, grid_cols=grid_cols, num_actions=num_actions).to(self.device)
+        self.optimizer = torch.optim.Adam(self.network.parameters(), lr=lr)
+        self.hidden = None
+        self.states, self.actions, self.log_probs, self.values, self.rewards, self.dones = [], [], [], [], [], []
+        self.episode_count = 0
+        self.total_reward = 0.0
+        self.recent_rewards = deque(maxlen=100)
+
+    # -- single-env API ------------------------------------------------------------
+    def reset(self):
+        self.hidden = None
+
+    def select_action(self, state: np.ndarray) -> int:  # agents/solver.py:75-99
+        self.network.eval()
+        st = torch.as_tensor(np.asarray(state, np.float32)).unsqueeze(0).to(self.device)
+        with torch.no_grad():
+            action, log_prob, value, self.hidden = self.network.get_action(st, self.hidden)
+        self.states.append(state)
+        self.actions.append(int(action.item()))
+        self.log_probs.append(float(log_prob.item()))
+        self.values.append(float(value.item()))
+        return int(action.item())
+
+    def store_transition(self, reward: float, done: bool):
+        self.rewards.append(reward)
+        self.dones.append(done)
+
+    def end_episode(self, final_reward: float):
+        self.total_reward += final_reward
+        self.recent_rewards.append(final_reward)
+        self.episode_count += 1
+
+    def _compute_gae(self, rewards: torch.Tensor, values: torch.Tensor, dones: torch.Tensor) -> torch.Tensor:
+        """agents/solver.py:228-244 on one flat buffer (bootstrap 0 at the end)."""
+        adv, _ = compute_gae(rewards, values, dones, gamma=self.gamma, lam=self.gae_lambda)
+        return adv
+
+    def _clear_buffers(self):
+        for b in (self.states, self.actions, self.log_probs, self.values, self.rewards, self.dones):
+            b.clear()
+
+    def update(self) -> Dict[str, float]:  # agents/solver.py:112-217
+        if len(self.states) == 0:
+            return {"solver_loss": 0.0}
+        n = min(len(self.states), len(self.actions), len(self.log_probs), len(self.values), len(self.rewards),
+                len(self.dones))
+        if n == 0:
+            self._clear_buffers()
+            return {"solver_loss": 0.0}
+        d = self.device
+        states = torch.as_tensor(np.array(self.states[:n], np.float32)).to(d)
+        actions = torch.as_tensor(self.actions[:n], dtype=torch.int64).to(d)
+        old_logp = torch.as_tensor(self.log_probs[:n], dtype=torch.float32).to(d)
+        values = torch.as_tensor(self.values[:n], dtype=torch.float32).to(d)
+        rewards = torch.as_tensor(self.rewards[:n], dtype=torch.float32).to(d)
+        dones = torch.as_tensor(self.dones[:n], dtype=torch.float32).to(d)
+        adv, ret = compute_gae(rewards, values, dones, gamma=self.gamma, lam=self.gae_lambda)
+        if n > 1:
+            adv = normalize_advantages(adv)
+        m = self._ppo_epochs(states, actions, old_logp, adv, ret, n, np.random.permutation)
+        m["solver_avg_reward"] = float(np.mean(self.recent_rewards)) if self.recent_rewards else 0.0
+        m["solver_episodes"] = self.episode_count
+        self._clear_buffers()
+        return m
+
+    def _ppo_epochs(self, states, actions, old_logp, adv, ret, n, perm_fn, minibatch=None) -> Dict[str, float]:
+        """agents/solver.py:157-204: epochs x shuffled minibatches, zero-hidden re-forward."""
+        self.network.train()
+        bs = minibatch or self.batch_size
+        tot = torch.zeros(3, device=self.device)
+        updates = 0
+        params = list(self.network.parameters())
+        for _ in range(self.ppo_epochs):
+            idx = torch.as_tensor(perm_fn(n), device=self.device)
+            for start in range(0, n, bs):
+                b = idx[start:start + bs]
+                logits, new_values, _ = self.network(states[b])
+                loss, parts = ppo_loss(logits, new_values.reshape(-1), actions[b], old_logp[b], adv[b], ret[b],
+                                       self.clip_epsilon, self.value_coeff, self.entropy_coeff)
+                self.optimizer.zero_grad(set_to_none=False)
+                loss.backward()
+                allreduce_grads(params)
+                nn.utils.clip_grad_norm_(params, self.max_grad_norm)
+                self.optimizer.step()
+                tot += parts[1:].detach()
+                updates += 1
+        t = (tot / max(updates, 1)).cpu().numpy()
+        return {"solver_policy_loss": float(t[0]), "solver_value_loss": float(t[1]), "solver_entropy": float(t[2])}
+
+    # -- batched API ------------------------------------------------------------------
+    @torch.no_grad()
+    def act(self, obs: torch.Tensor, hidden=None, generator: Optional[torch.Generator] = None):
+        """Batched select_action: (action [N], log_prob [N], value [N], hidden)."""
+        self.network.eval()
+        logits, value, hidden = self.network(obs, hidden)
+        logp_all = F.log_softmax(logits.float(), dim=-1)
+        action = torch.multinomial(logp_all.exp(), 1, generator=generator).reshape(-1)
+        # Categorical(probs).log_prob = log(clamp(p / sum p, eps, 1 - eps))
+        p = logp_all.exp()
+        p = p / p.sum(-1, keepdim=True)
+        eps = torch.finfo(p.dtype).eps
+        logp = torch.log(p.gather(1, action[:, None]).clamp(eps, 1 - eps)).reshape(-1)
+        return action, logp, value.reshape(-1).float(), hidden
+
+    def update_rollout(self, ro: Rollout, minibatch: int = 4096) -> Dict[str, float]:
+        """One PPO update on a [T, N] rollout (GAE per env column, global advantage norm)."""
+        T, N = ro.rewards.shape
+        adv, ret = compute_gae(ro.rewards, ro.values, ro.dones, ro.last_value, self.gamma, self.gae_lambda)
+        sel = None if ro.mask is None else ro.mask.reshape(1, N).expand(T, N).reshape(-1)
+        flat = lambda x: x.reshape(T * N, *x.shape[2:])  # noqa: E731
+        states, actions, old_logp, adv, ret = flat(ro.obs), flat(ro.actions), flat(ro.logp), flat(adv), flat(ret)
+        if sel is not None:
+            states, actions, old_logp, adv, ret = (x[sel] for x in (states, actions, old_logp, adv, ret))
+        n = adv.shape[0]
+        if n == 0:
+            return {"solver_loss": 0.0}
+        adv = normalize_advantages(adv)
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(int(torch.randint(0, 2 ** 31, (1,)).item()))
+        perm = lambda k: torch.randperm(k, device=self.device, generator=gen)  # noqa: E731
+        return self._ppo_epochs(states, actions, old_logp, adv, ret, n, perm, minibatch=minibatch)
+
+    # -- checkpoints ---------------------------------------------------------------------
+    def save(self, path: str):  # agents/solver.py:246-252 dict format
+        torch.save({"network": self.network.state_dict(), "optimizer": self.optimizer.state_dict(),
+                    "episode_count": self.episode_count}, path)
+
+    def load(self, path: str):
+        ck = torch.load(path, map_location=self.device, weights_only=True)
+        self.network.load_state_dict(ck["network"])
+        self.optimizer.load_state_dict(ck["optimizer"])
+        self.episode_count = ck.get("episode_count", 0)

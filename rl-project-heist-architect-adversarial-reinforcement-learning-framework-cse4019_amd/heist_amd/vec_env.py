@@ -79,6 +79,23 @@ class LayoutBatch:
         return LayoutBatch(t(W), t(nw), t(CP), t(nc), t(GP), t(GM), t(GF), t(ng), t(b))
 
 
+def _layout_to_lists(lb: "LayoutBatch"):
+    W, nw, CP, nc, GP, GM, GF, ng = (t.cpu().numpy() for t in (lb.wall_rc, lb.n_walls, lb.cam_params, lb.n_cams,
+                                                              lb.guard_paths, lb.guard_meta, lb.guard_fov, lb.n_guards))
+    out = []
+    for e in range(len(nw)):
+        walls = [(int(r), int(c)) for r, c in W[e, :nw[e]]]
+        cams = [{"row": int(c[0]), "col": int(c[1]), "fov_angle": float(c[2]), "rotation_speed": float(c[4]),
+                 "heading": float(c[3]), "vision_range": int(c[5])} for c in CP[e, :nc[e]]]
+        guards = [{"patrol_path": [(int(r), int(c)) for r, c in GP[e, i, :GM[e, i, 0]]], "speed": int(GM[e, i, 1]),
+                   "vision_range": int(GM[e, i, 2]), "fov_angle": float(GF[e, i])} for i in range(ng[e])]
+        out.append((walls, cams, guards))
+    return out
+
+
+LayoutBatch.to_lists = _layout_to_lists
+
+
 class HeistEnv:
     """Batched HeistEnvironment on one HIP device.
 
@@ -132,24 +149,54 @@ class HeistEnv:
         return nat.stream(self.device)
 
     # -- layout ------------------------------------------------------------------
-    def set_layout_batch(self, lb: LayoutBatch) -> torch.Tensor:
-        """heist_set_layout on pre-packed device arrays; returns valid [N] bool."""
+    def set_layout_batch(self, lb: LayoutBatch, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """heist_set_layout on pre-packed device arrays (only envs in mask if given);
+        returns valid [N] bool."""
+        n, mc, mg, mp = self.n_envs, max(1, self.max_cams), max(1, self.max_guards), self.max_path
+        want = {"wall_rc": (n, lb.max_walls, 2), "n_walls": (n,), "cam_params": (n, mc, 6), "n_cams": (n,),
+                "guard_paths": (n, mg, mp, 2), "guard_meta": (n, mg, 3), "guard_fov": (n, mg), "n_guards": (n,),
+                "budget": (n,)}
+        dtypes = {"cam_params": torch.float64, "guard_fov": torch.float64}
+        for k, shp in want.items():  # the kernel indexes with this handle's capacities
+            t = getattr(lb, k)
+            if tuple(t.shape) != shp or t.dtype != dtypes.get(k, torch.int32) or t.device != self.device \
+                    or not t.is_contiguous():
+                raise ValueError("LayoutBatch.%s: expected contiguous %s %s on %s, got %s %s on %s"
+                                 % (k, dtypes.get(k, torch.int32), shp, self.device, t.dtype, tuple(t.shape), t.device))
+        m = None if mask is None else mask.to(device=self.device, dtype=torch.uint8).contiguous()
         with torch.cuda.device(self.device):
             nat.check(nat.lib().heist_set_layout(
                 self._h, lb.max_walls, nat.ptr(lb.wall_rc), nat.ptr(lb.n_walls), nat.ptr(lb.cam_params),
                 nat.ptr(lb.n_cams), nat.ptr(lb.guard_paths), nat.ptr(lb.guard_meta), nat.ptr(lb.guard_fov),
-                nat.ptr(lb.n_guards), nat.ptr(lb.budget), nat.ptr(self.valid), self._stream()), "heist_set_layout")
+                nat.ptr(lb.n_guards), nat.ptr(lb.budget), nat.ptr(m), nat.ptr(self.valid), self._stream()),
+                "heist_set_layout")
         return self.valid.view(torch.bool)
 
-    def set_layouts(self, layouts: Sequence[Layout], budget: Union[int, Sequence[int]] = None) -> torch.Tensor:
-        """HeistEnvironment.set_layout (environment.py:102-152) for every env."""
-        if len(layouts) != self.n_envs:
-            raise ValueError("expected %d layouts, got %d" % (self.n_envs, len(layouts)))
+    def set_layouts(self, layouts: Sequence[Layout], budget: Union[int, Sequence[int]] = None,
+                    env_ids: Optional[Sequence[int]] = None) -> torch.Tensor:
+        """HeistEnvironment.set_layout (environment.py:102-152) for every env, or only for
+        env_ids (then layouts[i] goes to env env_ids[i])."""
         if budget is None:
             budget = self.config.architect_budget
+        mask = None
+        if env_ids is not None:
+            if len(layouts) != len(env_ids):
+                raise ValueError("expected one layout per env id")
+            full = [([], [], [])] * self.n_envs
+            b = np.broadcast_to(np.asarray(budget, np.int32), (len(env_ids),))
+            bud = np.zeros(self.n_envs, np.int32)
+            for i, e in enumerate(env_ids):
+                full[int(e)] = layouts[i]
+                bud[int(e)] = b[i]
+            m = np.zeros(self.n_envs, np.uint8)
+            m[np.asarray(env_ids, np.int64)] = 1
+            mask = torch.from_numpy(m).to(self.device)
+            layouts, budget = full, bud
+        elif len(layouts) != self.n_envs:
+            raise ValueError("expected %d layouts, got %d" % (self.n_envs, len(layouts)))
         lb = LayoutBatch.from_lists(layouts, budget, self.max_cams, self.max_guards, self.max_path, self.device,
                                     self.rows, self.cols)
-        return self.set_layout_batch(lb)
+        return self.set_layout_batch(lb, mask)
 
     # -- episode -----------------------------------------------------------------
     def reset(self, mask: Optional[torch.Tensor] = None) -> torch.Tensor:

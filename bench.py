@@ -62,6 +62,42 @@ def cpu_baseline(layouts, cfg, budget, target_s=10.0, threads=1):
                       % (len(sample), steps, n, dt)}
 
 
+def measure_rollout(env, dev, steps=20, warmup=3):
+    """env step + batched Solver forward (fp32, carried LSTM state) + action sampling."""
+    from heist_amd.agents import SolverAgent
+    ag = SolverAgent(env.rows, env.cols, device=dev)
+    h = c = torch.zeros(1, env.n_envs, 128, device=dev)
+    for k in range(warmup + steps):
+        if k == warmup:
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+        a, lp, v, (h, c) = ag.act(env.obs, (h, c))
+        env.step(a)
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    return {"value": steps * env.n_envs / dt, "unit": "env-steps/s", "ms_per_step": dt / steps * 1e3,
+            "dtype": "fp32 policy", "note": "heist_step + SolverNetwork forward on PyTorch-ROCm + multinomial"}
+
+
+def measure_train(cfg, dev, n_envs, rollout_len=32, minibatch=16384):
+    """Batched AdversarialTrainer iteration: rollout + heist_gae + adv-norm + 3 PPO epochs
+    (heist_ppo_loss, Adam) + Architect scoring/update/re-layout."""
+    from heist_amd.training import AdversarialTrainer
+    import tempfile
+    d = tempfile.mkdtemp()
+    tr = AdversarialTrainer(cfg, solver_episodes_per_layout=4, total_episodes=10 ** 9, save_dir=d, log_dir=d,
+                            n_envs=n_envs, rollout_len=rollout_len, minibatch=minibatch, device=dev, seed=0)
+    tr._assign_layouts(np.arange(n_envs))
+    tr.train_iteration()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    tr.train_iteration()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    return {"value": rollout_len * n_envs / dt, "unit": "env-steps/s", "s_per_iteration": dt,
+            "config": "T=%d x %d envs, 3 epochs, minibatch %d, fp32" % (rollout_len, n_envs, minibatch)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -71,6 +107,7 @@ def main():
     ap.add_argument("--budget", type=int, default=15)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-secondary", action="store_true", help="skip the rollout / full-train numbers")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,6 +184,9 @@ def main():
                          "algorithmic_bytes_per_env_step": b_step},
             "cpu_baseline": None,
         }
+        if not args.no_secondary:
+            line["secondary"] = {"rollout": measure_rollout(env, dev),
+                                 "full_train": measure_train(cfg, dev, N)}
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(layouts, cfg, args.budget, target_s=args.cpu_seconds, threads=1)
         print(json.dumps(line), flush=True)

@@ -55,12 +55,13 @@ def test_masked_set_layout_and_reset(gpu_device):
     for _ in range(7):
         env.step(torch.full((n,), 4))
     obs_before = env.obs.clone()
+    tick_before = env.export()["tick"].clone()
     m = torch.zeros(n, dtype=torch.uint8, device=gpu_device)
     m[[1, 5, 9]] = 1
     env.reset(m)
     assert torch.equal(env.obs[keep], obs_before[keep])
     st = env.export()
-    assert (st["tick"][[1, 5, 9]] == 0).all() and (st["tick"][keep] == 7).all()
+    assert (st["tick"][[1, 5, 9]] == 0).all() and torch.equal(st["tick"][keep], tick_before[keep])
 
 
 def test_single_env_class_matches_golden_traces(gpu_device):

@@ -115,6 +115,11 @@ int heist_architect_decode(const int64_t* asset_map, int n, int rows, int cols, 
                            double* cam_out, int32_t* n_cams, int32_t* guard_paths, int32_t* guard_meta,
                            double* guard_fov, int32_t* n_guards, heist_stream_t stream);
 
+/* math.sin / math.cos of the reference's raycast (security.py:74-75, :174-175) as the GPU
+ * evaluates them: glibc 2.35's dbl-64 algorithm, bit-exact to the host libm for
+ * |x| < 105414350.  x, sin_out, cos_out [n] float64 (parity checks and tooling). */
+int heist_sincos(const double* x, int64_t n, double* sin_out, double* cos_out, heist_stream_t stream);
+
 /* Replaces SolverAgent._compute_gae + returns (agents/solver.py:142-143, :228-244) on a
  * [T][N] rollout (column e = env e's concatenated episodes).  dones [T][N] uint8.
  * last_value [N] bootstraps t = T-1 (NULL = 0, the reference's buffer-end rule).  gamma and

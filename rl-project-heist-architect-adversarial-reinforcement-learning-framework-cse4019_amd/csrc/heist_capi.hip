@@ -31,6 +31,7 @@ hipError_t launch_arch_decode(const int64_t* amap, int n, int R, int C, const fl
                               int max_guards, int max_path, int32_t* wall_rc, int32_t* n_walls, double* cam_out,
                               int32_t* n_cams, int32_t* guard_paths, int32_t* guard_meta, double* guard_fov,
                               int32_t* n_guards, hipStream_t st);
+hipError_t launch_sincos(const double* x, int64_t n, double* so, double* co, hipStream_t st);
 hipError_t launch_gae(const float* r, const float* v, const uint8_t* d, const float* last_value, int T, int N,
                       double gamma, double lam, float* adv, float* ret, hipStream_t st);
 hipError_t launch_adv_moments(const float* x, int64_t n, int phase, double* acc, hipStream_t st);
@@ -293,6 +294,12 @@ int heist_architect_decode(const int64_t* asset_map, int n, int rows, int cols, 
                                              cam_out, n_cams, guard_paths, guard_meta, guard_fov, n_guards,
                                              (hipStream_t)stream),
                    "heist_architect_decode");
+}
+
+int heist_sincos(const double* x, int64_t n, double* sin_out, double* cos_out, heist_stream_t stream) {
+  HEIST_REQUIRE(x && sin_out && cos_out, "heist_sincos: null pointer");
+  if (n <= 0) return 0;
+  return check_hip(heist::launch_sincos(x, n, sin_out, cos_out, (hipStream_t)stream), "heist_sincos");
 }
 
 int heist_gae(const float* rewards, const float* values, const uint8_t* dones, const float* last_value, int T, int n,

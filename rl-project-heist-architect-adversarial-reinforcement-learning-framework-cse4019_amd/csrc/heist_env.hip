@@ -661,6 +661,17 @@ __global__ void export_kernel(EnvParams p, int32_t* scalars, int8_t* grid, doubl
   }
 }
 
+__global__ __launch_bounds__(256) void sincos_kernel(const double* __restrict__ x, int64_t n,
+                                                     double* __restrict__ so, double* __restrict__ co) {
+  __shared__ double tab[kTabDoubles];
+  for (int i = threadIdx.x; i < kTabDoubles; i += blockDim.x) tab[i] = kSinCosTab[i];
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    so[i] = heist_trig::sin(x[i], tab);
+    co[i] = heist_trig::cos(x[i], tab);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------
@@ -730,6 +741,12 @@ hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t
                         uint8_t* out, hipStream_t st) {
   const size_t lds = env_lds_bytes(R * C, 1, 0);
   hipLaunchKernelGGL(cones_kernel, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_sincos(const double* x, int64_t n, double* so, double* co, hipStream_t st) {
+  int64_t b = (n + 255) / 256;
+  hipLaunchKernelGGL(sincos_kernel, dim3((unsigned)(b > 4096 ? 4096 : (b < 1 ? 1 : b))), dim3(256), 0, st, x, n, so, co);
   return hipGetLastError();
 }
 

@@ -35,6 +35,7 @@ SIGNATURES = {
     "heist_cones": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     "heist_architect_decode": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp]),
+    "heist_sincos": (_i, [_vp, _i64, _vp, _vp, _vp]),
     "heist_gae": (_i, [_vp, _vp, _vp, _vp, _i, _i, _d, _d, _vp, _vp, _vp]),
     "heist_adv_moments": (_i, [_vp, _i64, _i, _vp, _vp]),
     "heist_adv_apply": (_i, [_vp, _i64, _vp, _f, _vp]),

@@ -157,6 +157,8 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
     p.axis_heading[3] = htab[(size_t)(R - 1) * W2 + (1 + C - 1)];
   }
   p.step_waves = 4;
+  p.trig_mode = 1;
+  if (const char* m = getenv("HEIST_TRIG_MODE")) p.trig_mode = atoi(m) ? 1 : 0;
   if (const char* w = getenv("HEIST_STEP_WAVES")) {
     const int v = atoi(w);
     if (v == 1 || v == 2 || v == 4) p.step_waves = v;

@@ -93,8 +93,14 @@ __device__ void cast_rays(const EnvLds& L, int R, int C) {
     const int i = j - E.first;
     const double angle = E.hmh + (E.fov * (double)i) / (double)E.num_rays;  // security.py:70
     const double rad = angle * kDegToRad;                                   // math.radians
-    const double dx = heist_trig::cos(rad, L.tab);
-    const double dy = -heist_trig::sin(rad, L.tab);
+    double dx, dy;
+    if (L.meta[2]) {
+      heist_trig::sincos(rad, L.tab, &dy, &dx);
+      dy = -dy;
+    } else {
+      dx = heist_trig::cos(rad, L.tab);
+      dy = -heist_trig::sin(rad, L.tab);
+    }
     const double stride = E.kind == 0 ? 0.5 : 1.0;
     const int n_samp = E.kind == 0 ? 2 * E.range : E.range;
     const double col = (double)E.col, row = (double)E.row;
@@ -129,8 +135,9 @@ __device__ void cast_rays(const EnvLds& L, int R, int C) {
 }
 
 // One thread turns per-emitter ray counts into the flattened ray index.
-__device__ __forceinline__ void index_rays(const EnvLds& L, int n_em) {
+__device__ __forceinline__ void index_rays(const EnvLds& L, int n_em, int trig_mode = 1) {
   if (threadIdx.x == 0) {
+    L.meta[2] = trig_mode;
     int t = 0;
     for (int k = 0; k < n_em; ++k) {
       L.em[k].first = t;
@@ -163,7 +170,7 @@ __device__ __forceinline__ Emit guard_emit(const Guard& gd) {
 template <int NT>
 __device__ __forceinline__ void raycast_pass(const EnvParams& p, const EnvLds& L, int n_em, int n_cams) {
   __syncthreads();
-  index_rays(L, n_em);
+  index_rays(L, n_em, p.trig_mode);
   __syncthreads();
   cast_rays<NT>(L, p.R, p.C);
   __syncthreads();
@@ -615,6 +622,7 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
     L.em[0] = E;
     L.meta[0] = 1;
     L.meta[1] = E.num_rays + 1;
+    L.meta[2] = 1;
   }
   __syncthreads();
   cast_rays<64>(L, R, C);
@@ -667,8 +675,7 @@ __global__ __launch_bounds__(256) void sincos_kernel(const double* __restrict__ 
   for (int i = threadIdx.x; i < kTabDoubles; i += blockDim.x) tab[i] = kSinCosTab[i];
   __syncthreads();
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    so[i] = heist_trig::sin(x[i], tab);
-    co[i] = heist_trig::cos(x[i], tab);
+    heist_trig::sincos(x[i], tab, so + i, co + i);
   }
 }
 

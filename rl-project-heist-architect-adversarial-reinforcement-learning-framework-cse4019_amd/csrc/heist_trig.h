@@ -140,4 +140,49 @@ HEIST_HD double cos(double x, const double* tab) {
   return (n & 2) ? -r : r;
 }
 
+// sin(x) and cos(x) together, bit-identical to sin() and cos() above, without
+// per-branch divergence.  In every glibc branch one of the two values comes from a
+// sin-type kernel (taylor_sin or do_sin) and the other from do_cos, on arguments that
+// depend on the branch; so the arguments are selected per lane, each kernel runs once,
+// and the results are routed and negated afterwards:
+//   |x| < 0.855 (k < 0x3feb6000):  sin = sin_type(x, 0)            cos = do_cos(x, 0)
+//   |x| < 2.426:   t = hp0 - |x|   sin = copysign(do_cos(t, hp1), x)  cos = sin_type(t + hp1, da)
+//   otherwise:     x = n pi/2 + a  sin = (n odd ? do_cos : sin_type)(a, da), cos uses n + 1
+// plus the tiny-argument early returns (sin x = x, cos x = 1).
+HEIST_HD void sincos(double x, const double* tab, double* s_out, double* c_out) {
+  const uint32_t k = hiword_abs(x);
+  const double ax = fabs(x);
+  const bool in_a = k < 0x3feb6000u;
+  const bool in_b = !in_a && k < 0x400368fdu;
+  double a = x, da = 0.0;
+  int n = 0;
+  if (!in_a && !in_b) n = reduce(x, &a, &da);
+  const double t = kHp0 - ax;                 // branch B
+  const double ab = t + kHp1;
+  const double dab = (t - ab) + kHp1;
+  const double sa = in_a ? x : (in_b ? ab : a);      // sin-type argument
+  const double sda = in_a ? 0.0 : (in_b ? dab : da);
+  const double ca = in_a ? x : (in_b ? t : a);       // do_cos argument
+  const double cdx = in_a ? 0.0 : (in_b ? kHp1 : da);
+  const double ts = taylor_sin(sa, sda);
+  const double ds = do_sin(sa, sda, tab);
+  const double S = fabs(sa) < kTaylorMax ? ts : ds;
+  const double D = do_cos(ca, cdx, tab);
+  double sv, cv;
+  if (in_a) {
+    sv = S;
+    cv = D;
+  } else if (in_b) {
+    sv = copysign(D, x);
+    cv = S;
+  } else {
+    const double s0 = (n & 1) ? D : S;
+    const double c0 = (n & 1) ? S : D;
+    sv = (n & 2) ? -s0 : s0;
+    cv = ((n + 1) & 2) ? -c0 : c0;
+  }
+  *s_out = k < 0x3e500000u ? x : sv;
+  *c_out = k < 0x3e400000u ? 1.0 : cv;
+}
+
 }  // namespace heist_trig

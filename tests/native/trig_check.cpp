@@ -19,10 +19,12 @@ static double (*volatile p_cos)(double) = ::cos;
 static void check(double x) {
   double s0 = p_sin(x), c0 = p_cos(x);
   double s1 = heist_trig::sin(x, kTab), c1 = heist_trig::cos(x, kTab);
+  double s2, c2;
+  heist_trig::sincos(x, kTab, &s2, &c2);
   ++g_n;
-  if (memcmp(&s0, &s1, 8) || memcmp(&c0, &c1, 8)) {
+  if (memcmp(&s0, &s1, 8) || memcmp(&c0, &c1, 8) || memcmp(&s0, &s2, 8) || memcmp(&c0, &c2, 8)) {
     if (++g_bad <= 10)
-      printf("MISMATCH x=%a sin libm=%a emu=%a cos libm=%a emu=%a\n", x, s0, s1, c0, c1);
+      printf("MISMATCH x=%a sin libm=%a emu=%a joint=%a cos libm=%a emu=%a joint=%a\n", x, s0, s1, s2, c0, c1, c2);
   }
 }
 

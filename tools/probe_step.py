@@ -12,8 +12,9 @@ from heist_amd import EnvironmentConfig, HeistEnv  # noqa: E402
 from heist_amd.layouts import synthetic_layouts  # noqa: E402
 
 
-def make(n, budget, n_cams, n_guards, R=20, waves=2):
+def make(n, budget, n_cams, n_guards, R=20, waves=4, trig=1):
     os.environ["HEIST_STEP_WAVES"] = str(waves)
+    os.environ["HEIST_TRIG_MODE"] = str(trig)
     cfg = EnvironmentConfig(grid_rows=R, grid_cols=R)
     env = HeistEnv(n, cfg, device="cuda")
     lays = synthetic_layouts(n, R, R, budget, seed=1, n_cams=n_cams, n_guards=n_guards)
@@ -37,12 +38,12 @@ def time_env(env, acts, iters=40):
 
 
 cases = {}
-for w in (1, 2, 4):
+for trig in (0, 1):
     for n in (1024, 4096, 16384):
-        cases["w%d_n%d_b15" % (w, n)] = make(n, 15, None, None, waves=w)
-    for nc, ng in ((0, 0), (4, 0), (2, 1)):
-        cases["w%d_n4096_c%d_g%d" % (w, nc, ng)] = make(4096, 3 * nc + 5 * ng + 2, nc, ng, waves=w)
-    cases["w%d_n4096_32x32_c4_g3" % w] = make(4096, 40, 4, 3, R=32, waves=w)
+        cases["t%d_n%d_b15" % (trig, n)] = make(n, 15, None, None, trig=trig)
+    for nc, ng in ((4, 0), (0, 2)):
+        cases["t%d_n4096_c%d_g%d" % (trig, nc, ng)] = make(4096, 3 * nc + 5 * ng + 2, nc, ng, trig=trig)
+    cases["t%d_n4096_32x32_c4_g3" % trig] = make(4096, 40, 4, 3, R=32, trig=trig)
 res = {k: [] for k in cases}
 for rnd in range(5):
     for k, (env, acts) in cases.items():

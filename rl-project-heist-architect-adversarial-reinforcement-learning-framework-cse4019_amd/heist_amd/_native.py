@@ -93,4 +93,7 @@ def stream(device=None):
 def require_gpu(device=None):
     if not torch.cuda.is_available():
         raise HeistError("no HIP device: heist_amd has no CPU fallback")
-    return torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    d = torch.device(device) if device is not None else torch.device("cuda")
+    if d.type != "cuda":
+        raise HeistError("heist_amd runs on HIP devices, got %s" % d)
+    return torch.device("cuda", d.index if d.index is not None else torch.cuda.current_device())

@@ -157,12 +157,16 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
     p.axis_heading[3] = htab[(size_t)(R - 1) * W2 + (1 + C - 1)];
   }
   p.step_waves = 4;
-  p.trig_mode = 1;
-  if (const char* m = getenv("HEIST_TRIG_MODE")) p.trig_mode = atoi(m) ? 1 : 0;
+  p.ray_chunk = 4;
+  if (const char* u = getenv("HEIST_RAY_CHUNK")) {  // tuning knob; unsupported pairs fall back to 4
+    const int v = atoi(u);
+    if (v == 2 || v == 8) p.ray_chunk = v;
+  }
   if (const char* w = getenv("HEIST_STEP_WAVES")) {
     const int v = atoi(w);
     if (v == 1 || v == 2 || v == 4) p.step_waves = v;
   }
+  if (p.step_waves != 4) p.ray_chunk = 4;
   for (int k = 0; k < 8; ++k) p.tile_lut[k] = k <= 5 ? (float)k / 5.0f : 0.0f;  // environment.py:319
 
   const size_t sizes[] = {

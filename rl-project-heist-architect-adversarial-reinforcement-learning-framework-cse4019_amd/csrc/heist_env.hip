@@ -48,29 +48,45 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(
 struct EnvLds {
   double* tab;     // [440] glibc sin/cos table
   uint8_t* grid;   // [RC]
-  uint8_t* vis;    // [RC]
+  uint8_t* vis;    // [RC + 1]; vis[RC] is a write sink for masked-off ray samples
+  uint8_t* wall;   // [(R+2)(C+2)] 1 = stops a ray: a wall or the ring just outside the grid
   Emit* em;        // [n_emit]
   uint16_t* path;  // [max_guards][max_path]
   float* plane;    // [RC] static position channel (plane0)
   int* meta;       // [0] emitters, [1] total rays
 };
 
-__host__ __device__ inline size_t env_lds_bytes(int RC, int n_emit, int path_words) {
-  return align16(sizeof(double) * kTabDoubles) + 2 * align16(RC) + align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) +
+__host__ __device__ inline size_t env_lds_bytes(int R, int C, int n_emit, int path_words) {
+  const int RC = R * C;
+  return align16(sizeof(double) * kTabDoubles) + align16(RC) + align16(RC + 1) + align16((R + 2) * (C + 2)) +
+         align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) +
          align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1)) + align16(sizeof(float) * RC) + 16;
 }
 
-__device__ __forceinline__ EnvLds carve(unsigned char* smem, int RC, int n_emit, int path_words) {
+__device__ __forceinline__ EnvLds carve(unsigned char* smem, int R, int C, int n_emit, int path_words) {
+  const int RC = R * C;
   EnvLds L;
   size_t o = 0;
   L.tab = reinterpret_cast<double*>(smem + o); o += align16(sizeof(double) * kTabDoubles);
   L.grid = smem + o; o += align16(RC);
-  L.vis = smem + o; o += align16(RC);
+  L.vis = smem + o; o += align16(RC + 1);
+  L.wall = smem + o; o += align16((R + 2) * (C + 2));
   L.em = reinterpret_cast<Emit*>(smem + o); o += align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1));
   L.path = reinterpret_cast<uint16_t*>(smem + o); o += align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1));
   L.plane = reinterpret_cast<float*>(smem + o); o += align16(sizeof(float) * RC);
   L.meta = reinterpret_cast<int*>(smem + o);
   return L;
+}
+
+// The padded stop map for tile grid g (any stride-C byte array: LDS or HBM).
+template <int NT>
+__device__ __forceinline__ void build_wall_map(const uint8_t* g, const EnvLds& L, int R, int C) {
+  const int PC = C + 2;
+  for (int i = threadIdx.x; i < (R + 2) * PC; i += NT) {
+    const int r = i / PC - 1, c = i - (r + 1) * PC - 1;
+    const bool out = (unsigned)r >= (unsigned)R || (unsigned)c >= (unsigned)C;
+    L.wall[i] = out ? 1 : (g[r * C + c] == kWall ? 1 : 0);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -82,10 +98,19 @@ __device__ __forceinline__ EnvLds carve(unsigned char* smem, int RC, int n_emit,
 // duplicated integer samples of security.py:78-82 are idempotent and skipped); guard
 // rays sample dist = 1..range.  A wall or the grid edge ends the ray; the emitter's own
 // tile is never marked by its rays.
-template <int NT>
+//
+// A sample moves at most one tile per axis from the previous one, so the first sample
+// that leaves the grid lands on the stop map's outer ring: clamping (r, c) to
+// [-1, R] x [-1, C] makes every lookup unconditional.  U samples of a ray are computed,
+// their U stop-map reads issued together, then the vis stores go out branch-free (a
+// masked sample writes the sink byte vis[RC]).
+template <int NT, int U>
 __device__ void cast_rays(const EnvLds& L, int R, int C) {
   const int n_em = L.meta[0];
   const int total = L.meta[1];
+  const int PC = C + 2;
+  const uint8_t* wb = L.wall + PC + 1;  // wb[r * PC + c] for r in [-1, R], c in [-1, C]
+  const int sink = R * C;
   int k = 0;
   for (int j = threadIdx.x; j < total; j += NT) {
     while (k + 1 < n_em && L.em[k + 1].first <= j) ++k;
@@ -93,41 +118,35 @@ __device__ void cast_rays(const EnvLds& L, int R, int C) {
     const int i = j - E.first;
     const double angle = E.hmh + (E.fov * (double)i) / (double)E.num_rays;  // security.py:70
     const double rad = angle * kDegToRad;                                   // math.radians
-    double dx, dy;
-    if (L.meta[2]) {
-      heist_trig::sincos(rad, L.tab, &dy, &dx);
-      dy = -dy;
-    } else {
-      dx = heist_trig::cos(rad, L.tab);
-      dy = -heist_trig::sin(rad, L.tab);
-    }
+    double sn, cs;
+    heist_trig::sincos(rad, L.tab, &sn, &cs);
+    // dist = stride * s with stride a power of two, so dx * dist == (dx * stride) * s
+    // bit for bit; dy = -sin (security.py:72-75).
     const double stride = E.kind == 0 ? 0.5 : 1.0;
+    const double dxs = cs * stride, dys = -sn * stride;
     const int n_samp = E.kind == 0 ? 2 * E.range : E.range;
     const double col = (double)E.col, row = (double)E.row;
-    for (int s0 = 1; s0 <= n_samp; s0 += 4) {
-      int cell[4];
-      bool own[4];
+    const int own = E.row * C + E.col;
+    double kd = 1.0;
+    for (int s0 = 1; s0 <= n_samp; s0 += U, kd += (double)U) {
+      int wv[U], cell[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const double dist = stride * (double)(s0 + u);  // exact
-        const double fx = col + dx * dist;
-        const double fy = row + dy * dist;
-        const int c = (int)rint(fx);  // Python round(): half to even
-        const int r = (int)rint(fy);
-        const bool in = s0 + u <= n_samp && (unsigned)r < (unsigned)R && (unsigned)c < (unsigned)C;
-        cell[u] = in ? r * C + c : -1;
-        own[u] = r == E.row && c == E.col;
+      for (int u = 0; u < U; ++u) {
+        const double ku = kd + (double)u;  // exact small integer
+        const double fx = col + dxs * ku;
+        const double fy = row + dys * ku;
+        int c = (int)rint(fx);  // Python round(): half to even
+        int r = (int)rint(fy);
+        c = min(max(c, -1), C);
+        r = min(max(r, -1), R);
+        wv[u] = wb[r * PC + c] | (s0 + u > n_samp ? 1 : 0);
+        cell[u] = r * C + c;
       }
-      int w[4];
+      int stop = 0;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) w[u] = cell[u] >= 0 ? (int)L.grid[cell[u]] : kWall;
-      bool stop = false;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (!stop) {
-          if (w[u] == kWall) stop = true;
-          else if (!own[u]) L.vis[cell[u]] = 1;
-        }
+      for (int u = 0; u < U; ++u) {
+        stop |= wv[u];
+        L.vis[(stop | (cell[u] == own ? 1 : 0)) ? sink : cell[u]] = 1;
       }
       if (stop) break;
     }
@@ -135,9 +154,8 @@ __device__ void cast_rays(const EnvLds& L, int R, int C) {
 }
 
 // One thread turns per-emitter ray counts into the flattened ray index.
-__device__ __forceinline__ void index_rays(const EnvLds& L, int n_em, int trig_mode = 1) {
+__device__ __forceinline__ void index_rays(const EnvLds& L, int n_em) {
   if (threadIdx.x == 0) {
-    L.meta[2] = trig_mode;
     int t = 0;
     for (int k = 0; k < n_em; ++k) {
       L.em[k].first = t;
@@ -167,12 +185,12 @@ __device__ __forceinline__ Emit guard_emit(const Guard& gd) {
 }
 
 // Visibility (visibility.py:31-65) once the emitter table is in LDS and vis is zeroed.
-template <int NT>
+template <int NT, int U>
 __device__ __forceinline__ void raycast_pass(const EnvParams& p, const EnvLds& L, int n_em, int n_cams) {
   __syncthreads();
-  index_rays(L, n_em, p.trig_mode);
+  index_rays(L, n_em);
   __syncthreads();
-  cast_rays<NT>(L, p.R, p.C);
+  cast_rays<NT, U>(L, p.R, p.C);
   __syncthreads();
   const int t = threadIdx.x;
   if (t >= n_cams && t < n_em) {  // a guard's own tile (visibility.py:59)
@@ -221,6 +239,7 @@ __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds
   } else {
     for (int i = t; i < p.RC; i += NT) L.grid[i] = src[i];
   }
+  build_wall_map<NT>(src, L, p.R, p.C);
   const int pw = p.max_guards * p.max_path;
   const uint16_t* ps = p.paths + (size_t)e * pw;
   for (int i = t; i < pw; i += NT) L.path[i] = ps[i];
@@ -311,7 +330,7 @@ __device__ __forceinline__ double guard_heading_after(const EnvParams& p, int dr
 // step / reset
 // ---------------------------------------------------------------------------
 
-template <int W>
+template <int W, int U>
 __global__ __launch_bounds__(64 * W) void step_kernel(EnvParams p, const int64_t* __restrict__ actions,
                                                        float* __restrict__ obs, float* __restrict__ rew,
                                                        double* __restrict__ rew64, uint8_t* __restrict__ done_out,
@@ -320,7 +339,7 @@ __global__ __launch_bounds__(64 * W) void step_kernel(EnvParams p, const int64_t
   extern __shared__ __align__(16) unsigned char smem[];
   const int e = blockIdx.x;
   const int t = threadIdx.x;
-  const EnvLds L = carve(smem, p.RC, p.max_cams + p.max_guards, p.max_guards * p.max_path);
+  const EnvLds L = carve(smem, p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path);
   EnvScalars s = p.scal[e];
   const int n_cams = s.n_cams, n_em = s.n_cams + s.n_guards;
   EmitterRaw raw;
@@ -342,7 +361,7 @@ __global__ __launch_bounds__(64 * W) void step_kernel(EnvParams p, const int64_t
     }
   }
   // 2. cameras rotate, guards patrol (security.py:49-51, :145-159) -- in registers
-  Guard gd = as_guard(raw);  // meaningful on guard threads only
+  uint16_t pos0 = 0;  // a guard thread's patrol start, for the auto-reset below
   if (t < n_cams) {
     Cam cm = as_cam(raw);
     if (act) {
@@ -352,6 +371,8 @@ __global__ __launch_bounds__(64 * W) void step_kernel(EnvParams p, const int64_t
     L.em[t] = cam_emit(cm);
   } else if (t < n_em) {
     const int g = t - n_cams;
+    Guard gd = as_guard(raw);
+    pos0 = gd.pos0;
     if (act && gd.len >= 2) {
       int nidx = gd.idx + gd.step;
       if (nidx >= gd.len) nidx -= gd.len;
@@ -368,7 +389,7 @@ __global__ __launch_bounds__(64 * W) void step_kernel(EnvParams p, const int64_t
     L.em[t] = guard_emit(gd);
   }
   // 3. visibility (environment.py:257-258); an already-done env recomputes the same plane
-  raycast_pass<NT>(p, L, n_em, n_cams);
+  raycast_pass<NT, U>(p, L, n_em, n_cams);
 
   if (act) {
     // 4-5. shaping, detection, vault, timeout (environment.py:235, :261-297)
@@ -401,17 +422,19 @@ __global__ __launch_bounds__(64 * W) void step_kernel(EnvParams p, const int64_t
   }
   const int done_now = s.done;
   if (auto_reset && done_now) {  // block-uniform: the barriers inside are safe
+    __syncthreads();  // every wave has read vis (detection) before it is cleared
     reset_solver(p, s);
     if (t >= n_cams && t < n_em) {  // guards back to patrol point 0, headings carry over (environment.py:204-208)
-      gd.idx = 0;
-      gd.pos = gd.pos0;
       Guard* gp = p.guards + (size_t)e * p.max_guards + (t - n_cams);
       gp->idx = 0;
-      gp->pos = gd.pos0;
-      L.em[t] = guard_emit(gd);
+      gp->pos = pos0;
+      Emit E = L.em[t];  // this tick's heading, fov and range stay
+      E.row = unpack_r(pos0);
+      E.col = unpack_c(pos0);
+      L.em[t] = E;
     }
     clear_vis<NT>(p, L);
-    raycast_pass<NT>(p, L, n_em, n_cams);
+    raycast_pass<NT, U>(p, L, n_em, n_cams);
   }
   write_obs<NT>(p, e, s, L, obs);
   if (t == 0) {
@@ -423,7 +446,7 @@ __global__ __launch_bounds__(64 * W) void step_kernel(EnvParams p, const int64_t
   }
 }
 
-template <int W>
+template <int W, int U>
 __global__ __launch_bounds__(64 * W) void reset_kernel(EnvParams p, const uint8_t* __restrict__ mask,
                                                         float* __restrict__ obs) {
   constexpr int NT = 64 * W;
@@ -431,7 +454,7 @@ __global__ __launch_bounds__(64 * W) void reset_kernel(EnvParams p, const uint8_
   const int e = blockIdx.x;
   const int t = threadIdx.x;
   if (mask && !mask[e]) return;
-  const EnvLds L = carve(smem, p.RC, p.max_cams + p.max_guards, p.max_guards * p.max_path);
+  const EnvLds L = carve(smem, p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path);
   EnvScalars s = p.scal[e];
   const int n_cams = s.n_cams, n_em = s.n_cams + s.n_guards;
   EmitterRaw raw;
@@ -449,7 +472,7 @@ __global__ __launch_bounds__(64 * W) void reset_kernel(EnvParams p, const uint8_
     gp->pos = gd.pos0;
     L.em[t] = guard_emit(gd);
   }
-  raycast_pass<NT>(p, L, n_em, n_cams);
+  raycast_pass<NT, U>(p, L, n_em, n_cams);
   write_obs<NT>(p, e, s, L, obs);
   if (t == 0) p.scal[e] = s;
 }
@@ -604,7 +627,7 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
   const int e = blockIdx.x;
   const int lane = threadIdx.x;
   const int RC = R * C;
-  const EnvLds L = carve(smem, RC, 1, 0);
+  const EnvLds L = carve(smem, R, C, 1, 0);
   const double2* tab2 = reinterpret_cast<const double2*>(kSinCosTab);
   for (int i = lane; i < kTabDoubles / 2; i += 64) reinterpret_cast<double2*>(L.tab)[i] = tab2[i];
   for (int i = lane; i < RC; i += 64) {
@@ -622,10 +645,11 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
     L.em[0] = E;
     L.meta[0] = 1;
     L.meta[1] = E.num_rays + 1;
-    L.meta[2] = 1;
   }
   __syncthreads();
-  cast_rays<64>(L, R, C);
+  build_wall_map<64>(L.grid, L, R, C);
+  __syncthreads();
+  cast_rays<64, 4>(L, R, C);
   __syncthreads();
   for (int i = lane; i < RC; i += 64) out[(size_t)e * RC + i] = L.vis[i];
 }
@@ -684,7 +708,7 @@ __global__ __launch_bounds__(256) void sincos_kernel(const double* __restrict__ 
 // ---------------------------------------------------------------------------
 
 static size_t env_lds(const EnvParams& p) {
-  return env_lds_bytes(p.RC, p.max_cams + p.max_guards, p.max_guards * p.max_path);
+  return env_lds_bytes(p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path);
 }
 
 hipError_t launch_init(const EnvParams& p, hipStream_t st) {
@@ -701,34 +725,33 @@ hipError_t launch_set_layout(const EnvParams& p, int max_walls, const int32_t* w
   return hipGetLastError();
 }
 
+// (waves per env, samples per ray chunk) variants; W = 4, U = 4 is the default.
+#define HEIST_ENV_VARIANTS(X) X(1, 4) X(2, 4) X(4, 4) X(4, 2) X(4, 8)
+
 hipError_t launch_reset(const EnvParams& p, const uint8_t* mask, float* obs, hipStream_t st) {
   const size_t lds = env_lds(p);
-  switch (p.step_waves) {
-    case 1: hipLaunchKernelGGL(reset_kernel<1>, dim3(p.n_envs), dim3(64), lds, st, p, mask, obs); break;
-    case 4: hipLaunchKernelGGL(reset_kernel<4>, dim3(p.n_envs), dim3(256), lds, st, p, mask, obs); break;
-    default: hipLaunchKernelGGL(reset_kernel<2>, dim3(p.n_envs), dim3(128), lds, st, p, mask, obs); break;
+#define HEIST_RESET_CASE(W, U)                                                                     \
+  if (p.step_waves == W && p.ray_chunk == U) {                                                    \
+    hipLaunchKernelGGL((reset_kernel<W, U>), dim3(p.n_envs), dim3(64 * W), lds, st, p, mask, obs); \
+    return hipGetLastError();                                                                     \
   }
-  return hipGetLastError();
+  HEIST_ENV_VARIANTS(HEIST_RESET_CASE)
+#undef HEIST_RESET_CASE
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_step(const EnvParams& p, const int64_t* actions, float* obs, float* rew, double* rew64,
                        uint8_t* done_out, int8_t* status_out, int auto_reset, hipStream_t st) {
   const size_t lds = env_lds(p);
-  switch (p.step_waves) {
-    case 1:
-      hipLaunchKernelGGL(step_kernel<1>, dim3(p.n_envs), dim3(64), lds, st, p, actions, obs, rew, rew64, done_out,
-                         status_out, auto_reset);
-      break;
-    case 4:
-      hipLaunchKernelGGL(step_kernel<4>, dim3(p.n_envs), dim3(256), lds, st, p, actions, obs, rew, rew64, done_out,
-                         status_out, auto_reset);
-      break;
-    default:
-      hipLaunchKernelGGL(step_kernel<2>, dim3(p.n_envs), dim3(128), lds, st, p, actions, obs, rew, rew64, done_out,
-                         status_out, auto_reset);
-      break;
+#define HEIST_STEP_CASE(W, U)                                                                        \
+  if (p.step_waves == W && p.ray_chunk == U) {                                                       \
+    hipLaunchKernelGGL((step_kernel<W, U>), dim3(p.n_envs), dim3(64 * W), lds, st, p, actions, obs, rew, \
+                       rew64, done_out, status_out, auto_reset);                                     \
+    return hipGetLastError();                                                                        \
   }
-  return hipGetLastError();
+  HEIST_ENV_VARIANTS(HEIST_STEP_CASE)
+#undef HEIST_STEP_CASE
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_export(const EnvParams& p, int32_t* scalars, int8_t* grid, double* cam_heading, int32_t* guard_idx,
@@ -746,7 +769,7 @@ hipError_t launch_bfs(const int32_t* grid, int n, int R, int C, int sr, int sc, 
 
 hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
                         uint8_t* out, hipStream_t st) {
-  const size_t lds = env_lds_bytes(R * C, 1, 0);
+  const size_t lds = env_lds_bytes(R, C, 1, 0);
   hipLaunchKernelGGL(cones_kernel, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, out);
   return hipGetLastError();
 }

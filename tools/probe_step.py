@@ -12,9 +12,9 @@ from heist_amd import EnvironmentConfig, HeistEnv  # noqa: E402
 from heist_amd.layouts import synthetic_layouts  # noqa: E402
 
 
-def make(n, budget, n_cams, n_guards, R=20, waves=4, trig=1):
+def make(n, budget, n_cams, n_guards, R=20, waves=4, chunk=4):
     os.environ["HEIST_STEP_WAVES"] = str(waves)
-    os.environ["HEIST_TRIG_MODE"] = str(trig)
+    os.environ["HEIST_RAY_CHUNK"] = str(chunk)
     cfg = EnvironmentConfig(grid_rows=R, grid_cols=R)
     env = HeistEnv(n, cfg, device="cuda")
     lays = synthetic_layouts(n, R, R, budget, seed=1, n_cams=n_cams, n_guards=n_guards)
@@ -38,12 +38,13 @@ def time_env(env, acts, iters=40):
 
 
 cases = {}
-for trig in (0, 1):
-    for n in (1024, 4096, 16384):
-        cases["t%d_n%d_b15" % (trig, n)] = make(n, 15, None, None, trig=trig)
-    for nc, ng in ((4, 0), (0, 2)):
-        cases["t%d_n4096_c%d_g%d" % (trig, nc, ng)] = make(4096, 3 * nc + 5 * ng + 2, nc, ng, trig=trig)
-    cases["t%d_n4096_32x32_c4_g3" % trig] = make(4096, 40, 4, 3, R=32, trig=trig)
+for chunk in (2, 4, 8):  # samples per ray chunk
+    for n in (4096, 16384):
+        cases["u%d_n%d_b15" % (chunk, n)] = make(n, 15, None, None, chunk=chunk)
+    cases["u%d_n4096_c4_g0" % chunk] = make(4096, 14, 4, 0, chunk=chunk)
+cases["w2_n4096_b15"] = make(4096, 15, None, None, waves=2)
+os.environ.pop("HEIST_RAY_CHUNK", None)
+os.environ.pop("HEIST_STEP_WAVES", None)
 res = {k: [] for k in cases}
 for rnd in range(5):
     for k, (env, acts) in cases.items():

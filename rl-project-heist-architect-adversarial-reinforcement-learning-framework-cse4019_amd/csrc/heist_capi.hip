@@ -24,6 +24,8 @@ hipError_t launch_export(const EnvParams& p, int32_t* scalars, int8_t* grid, dou
                          double* guard_heading, hipStream_t st);
 hipError_t launch_bfs(const int32_t* grid, int n, int R, int C, int sr, int sc, int gr, int gc, uint8_t* out,
                       hipStream_t st);
+int vis_gap_for(int R, int C, int U);
+bool env_variant_exists(int W, int U, int O, int D);
 hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
                         uint8_t* out, hipStream_t st);
 hipError_t launch_arch_decode(const int64_t* amap, int n, int R, int C, const float* cam, int cam_stride,
@@ -157,16 +159,18 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
     p.axis_heading[3] = htab[(size_t)(R - 1) * W2 + (1 + C - 1)];
   }
   p.step_waves = 4;
-  p.ray_chunk = 4;
-  if (const char* u = getenv("HEIST_RAY_CHUNK")) {  // tuning knob; unsupported pairs fall back to 4
-    const int v = atoi(u);
-    if (v == 2 || v == 8) p.ray_chunk = v;
+  p.ray_chunk = 4;  // tuning knobs; a combination without a compiled variant falls back to (4, 4, 1)
+  p.step_occ = 1;
+  if (const char* u = getenv("HEIST_RAY_CHUNK")) p.ray_chunk = atoi(u);
+  if (const char* o = getenv("HEIST_STEP_OCC")) p.step_occ = atoi(o);
+  if (const char* w = getenv("HEIST_STEP_WAVES")) p.step_waves = atoi(w);
+  p.vis_gap = heist::vis_gap_for(R, C, p.ray_chunk == 2 ? 2 : 4);
+  if (!heist::env_variant_exists(p.step_waves, p.ray_chunk, p.step_occ, p.vis_gap)) {
+    p.step_waves = 4;
+    p.ray_chunk = 4;
+    p.step_occ = 1;
+    p.vis_gap = heist::vis_gap_for(R, C, 4);
   }
-  if (const char* w = getenv("HEIST_STEP_WAVES")) {
-    const int v = atoi(w);
-    if (v == 1 || v == 2 || v == 4) p.step_waves = v;
-  }
-  if (p.step_waves != 4) p.ray_chunk = 4;
   for (int k = 0; k < 8; ++k) p.tile_lut[k] = k <= 5 ? (float)k / 5.0f : 0.0f;  // environment.py:319
 
   const size_t sizes[] = {

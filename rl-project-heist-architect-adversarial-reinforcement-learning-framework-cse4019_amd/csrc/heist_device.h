@@ -73,7 +73,9 @@ struct EnvParams {
   float tile_lut[8];          // float32(tile) / 5  (environment.py:319)
   double axis_heading[4];     // heading_tab at (dr,dc) = (-1,0), (1,0), (0,-1), (0,1)
   int step_waves;             // wavefronts per env in step/reset (1, 2 or 4)
-  int ray_chunk;              // samples per ray computed together (2, 4, 8)
+  int ray_chunk;              // samples per ray computed together (2, 4)
+  int step_occ;               // min waves per SIMD the step kernel is compiled for (1, 8)
+  int vis_gap;                // LDS distance stop map -> vis plane (1024 or 5376), see heist_env.hip
 };
 
 // security.py:67 max(int(fov * 2), 30); capped at 32000 rays (fov 16000 deg) so the

@@ -46,44 +46,56 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(
 // ---------------------------------------------------------------------------
 
 struct EnvLds {
+  uint8_t* wall;   // LDS offset 0: [(R+2U)(C+2U)] ray stop map, 1 = wall or outside the grid
+  uint8_t* vis;    // LDS offset D: visibility with the same padded geometry (ring bytes unused)
   double* tab;     // [440] glibc sin/cos table
   uint8_t* grid;   // [RC]
-  uint8_t* vis;    // [RC + 1]; vis[RC] is a write sink for masked-off ray samples
-  uint8_t* wall;   // [(R+2)(C+2)] 1 = stops a ray: a wall or the ring just outside the grid
   Emit* em;        // [n_emit]
   uint16_t* path;  // [max_guards][max_path]
   float* plane;    // [RC] static position channel (plane0)
   int* meta;       // [0] emitters, [1] total rays
+  int PC;          // padded row stride C + 2U
+  int off0;        // padded index of tile (0, 0): U * PC + U
+  __device__ __forceinline__ int at(int r, int c) const { return off0 + r * PC + c; }
 };
 
-__host__ __device__ inline size_t env_lds_bytes(int R, int C, int n_emit, int path_words) {
+// The padded planes hold (R + 2U) x (C + 2U) bytes; D is the compile-time distance from
+// the stop map to the visibility plane (so one address serves both), 1024 for grids up to
+// 24 x 24 at U = 4 and 5376 for the 64 x 64 maximum.
+__host__ __device__ inline int padded_bytes(int R, int C, int U) { return (R + 2 * U) * (C + 2 * U); }
+
+__host__ __device__ inline size_t env_lds_bytes(int R, int C, int n_emit, int path_words, int D) {
   const int RC = R * C;
-  return align16(sizeof(double) * kTabDoubles) + align16(RC) + align16(RC + 1) + align16((R + 2) * (C + 2)) +
+  return 2 * (size_t)D + align16(sizeof(double) * kTabDoubles) + align16(RC) +
          align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) +
          align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1)) + align16(sizeof(float) * RC) + 16;
 }
 
+template <int U, int D>
 __device__ __forceinline__ EnvLds carve(unsigned char* smem, int R, int C, int n_emit, int path_words) {
   const int RC = R * C;
   EnvLds L;
-  size_t o = 0;
+  L.wall = smem;
+  L.vis = smem + D;
+  size_t o = 2 * (size_t)D;
   L.tab = reinterpret_cast<double*>(smem + o); o += align16(sizeof(double) * kTabDoubles);
   L.grid = smem + o; o += align16(RC);
-  L.vis = smem + o; o += align16(RC + 1);
-  L.wall = smem + o; o += align16((R + 2) * (C + 2));
   L.em = reinterpret_cast<Emit*>(smem + o); o += align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1));
   L.path = reinterpret_cast<uint16_t*>(smem + o); o += align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1));
   L.plane = reinterpret_cast<float*>(smem + o); o += align16(sizeof(float) * RC);
   L.meta = reinterpret_cast<int*>(smem + o);
+  L.PC = C + 2 * U;
+  L.off0 = U * L.PC + U;
   return L;
 }
 
 // The padded stop map for tile grid g (any stride-C byte array: LDS or HBM).
-template <int NT>
+template <int NT, int U>
 __device__ __forceinline__ void build_wall_map(const uint8_t* g, const EnvLds& L, int R, int C) {
-  const int PC = C + 2;
-  for (int i = threadIdx.x; i < (R + 2) * PC; i += NT) {
-    const int r = i / PC - 1, c = i - (r + 1) * PC - 1;
+  const int PC = L.PC;
+  for (int i = threadIdx.x; i < (R + 2 * U) * PC; i += NT) {
+    const int pr = i / PC;
+    const int r = pr - U, c = i - pr * PC - U;
     const bool out = (unsigned)r >= (unsigned)R || (unsigned)c >= (unsigned)C;
     L.wall[i] = out ? 1 : (g[r * C + c] == kWall ? 1 : 0);
   }
@@ -93,24 +105,56 @@ __device__ __forceinline__ void build_wall_map(const uint8_t* g, const EnvLds& L
 // Raycasting
 // ---------------------------------------------------------------------------
 
+// x + 0x1.8p52 rounds x to an integer half-to-even (Python round()) and leaves it in the
+// low word, exact for |x| < 2^51.  Adding an EVEN offset k to the constant yields
+// round(x) + k with the same tie breaks, which folds the ring offset into the rounding.
+template <int K>
+__device__ __forceinline__ int round_plus(double x) {
+  static_assert((K & 1) == 0, "the offset must be even to keep half-to-even ties");
+  constexpr double kMagic = 0x1.8p52 + (double)K;
+  return (int)(uint32_t)__builtin_bit_cast(uint64_t, x + kMagic);
+}
+
+// U consecutive samples of one ray: positions, U stop-map reads in flight together, then
+// branch-free visibility stores (a masked sample writes byte 0 of the vis plane, a ring
+// byte nobody reads).  TAIL masks samples past the ray's last one (u >= left).
+template <int U, int D, bool TAIL>
+__device__ __forceinline__ bool sample_chunk(unsigned char* smem, int PC, int own, double col, double row,
+                                             double dxs, double dys, double kd, int left) {
+  int a[U], w[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const double ku = kd + (double)u;  // exact small integer
+    const int c = round_plus<U>(col + dxs * ku);  // padded column c + U
+    const int r = round_plus<U>(row + dys * ku);
+    a[u] = __mul24(r, PC) + c;
+    w[u] = smem[a[u]];
+  }
+  bool stop = false;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    stop |= w[u] != 0 || (TAIL && u >= left);
+    smem[D + ((stop || a[u] == own) ? 0 : a[u])] = 1;
+  }
+  return stop;
+}
+
 // Cast every ray of the env's emitters and mark visible tiles (visibility.py:48-57).
 // Camera rays sample dist = 0.5, 1.0, ..., range (np.linspace(0,1,3) sub-steps; the
 // duplicated integer samples of security.py:78-82 are idempotent and skipped); guard
 // rays sample dist = 1..range.  A wall or the grid edge ends the ray; the emitter's own
 // tile is never marked by its rays.
 //
-// A sample moves at most one tile per axis from the previous one, so the first sample
-// that leaves the grid lands on the stop map's outer ring: clamping (r, c) to
-// [-1, R] x [-1, C] makes every lookup unconditional.  U samples of a ray are computed,
-// their U stop-map reads issued together, then the vis stores go out branch-free (a
-// masked sample writes the sink byte vis[RC]).
-template <int NT, int U>
-__device__ void cast_rays(const EnvLds& L, int R, int C) {
+// A sample moves at most one tile per axis from the previous one, and a chunk of U
+// samples only starts while the ray is still inside the grid, so every sample lands
+// within U tiles of the grid: a U-wide ring of stop bytes makes every lookup
+// unconditional, with no clamping.
+template <int NT, int U, int D>
+__device__ void cast_rays(unsigned char* smem, const EnvLds& L) {
+  static_assert(U == 2 || U == 4, "ring offset assumes an even chunk");
   const int n_em = L.meta[0];
   const int total = L.meta[1];
-  const int PC = C + 2;
-  const uint8_t* wb = L.wall + PC + 1;  // wb[r * PC + c] for r in [-1, R], c in [-1, C]
-  const int sink = R * C;
+  const int PC = L.PC;
   int k = 0;
   for (int j = threadIdx.x; j < total; j += NT) {
     while (k + 1 < n_em && L.em[k + 1].first <= j) ++k;
@@ -126,30 +170,17 @@ __device__ void cast_rays(const EnvLds& L, int R, int C) {
     const double dxs = cs * stride, dys = -sn * stride;
     const int n_samp = E.kind == 0 ? 2 * E.range : E.range;
     const double col = (double)E.col, row = (double)E.row;
-    const int own = E.row * C + E.col;
+    const int own = (E.row + U) * PC + (E.col + U);
     double kd = 1.0;
-    for (int s0 = 1; s0 <= n_samp; s0 += U, kd += (double)U) {
-      int wv[U], cell[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const double ku = kd + (double)u;  // exact small integer
-        const double fx = col + dxs * ku;
-        const double fy = row + dys * ku;
-        int c = (int)rint(fx);  // Python round(): half to even
-        int r = (int)rint(fy);
-        c = min(max(c, -1), C);
-        r = min(max(r, -1), R);
-        wv[u] = wb[r * PC + c] | (s0 + u > n_samp ? 1 : 0);
-        cell[u] = r * C + c;
+    int s0 = 1;
+    bool stop = false;
+    for (; s0 + U - 1 <= n_samp; s0 += U, kd += (double)U) {
+      if (sample_chunk<U, D, false>(smem, PC, own, col, row, dxs, dys, kd, U)) {
+        stop = true;
+        break;
       }
-      int stop = 0;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        stop |= wv[u];
-        L.vis[(stop | (cell[u] == own ? 1 : 0)) ? sink : cell[u]] = 1;
-      }
-      if (stop) break;
     }
+    if (!stop && s0 <= n_samp) sample_chunk<U, D, true>(smem, PC, own, col, row, dxs, dys, kd, n_samp - s0 + 1);
   }
 }
 
@@ -185,25 +216,25 @@ __device__ __forceinline__ Emit guard_emit(const Guard& gd) {
 }
 
 // Visibility (visibility.py:31-65) once the emitter table is in LDS and vis is zeroed.
-template <int NT, int U>
-__device__ __forceinline__ void raycast_pass(const EnvParams& p, const EnvLds& L, int n_em, int n_cams) {
+template <int NT, int U, int D>
+__device__ __forceinline__ void raycast_pass(unsigned char* smem, const EnvLds& L, int n_em, int n_cams) {
   __syncthreads();
   index_rays(L, n_em);
   __syncthreads();
-  cast_rays<NT, U>(L, p.R, p.C);
+  cast_rays<NT, U, D>(smem, L);
   __syncthreads();
   const int t = threadIdx.x;
   if (t >= n_cams && t < n_em) {  // a guard's own tile (visibility.py:59)
     const Emit E = L.em[t];
-    L.vis[E.row * p.C + E.col] = 1;
+    L.vis[L.at(E.row, E.col)] = 1;
   }
   __syncthreads();
 }
 
-template <int NT>
+template <int NT, int U>
 __device__ __forceinline__ void clear_vis(const EnvParams& p, const EnvLds& L) {
   uint32_t* v4 = reinterpret_cast<uint32_t*>(L.vis);
-  for (int i = threadIdx.x; i < (p.RC + 3) / 4; i += NT) v4[i] = 0u;
+  for (int i = threadIdx.x; i < (padded_bytes(p.R, p.C, U) + 3) / 4; i += NT) v4[i] = 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -224,7 +255,7 @@ __device__ __forceinline__ Guard as_guard(const EmitterRaw& r) { return __builti
 // Issue every per-env HBM read before the first barrier: sin/cos table, grid, guard
 // paths and the static position plane into LDS; this thread's camera/guard record into
 // registers.  EnvScalars come in through scalar loads.
-template <int NT>
+template <int NT, int U>
 __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds& L, int n_cams, int n_em,
                                          EmitterRaw& raw) {
   const int t = threadIdx.x;
@@ -239,7 +270,7 @@ __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds
   } else {
     for (int i = t; i < p.RC; i += NT) L.grid[i] = src[i];
   }
-  build_wall_map<NT>(src, L, p.R, p.C);
+  build_wall_map<NT, U>(src, L, p.R, p.C);
   const int pw = p.max_guards * p.max_path;
   const uint16_t* ps = p.paths + (size_t)e * pw;
   for (int i = t; i < pw; i += NT) L.path[i] = ps[i];
@@ -272,17 +303,17 @@ __device__ __forceinline__ void patch4(float4& v, int m, float val) {
 // Observation row [3][R][C] (environment.py:347-374): occupancy / 5, visibility, and the
 // position channel (static plane with the solver and vault cells patched; the vault
 // wins if the solver stands on it).
-template <int NT>
+template <int NT, int U>
 __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvScalars& s, const EnvLds& L,
                                           float* __restrict__ obs) {
   const int t = threadIdx.x;
-  const int RC = p.RC;
+  const int RC = p.RC, C = p.C;
   float* o = obs + (size_t)e * 3 * RC;
-  const int solver = s.pos_r * p.C + s.pos_c;
-  const int vault = p.vr * p.C + p.vc;
+  const int solver = s.pos_r * C + s.pos_c;
+  const int vault = p.vr * C + p.vc;
   const float sv = p.plane1[solver];
-  if ((RC & 3) == 0) {
-    const int n4 = RC / 4;
+  if ((C & 3) == 0) {  // a float4 never crosses a row; padded vis rows are 4-byte aligned for U = 4
+    const int n4 = RC / 4, c4 = C / 4;
     float4* o0 = reinterpret_cast<float4*>(o);
     float4* o1 = o0 + n4;
     float4* o2 = o1 + n4;
@@ -290,7 +321,14 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
       const uint32_t b = *reinterpret_cast<const uint32_t*>(L.grid + 4 * q);
       o0[q] = make_float4(p.tile_lut[b & 7], p.tile_lut[(b >> 8) & 7], p.tile_lut[(b >> 16) & 7],
                           p.tile_lut[(b >> 24) & 7]);
-      const uint32_t v = *reinterpret_cast<const uint32_t*>(L.vis + 4 * q);
+      const int r = q / c4;
+      const uint8_t* vp = L.vis + L.at(r, 4 * (q - r * c4));
+      uint32_t v;
+      if ((U & 3) == 0) {
+        v = *reinterpret_cast<const uint32_t*>(vp);
+      } else {
+        v = (uint32_t)vp[0] | ((uint32_t)vp[1] << 8) | ((uint32_t)vp[2] << 16) | ((uint32_t)vp[3] << 24);
+      }
       o1[q] = make_float4((v & 0xff) ? 1.0f : 0.0f, (v & 0xff00) ? 1.0f : 0.0f, (v & 0xff0000) ? 1.0f : 0.0f,
                           (v & 0xff000000u) ? 1.0f : 0.0f);
     }
@@ -305,9 +343,14 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
       const int ch = q / RC;
       const int cell = q - ch * RC;
       float v;
-      if (ch == 0) v = p.tile_lut[L.grid[cell] & 7];
-      else if (ch == 1) v = L.vis[cell] ? 1.0f : 0.0f;
-      else v = cell == vault ? p.vault_val : (cell == solver ? sv : L.plane[cell]);
+      if (ch == 0) {
+        v = p.tile_lut[L.grid[cell] & 7];
+      } else if (ch == 1) {
+        const int r = cell / C;
+        v = L.vis[L.at(r, cell - r * C)] ? 1.0f : 0.0f;
+      } else {
+        v = cell == vault ? p.vault_val : (cell == solver ? sv : L.plane[cell]);
+      }
       o[q] = v;
     }
   }
@@ -330,8 +373,8 @@ __device__ __forceinline__ double guard_heading_after(const EnvParams& p, int dr
 // step / reset
 // ---------------------------------------------------------------------------
 
-template <int W, int U>
-__global__ __launch_bounds__(64 * W) void step_kernel(EnvParams p, const int64_t* __restrict__ actions,
+template <int W, int U, int O, int D>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) void step_kernel(EnvParams p, const int64_t* __restrict__ actions,
                                                        float* __restrict__ obs, float* __restrict__ rew,
                                                        double* __restrict__ rew64, uint8_t* __restrict__ done_out,
                                                        int8_t* __restrict__ status_out, int auto_reset) {
@@ -339,13 +382,13 @@ __global__ __launch_bounds__(64 * W) void step_kernel(EnvParams p, const int64_t
   extern __shared__ __align__(16) unsigned char smem[];
   const int e = blockIdx.x;
   const int t = threadIdx.x;
-  const EnvLds L = carve(smem, p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path);
+  const EnvLds L = carve<U, D>(smem, p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path);
   EnvScalars s = p.scal[e];
   const int n_cams = s.n_cams, n_em = s.n_cams + s.n_guards;
   EmitterRaw raw;
-  prefetch<NT>(p, e, L, n_cams, n_em, raw);
+  prefetch<NT, U>(p, e, L, n_cams, n_em, raw);
   const int a_raw = (int)actions[e];
-  clear_vis<NT>(p, L);
+  clear_vis<NT, U>(p, L);
   const bool act = !s.done;
   __syncthreads();  // grid, paths, table in LDS
 
@@ -389,7 +432,7 @@ __global__ __launch_bounds__(64 * W) void step_kernel(EnvParams p, const int64_t
     L.em[t] = guard_emit(gd);
   }
   // 3. visibility (environment.py:257-258); an already-done env recomputes the same plane
-  raycast_pass<NT, U>(p, L, n_em, n_cams);
+  raycast_pass<NT, U, D>(smem, L, n_em, n_cams);
 
   if (act) {
     // 4-5. shaping, detection, vault, timeout (environment.py:235, :261-297)
@@ -399,7 +442,7 @@ __global__ __launch_bounds__(64 * W) void step_kernel(EnvParams p, const int64_t
     reward += (double)(s.prev_dist - curr) * 0.1;
     s.prev_dist = curr;
     if (curr <= 3 && s.initial_dist > 3) reward += 0.05 * (double)(3 - curr);
-    if (L.vis[s.pos_r * p.C + s.pos_c]) {
+    if (L.vis[L.at(s.pos_r, s.pos_c)]) {
       s.detected = 1;
       reward += p.r_detect;
       s.done = 1;
@@ -433,10 +476,10 @@ __global__ __launch_bounds__(64 * W) void step_kernel(EnvParams p, const int64_t
       E.col = unpack_c(pos0);
       L.em[t] = E;
     }
-    clear_vis<NT>(p, L);
-    raycast_pass<NT, U>(p, L, n_em, n_cams);
+    clear_vis<NT, U>(p, L);
+    raycast_pass<NT, U, D>(smem, L, n_em, n_cams);
   }
-  write_obs<NT>(p, e, s, L, obs);
+  write_obs<NT, U>(p, e, s, L, obs);
   if (t == 0) {
     rew[e] = (float)reward;
     if (rew64) rew64[e] = reward;
@@ -446,20 +489,20 @@ __global__ __launch_bounds__(64 * W) void step_kernel(EnvParams p, const int64_t
   }
 }
 
-template <int W, int U>
-__global__ __launch_bounds__(64 * W) void reset_kernel(EnvParams p, const uint8_t* __restrict__ mask,
+template <int W, int U, int O, int D>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) void reset_kernel(EnvParams p, const uint8_t* __restrict__ mask,
                                                         float* __restrict__ obs) {
   constexpr int NT = 64 * W;
   extern __shared__ __align__(16) unsigned char smem[];
   const int e = blockIdx.x;
   const int t = threadIdx.x;
   if (mask && !mask[e]) return;
-  const EnvLds L = carve(smem, p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path);
+  const EnvLds L = carve<U, D>(smem, p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path);
   EnvScalars s = p.scal[e];
   const int n_cams = s.n_cams, n_em = s.n_cams + s.n_guards;
   EmitterRaw raw;
-  prefetch<NT>(p, e, L, n_cams, n_em, raw);
-  clear_vis<NT>(p, L);
+  prefetch<NT, U>(p, e, L, n_cams, n_em, raw);
+  clear_vis<NT, U>(p, L);
   reset_solver(p, s);
   if (t < n_cams) {
     L.em[t] = cam_emit(as_cam(raw));
@@ -472,8 +515,8 @@ __global__ __launch_bounds__(64 * W) void reset_kernel(EnvParams p, const uint8_
     gp->pos = gd.pos0;
     L.em[t] = guard_emit(gd);
   }
-  raycast_pass<NT, U>(p, L, n_em, n_cams);
-  write_obs<NT>(p, e, s, L, obs);
+  raycast_pass<NT, U, D>(smem, L, n_em, n_cams);
+  write_obs<NT, U>(p, e, s, L, obs);
   if (t == 0) p.scal[e] = s;
 }
 
@@ -620,20 +663,20 @@ __global__ __launch_bounds__(64) void bfs_kernel(const int32_t* __restrict__ gri
   if (lane == 0) out[e] = ok ? 1 : 0;
 }
 
+template <int D>
 __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* __restrict__ walls,
                                                     const int32_t* __restrict__ meta, const double* __restrict__ params,
                                                     uint8_t* __restrict__ out) {
+  constexpr int U = 4;
   extern __shared__ __align__(16) unsigned char smem[];
   const int e = blockIdx.x;
   const int lane = threadIdx.x;
   const int RC = R * C;
-  const EnvLds L = carve(smem, R, C, 1, 0);
+  const EnvLds L = carve<U, D>(smem, R, C, 1, 0);
   const double2* tab2 = reinterpret_cast<const double2*>(kSinCosTab);
   for (int i = lane; i < kTabDoubles / 2; i += 64) reinterpret_cast<double2*>(L.tab)[i] = tab2[i];
-  for (int i = lane; i < RC; i += 64) {
-    L.grid[i] = walls[(size_t)e * RC + i] ? kWall : kEmpty;
-    L.vis[i] = 0;
-  }
+  for (int i = lane; i < RC; i += 64) L.grid[i] = walls[(size_t)e * RC + i] ? kWall : kEmpty;
+  for (int i = lane; i < padded_bytes(R, C, U); i += 64) L.vis[i] = 0;
   if (lane == 0) {
     const int kind = meta[e * 4], row = meta[e * 4 + 1], col = meta[e * 4 + 2], range = meta[e * 4 + 3];
     const double fov = params[e * 2], heading = params[e * 2 + 1];
@@ -647,11 +690,14 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
     L.meta[1] = E.num_rays + 1;
   }
   __syncthreads();
-  build_wall_map<64>(L.grid, L, R, C);
+  build_wall_map<64, U>(L.grid, L, R, C);
   __syncthreads();
-  cast_rays<64, 4>(L, R, C);
+  cast_rays<64, U, D>(smem, L);
   __syncthreads();
-  for (int i = lane; i < RC; i += 64) out[(size_t)e * RC + i] = L.vis[i];
+  for (int i = lane; i < RC; i += 64) {
+    const int r = i / C;
+    out[(size_t)e * RC + i] = L.vis[L.at(r, i - r * C)];
+  }
 }
 
 __global__ void init_kernel(EnvParams p) {
@@ -708,7 +754,7 @@ __global__ __launch_bounds__(256) void sincos_kernel(const double* __restrict__ 
 // ---------------------------------------------------------------------------
 
 static size_t env_lds(const EnvParams& p) {
-  return env_lds_bytes(p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path);
+  return env_lds_bytes(p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path, p.vis_gap);
 }
 
 hipError_t launch_init(const EnvParams& p, hipStream_t st) {
@@ -725,15 +771,27 @@ hipError_t launch_set_layout(const EnvParams& p, int max_walls, const int32_t* w
   return hipGetLastError();
 }
 
-// (waves per env, samples per ray chunk) variants; W = 4, U = 4 is the default.
-#define HEIST_ENV_VARIANTS(X) X(1, 4) X(2, 4) X(4, 4) X(4, 2) X(4, 8)
+// (waves per env W, samples per ray chunk U, min waves per SIMD O, stop-map -> vis gap D)
+// variants; (4, 4, 1, D) is the default for either D.
+#define HEIST_ENV_VARIANTS(X) \
+  X(4, 4, 1, 1024) X(4, 4, 1, 5376) X(1, 4, 1, 1024) X(2, 4, 1, 1024) X(4, 2, 1, 1024) X(4, 4, 8, 1024)
+
+int vis_gap_for(int R, int C, int U) { return padded_bytes(R, C, U) <= 1024 ? 1024 : 5376; }
+
+bool env_variant_exists(int W, int U, int O, int D) {
+#define HEIST_HAS_CASE(W_, U_, O_, D_) \
+  if (W == W_ && U == U_ && O == O_ && D == D_) return true;
+  HEIST_ENV_VARIANTS(HEIST_HAS_CASE)
+#undef HEIST_HAS_CASE
+  return false;
+}
 
 hipError_t launch_reset(const EnvParams& p, const uint8_t* mask, float* obs, hipStream_t st) {
   const size_t lds = env_lds(p);
-#define HEIST_RESET_CASE(W, U)                                                                     \
-  if (p.step_waves == W && p.ray_chunk == U) {                                                    \
-    hipLaunchKernelGGL((reset_kernel<W, U>), dim3(p.n_envs), dim3(64 * W), lds, st, p, mask, obs); \
-    return hipGetLastError();                                                                     \
+#define HEIST_RESET_CASE(W, U, O, D)                                                                    \
+  if (p.step_waves == W && p.ray_chunk == U && p.step_occ == O && p.vis_gap == D) {                    \
+    hipLaunchKernelGGL((reset_kernel<W, U, O, D>), dim3(p.n_envs), dim3(64 * W), lds, st, p, mask, obs); \
+    return hipGetLastError();                                                                          \
   }
   HEIST_ENV_VARIANTS(HEIST_RESET_CASE)
 #undef HEIST_RESET_CASE
@@ -743,11 +801,11 @@ hipError_t launch_reset(const EnvParams& p, const uint8_t* mask, float* obs, hip
 hipError_t launch_step(const EnvParams& p, const int64_t* actions, float* obs, float* rew, double* rew64,
                        uint8_t* done_out, int8_t* status_out, int auto_reset, hipStream_t st) {
   const size_t lds = env_lds(p);
-#define HEIST_STEP_CASE(W, U)                                                                        \
-  if (p.step_waves == W && p.ray_chunk == U) {                                                       \
-    hipLaunchKernelGGL((step_kernel<W, U>), dim3(p.n_envs), dim3(64 * W), lds, st, p, actions, obs, rew, \
-                       rew64, done_out, status_out, auto_reset);                                     \
-    return hipGetLastError();                                                                        \
+#define HEIST_STEP_CASE(W, U, O, D)                                                                       \
+  if (p.step_waves == W && p.ray_chunk == U && p.step_occ == O && p.vis_gap == D) {                      \
+    hipLaunchKernelGGL((step_kernel<W, U, O, D>), dim3(p.n_envs), dim3(64 * W), lds, st, p, actions, obs, \
+                       rew, rew64, done_out, status_out, auto_reset);                                    \
+    return hipGetLastError();                                                                            \
   }
   HEIST_ENV_VARIANTS(HEIST_STEP_CASE)
 #undef HEIST_STEP_CASE
@@ -769,8 +827,12 @@ hipError_t launch_bfs(const int32_t* grid, int n, int R, int C, int sr, int sc, 
 
 hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
                         uint8_t* out, hipStream_t st) {
-  const size_t lds = env_lds_bytes(R, C, 1, 0);
-  hipLaunchKernelGGL(cones_kernel, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, out);
+  const int D = vis_gap_for(R, C, 4);
+  const size_t lds = env_lds_bytes(R, C, 1, 0, D);
+  if (D == 1024)
+    hipLaunchKernelGGL(cones_kernel<1024>, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, out);
+  else
+    hipLaunchKernelGGL(cones_kernel<5376>, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, out);
   return hipGetLastError();
 }
 

@@ -106,11 +106,12 @@ def _oracle_envs(cfg, layouts, budget):
     return envs
 
 
-@pytest.mark.parametrize("R,C,budget,n,T", [(20, 20, 15, 192, 260), (32, 32, 40, 64, 120), (13, 17, 25, 64, 150)])
+@pytest.mark.parametrize("R,C,budget,n,T", [(20, 20, 15, 192, 260), (32, 32, 40, 64, 120), (13, 17, 25, 64, 150),
+                                             (64, 64, 60, 16, 80), (6, 48, 12, 32, 80)])
 def test_batched_auto_reset_vs_oracle(R, C, budget, n, T, gpu_device):
     """Every env of a batch, with in-kernel auto-reset, equals its own oracle replay."""
     cfg = EnvironmentConfig(grid_rows=R, grid_cols=C, max_steps=60 if R != 20 else 200)
-    env = HeistEnv(n, cfg, max_cams=16, max_guards=8, max_path=16, device=gpu_device, auto_reset=True)
+    env = HeistEnv(n, cfg, max_cams=24, max_guards=12, max_path=16, device=gpu_device, auto_reset=True)
     lays = synthetic_layouts(n, R, C, budget, seed=R * 1000 + C)
     env.set_layouts(lays, budget=budget)
     obs = env.reset().cpu().numpy()

@@ -12,9 +12,10 @@ from heist_amd import EnvironmentConfig, HeistEnv  # noqa: E402
 from heist_amd.layouts import synthetic_layouts  # noqa: E402
 
 
-def make(n, budget, n_cams, n_guards, R=20, waves=4, chunk=4):
+def make(n, budget, n_cams, n_guards, R=20, waves=4, chunk=4, occ=1):
     os.environ["HEIST_STEP_WAVES"] = str(waves)
     os.environ["HEIST_RAY_CHUNK"] = str(chunk)
+    os.environ["HEIST_STEP_OCC"] = str(occ)
     cfg = EnvironmentConfig(grid_rows=R, grid_cols=R)
     env = HeistEnv(n, cfg, device="cuda")
     lays = synthetic_layouts(n, R, R, budget, seed=1, n_cams=n_cams, n_guards=n_guards)
@@ -38,13 +39,13 @@ def time_env(env, acts, iters=40):
 
 
 cases = {}
-for chunk in (2, 4, 8):  # samples per ray chunk
+for occ in (1, 8):  # min waves per SIMD the step kernel is compiled for
     for n in (4096, 16384):
-        cases["u%d_n%d_b15" % (chunk, n)] = make(n, 15, None, None, chunk=chunk)
-    cases["u%d_n4096_c4_g0" % chunk] = make(4096, 14, 4, 0, chunk=chunk)
-cases["w2_n4096_b15"] = make(4096, 15, None, None, waves=2)
-os.environ.pop("HEIST_RAY_CHUNK", None)
-os.environ.pop("HEIST_STEP_WAVES", None)
+        cases["o%d_n%d_b15" % (occ, n)] = make(n, 15, None, None, occ=occ)
+    cases["o%d_n4096_c4_g0" % occ] = make(4096, 14, 4, 0, occ=occ)
+    cases["o%d_n4096_c0_g2" % occ] = make(4096, 12, 0, 2, occ=occ)
+for k in ("HEIST_RAY_CHUNK", "HEIST_STEP_WAVES", "HEIST_STEP_OCC"):
+    os.environ.pop(k, None)
 res = {k: [] for k in cases}
 for rnd in range(5):
     for k, (env, acts) in cases.items():

@@ -91,6 +91,11 @@ int heist_step(heist_t h, const int64_t* actions, float* obs_out, float* reward_
 int heist_export(heist_t h, int32_t* scalars, int8_t* grid, double* cam_heading, int32_t* guard_idx,
                  double* guard_heading, heist_stream_t stream);
 
+/* Instrumentation, no reference counterpart: with counter a device pointer to one uint64,
+ * every later heist_step / heist_reset on h atomically adds the number of ray samples it
+ * evaluated (the ALU work figure of SURVEY 8(d)); NULL switches counting off (default). */
+int heist_count_samples(heist_t h, uint64_t* counter);
+
 /* Replaces bfs_path_exists (utils.py:52-85) on a batch of grids [N][R][C] int32. */
 int heist_bfs_valid(const int32_t* grid, int n, int rows, int cols, int start_r, int start_c, int goal_r,
                     int goal_c, uint8_t* valid_out, heist_stream_t stream);

@@ -262,6 +262,12 @@ int heist_export(heist_t h, int32_t* scalars, int8_t* grid, double* cam_heading,
                    "heist_export");
 }
 
+int heist_count_samples(heist_t h, uint64_t* counter) {
+  if (int rc = check_handle(h)) return rc;
+  h->p.sample_counter = reinterpret_cast<unsigned long long*>(counter);
+  return 0;
+}
+
 int heist_bfs_valid(const int32_t* grid, int n, int rows, int cols, int sr, int sc, int gr, int gc, uint8_t* valid_out,
                     heist_stream_t stream) {
   HEIST_REQUIRE(grid && valid_out, "heist_bfs_valid: null pointer");

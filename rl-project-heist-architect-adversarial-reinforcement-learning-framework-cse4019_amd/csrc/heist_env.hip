@@ -117,8 +117,9 @@ __device__ __forceinline__ int round_plus(double x) {
 
 // U consecutive samples of one ray: positions, U stop-map reads in flight together, then
 // branch-free visibility stores (a masked sample writes byte 0 of the vis plane, a ring
-// byte nobody reads).  TAIL masks samples past the ray's last one (u >= left).
-template <int U, int D, bool TAIL>
+// byte nobody reads).  TAIL masks samples past the ray's last one (u >= left).  OWN is the
+// number of leading samples that may land on the emitter's own tile (see cast_rays).
+template <int U, int D, bool TAIL, int OWN>
 __device__ __forceinline__ bool sample_chunk(unsigned char* smem, int PC, int own, double col, double row,
                                              double dxs, double dys, double kd, int left) {
   int a[U], w[U];
@@ -134,9 +135,29 @@ __device__ __forceinline__ bool sample_chunk(unsigned char* smem, int PC, int ow
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     stop |= w[u] != 0 || (TAIL && u >= left);
-    smem[D + ((stop || a[u] == own) ? 0 : a[u])] = 1;
+    const bool skip = stop || (u < OWN && a[u] == own);
+    smem[D + (skip ? 0 : a[u])] = 1;
   }
   return stop;
+}
+
+// All samples of one ray from sample s0 = 1 on; the first chunk is peeled so that only it
+// carries the own-tile test.  Returns the number of samples evaluated (whole chunks).
+template <int U, int D, int OWN>
+__device__ __forceinline__ int march(unsigned char* smem, int PC, int own, double col, double row, double dxs,
+                                     double dys, int n_samp) {
+  double kd = 1.0;
+  int s0 = 1;
+  if (n_samp < U) {
+    sample_chunk<U, D, true, OWN>(smem, PC, own, col, row, dxs, dys, kd, n_samp);
+    return U;
+  }
+  if (sample_chunk<U, D, false, OWN>(smem, PC, own, col, row, dxs, dys, kd, U)) return U;
+  for (s0 += U, kd += (double)U; s0 + U - 1 <= n_samp; s0 += U, kd += (double)U)
+    if (sample_chunk<U, D, false, 0>(smem, PC, own, col, row, dxs, dys, kd, U)) return s0 + U - 1;
+  if (s0 > n_samp) return s0 - 1;
+  sample_chunk<U, D, true, 0>(smem, PC, own, col, row, dxs, dys, kd, n_samp - s0 + 1);
+  return s0 + U - 1;
 }
 
 // Cast every ray of the env's emitters and mark visible tiles (visibility.py:48-57).
@@ -148,14 +169,20 @@ __device__ __forceinline__ bool sample_chunk(unsigned char* smem, int PC, int ow
 // A sample moves at most one tile per axis from the previous one, and a chunk of U
 // samples only starts while the ray is still inside the grid, so every sample lands
 // within U tiles of the grid: a U-wide ring of stop bytes makes every lookup
-// unconditional, with no clamping.
+// unconditional, with no clamping.  Only a camera's first two samples (dist 0.5, 1) can
+// round back to its own tile (|dx|, |dy| < 0.5 cannot both hold beyond dist 1 since
+// dx^2 + dy^2 = 1), and a guard's rays never reach it at dist >= 1 (its tile is marked
+// afterwards anyway), so the own-tile test is confined to the first chunk of cameras.
+//
+// counter (optional): total samples evaluated, the ALU work figure of SURVEY 8(d).
 template <int NT, int U, int D>
-__device__ void cast_rays(unsigned char* smem, const EnvLds& L) {
+__device__ void cast_rays(unsigned char* smem, const EnvLds& L, unsigned long long* counter) {
   static_assert(U == 2 || U == 4, "ring offset assumes an even chunk");
   const int n_em = L.meta[0];
   const int total = L.meta[1];
   const int PC = L.PC;
   int k = 0;
+  unsigned long long n_eval = 0;
   for (int j = threadIdx.x; j < total; j += NT) {
     while (k + 1 < n_em && L.em[k + 1].first <= j) ++k;
     const Emit E = L.em[k];
@@ -166,22 +193,16 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L) {
     heist_trig::sincos(rad, L.tab, &sn, &cs);
     // dist = stride * s with stride a power of two, so dx * dist == (dx * stride) * s
     // bit for bit; dy = -sin (security.py:72-75).
-    const double stride = E.kind == 0 ? 0.5 : 1.0;
-    const double dxs = cs * stride, dys = -sn * stride;
-    const int n_samp = E.kind == 0 ? 2 * E.range : E.range;
     const double col = (double)E.col, row = (double)E.row;
     const int own = (E.row + U) * PC + (E.col + U);
-    double kd = 1.0;
-    int s0 = 1;
-    bool stop = false;
-    for (; s0 + U - 1 <= n_samp; s0 += U, kd += (double)U) {
-      if (sample_chunk<U, D, false>(smem, PC, own, col, row, dxs, dys, kd, U)) {
-        stop = true;
-        break;
-      }
-    }
-    if (!stop && s0 <= n_samp) sample_chunk<U, D, true>(smem, PC, own, col, row, dxs, dys, kd, n_samp - s0 + 1);
+    int done;
+    if (E.kind == 0)
+      done = march<U, D, 2>(smem, PC, own, col, row, cs * 0.5, -sn * 0.5, 2 * E.range);
+    else
+      done = march<U, D, 0>(smem, PC, own, col, row, cs, -sn, E.range);
+    n_eval += (unsigned long long)done;
   }
+  if (counter) atomicAdd(counter, n_eval);
 }
 
 // One thread turns per-emitter ray counts into the flattened ray index.
@@ -217,11 +238,12 @@ __device__ __forceinline__ Emit guard_emit(const Guard& gd) {
 
 // Visibility (visibility.py:31-65) once the emitter table is in LDS and vis is zeroed.
 template <int NT, int U, int D>
-__device__ __forceinline__ void raycast_pass(unsigned char* smem, const EnvLds& L, int n_em, int n_cams) {
+__device__ __forceinline__ void raycast_pass(const EnvParams& p, unsigned char* smem, const EnvLds& L, int n_em,
+                                             int n_cams) {
   __syncthreads();
   index_rays(L, n_em);
   __syncthreads();
-  cast_rays<NT, U, D>(smem, L);
+  cast_rays<NT, U, D>(smem, L, p.sample_counter);
   __syncthreads();
   const int t = threadIdx.x;
   if (t >= n_cams && t < n_em) {  // a guard's own tile (visibility.py:59)
@@ -432,7 +454,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     L.em[t] = guard_emit(gd);
   }
   // 3. visibility (environment.py:257-258); an already-done env recomputes the same plane
-  raycast_pass<NT, U, D>(smem, L, n_em, n_cams);
+  raycast_pass<NT, U, D>(p, smem, L, n_em, n_cams);
 
   if (act) {
     // 4-5. shaping, detection, vault, timeout (environment.py:235, :261-297)
@@ -477,7 +499,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
       L.em[t] = E;
     }
     clear_vis<NT, U>(p, L);
-    raycast_pass<NT, U, D>(smem, L, n_em, n_cams);
+    raycast_pass<NT, U, D>(p, smem, L, n_em, n_cams);
   }
   write_obs<NT, U>(p, e, s, L, obs);
   if (t == 0) {
@@ -515,7 +537,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     gp->pos = gd.pos0;
     L.em[t] = guard_emit(gd);
   }
-  raycast_pass<NT, U, D>(smem, L, n_em, n_cams);
+  raycast_pass<NT, U, D>(p, smem, L, n_em, n_cams);
   write_obs<NT, U>(p, e, s, L, obs);
   if (t == 0) p.scal[e] = s;
 }
@@ -692,7 +714,7 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
   __syncthreads();
   build_wall_map<64, U>(L.grid, L, R, C);
   __syncthreads();
-  cast_rays<64, U, D>(smem, L);
+  cast_rays<64, U, D>(smem, L, nullptr);
   __syncthreads();
   for (int i = lane; i < RC; i += 64) {
     const int r = i / C;

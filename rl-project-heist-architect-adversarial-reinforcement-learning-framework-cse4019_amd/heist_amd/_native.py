@@ -31,6 +31,7 @@ SIGNATURES = {
     "heist_reset": (_i, [_vp, _vp, _vp, _vp]),
     "heist_step": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
     "heist_export": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "heist_count_samples": (_i, [_vp, _vp]),
     "heist_bfs_valid": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "heist_cones": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     "heist_architect_decode": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp,

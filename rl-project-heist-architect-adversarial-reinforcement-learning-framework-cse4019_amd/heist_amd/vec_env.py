@@ -237,6 +237,16 @@ class HeistEnv:
             out["grid"] = gr
         return out
 
+    def count_samples(self, counter: Optional[torch.Tensor]) -> None:
+        """Instrumentation (no reference counterpart): later step/reset calls add the number of
+        ray samples they evaluate to ``counter`` (one int64 on this device, zeroed by the
+        caller) -- the ALU work figure of SURVEY 8(d).  ``None`` switches counting off."""
+        if counter is not None and (counter.dtype != torch.int64 or counter.numel() != 1
+                                    or counter.device != self.device):
+            raise ValueError("count_samples: need a one-element int64 tensor on %s" % self.device)
+        nat.check(nat.lib().heist_count_samples(self._h, nat.ptr(counter)), "heist_count_samples")
+        self._counter = counter  # keep the buffer alive while the library holds its pointer
+
     @property
     def visibility(self) -> torch.Tensor:
         """Current visibility plane [N, R, C] (obs channel 1)."""

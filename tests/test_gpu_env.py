@@ -171,3 +171,34 @@ def test_step_after_done_without_auto_reset(gpu_device):
     _, rew, done, status = env.step(torch.zeros(2, dtype=torch.int64))
     assert bool(done.all()) and (status == 4).all() and float(rew.abs().sum()) == 0.0
     assert torch.equal(env.obs, obs_before)
+
+
+def test_sample_counter_work_figure(gpu_device):
+    """heist_count_samples: an unobstructed camera ray evaluates all 2*range samples, a guard
+    ray all range samples; counting leaves the results unchanged."""
+    cfg = EnvironmentConfig()
+    fov = 60.0
+    lay = ([], [{"row": 10, "col": 10, "fov_angle": fov, "heading": 0.0, "rotation_speed": 15.0,
+                 "vision_range": 6}],
+           [{"patrol_path": [(5, 5), (5, 6)], "speed": 1, "vision_range": 4, "fov_angle": 90.0}])
+    envs = [HeistEnv(2, cfg, device=gpu_device) for _ in range(2)]
+    for e in envs:
+        e.set_layouts([lay, lay], budget=40)
+    cnt = torch.zeros(1, dtype=torch.int64, device=gpu_device)
+    envs[0].count_samples(cnt)
+    per_pass = 2 * ((max(int(fov * 2), 30) + 1) * 12 + (max(int(90.0 * 2), 30) + 1) * 4)
+    outs = []
+    for e in envs:
+        e.reset()
+        seq = [e.obs.clone()]
+        for _ in range(3):
+            obs, _, done, _ = e.step(torch.tensor([0, 4]))
+            assert not bool(done.any())  # no auto-reset pass in the count
+            seq.append(obs.clone())
+        outs.append(seq)
+    assert int(cnt.item()) == 4 * per_pass
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    envs[0].count_samples(None)
+    envs[0].step(torch.tensor([0, 0]))
+    assert int(cnt.item()) == 4 * per_pass

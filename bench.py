@@ -140,22 +140,35 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events bracket the timed launches on the stream they run on; their span / K is the
+    # mean launch duration (it includes the small inter-launch gaps, so it is conservative)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    e0.record(stream)
     for k in range(args.steps):
-        ev[k][0].record(stream)
         env.step(actions[args.warmup + k])
-        ev[k][1].record(stream)
+    e1.record(stream)
+    issue_s = time.perf_counter() - t0
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    kern_ms = e0.elapsed_time(e1) / args.steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # ALU work figure: ray samples evaluated per env-step, counted by the
+    # kernel on extra steps after the timed region
+    cnt = torch.zeros(N, dtype=torch.int64, device=dev)
+    env.count_samples(cnt)
+    n_count = 8
+    for k in range(n_count):
+        env.step(actions[k])
+    env.count_samples(None)
+    samples_per_step = float(cnt.sum().item()) / (n_count * N)
 
     ncam = float(np.mean([len(c) for _, c, _ in layouts]))
     ngu = float(np.mean([len(g) for _, _, g in layouts]))
@@ -181,7 +194,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "heist::step_kernel", "kernel_ms": kern_ms,
-                         "algorithmic_bytes_per_env_step": b_step},
+                         "algorithmic_bytes_per_env_step": b_step,
+                         "ray_samples_per_env_step": samples_per_step,
+                         "host_issue_us_per_step": issue_s / args.steps * 1e6},
             "cpu_baseline": None,
         }
         if not args.no_secondary:

@@ -91,9 +91,9 @@ int heist_step(heist_t h, const int64_t* actions, float* obs_out, float* reward_
 int heist_export(heist_t h, int32_t* scalars, int8_t* grid, double* cam_heading, int32_t* guard_idx,
                  double* guard_heading, heist_stream_t stream);
 
-/* Instrumentation, no reference counterpart: with counter a device pointer to one uint64,
- * every later heist_step / heist_reset on h atomically adds the number of ray samples it
- * evaluated (the ALU work figure of SURVEY 8(d)); NULL switches counting off (default). */
+/* Instrumentation, no reference counterpart: with counter a device array of n_envs uint64,
+ * every later heist_step / heist_reset on h adds to counter[e] the number of ray samples
+ * env e evaluated (the ALU work figure of SURVEY 8(d)); NULL switches counting off (default). */
 int heist_count_samples(heist_t h, uint64_t* counter);
 
 /* Replaces bfs_path_exists (utils.py:52-85) on a batch of grids [N][R][C] int32. */

@@ -76,7 +76,7 @@ struct EnvParams {
   int ray_chunk;              // samples per ray computed together (2, 4)
   int step_occ;               // min waves per SIMD the step kernel is compiled for (1, 8)
   int vis_gap;                // LDS distance stop map -> vis plane (1024 or 5376), see heist_env.hip
-  unsigned long long* sample_counter;  // optional: ray samples evaluated (work figure), else null
+  unsigned long long* sample_counter;  // optional [n_envs]: ray samples evaluated per env, else null
 };
 
 // security.py:67 max(int(fov * 2), 30); capped at 32000 rays (fov 16000 deg) so the

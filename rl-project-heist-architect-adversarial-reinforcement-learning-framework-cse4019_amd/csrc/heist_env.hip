@@ -174,15 +174,16 @@ __device__ __forceinline__ int march(unsigned char* smem, int PC, int own, doubl
 // dx^2 + dy^2 = 1), and a guard's rays never reach it at dist >= 1 (its tile is marked
 // afterwards anyway), so the own-tile test is confined to the first chunk of cameras.
 //
-// counter (optional): total samples evaluated, the ALU work figure of SURVEY 8(d).
+// counter (optional): samples evaluated are summed in LDS meta[2] (the ALU work figure of
+// SURVEY 8(d)); raycast_pass adds the env's total to its slot.
 template <int NT, int U, int D>
-__device__ void cast_rays(unsigned char* smem, const EnvLds& L, unsigned long long* counter) {
+__device__ void cast_rays(unsigned char* smem, const EnvLds& L, const unsigned long long* counter) {
   static_assert(U == 2 || U == 4, "ring offset assumes an even chunk");
   const int n_em = L.meta[0];
   const int total = L.meta[1];
   const int PC = L.PC;
   int k = 0;
-  unsigned long long n_eval = 0;
+  unsigned int n_eval = 0;
   for (int j = threadIdx.x; j < total; j += NT) {
     while (k + 1 < n_em && L.em[k + 1].first <= j) ++k;
     const Emit E = L.em[k];
@@ -200,9 +201,9 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, unsigned long lo
       done = march<U, D, 2>(smem, PC, own, col, row, cs * 0.5, -sn * 0.5, 2 * E.range);
     else
       done = march<U, D, 0>(smem, PC, own, col, row, cs, -sn, E.range);
-    n_eval += (unsigned long long)done;
+    n_eval += (unsigned int)done;
   }
-  if (counter) atomicAdd(counter, n_eval);
+  if (counter) atomicAdd(reinterpret_cast<unsigned int*>(&L.meta[2]), (unsigned int)n_eval);
 }
 
 // One thread turns per-emitter ray counts into the flattened ray index.
@@ -215,6 +216,7 @@ __device__ __forceinline__ void index_rays(const EnvLds& L, int n_em) {
     }
     L.meta[0] = n_em;
     L.meta[1] = t;
+    L.meta[2] = 0;
   }
 }
 
@@ -250,6 +252,7 @@ __device__ __forceinline__ void raycast_pass(const EnvParams& p, unsigned char* 
     const Emit E = L.em[t];
     L.vis[L.at(E.row, E.col)] = 1;
   }
+  if (p.sample_counter && t == 0) p.sample_counter[blockIdx.x] += (unsigned int)L.meta[2];
   __syncthreads();
 }
 

@@ -129,6 +129,8 @@ class HeistEnv:
         self.reward64 = torch.zeros(self.n_envs, dtype=torch.float64, **kw)
         self.done = torch.zeros(self.n_envs, dtype=torch.uint8, **kw)
         self.status = torch.zeros(self.n_envs, dtype=torch.int8, **kw)
+        self._done_bool = self.done.view(torch.bool)
+        self._bufs = tuple(t.data_ptr() for t in (self.obs, self.reward, self.reward64, self.done, self.status))
         self.valid = torch.zeros(self.n_envs, dtype=torch.uint8, **kw)
 
     # -- lifecycle ---------------------------------------------------------------
@@ -207,15 +209,34 @@ class HeistEnv:
         return self.obs
 
     def step(self, actions: torch.Tensor, auto_reset: Optional[bool] = None, obs_out: torch.Tensor = None):
-        """HeistEnvironment.step + get_state_tensor for all envs (environment.py:216-299)."""
-        a = actions.to(device=self.device, dtype=torch.int64).contiguous()
+        """HeistEnvironment.step + get_state_tensor for all envs (environment.py:216-299).
+
+        The per-call host path is kept short (cached buffer addresses, no device switch
+        when the handle's device is current) so that back-to-back steps stay GPU-bound."""
+        a = actions
+        if a.device != self.device or a.dtype != torch.int64 or not a.is_contiguous():
+            a = a.to(device=self.device, dtype=torch.int64).contiguous()
+        if a.numel() != self.n_envs:
+            raise ValueError("step: %d actions for %d envs" % (a.numel(), self.n_envs))
         ar = self.auto_reset if auto_reset is None else auto_reset
-        obs = self.obs if obs_out is None else obs_out
-        with torch.cuda.device(self.device):
-            nat.check(nat.lib().heist_step(self._h, nat.ptr(a), nat.ptr(obs), nat.ptr(self.reward),
-                                           nat.ptr(self.reward64), nat.ptr(self.done), nat.ptr(self.status),
-                                           1 if ar else 0, self._stream()), "heist_step")
-        return obs, self.reward, self.done.view(torch.bool), self.status
+        if obs_out is None:
+            obs, optr = self.obs, self._bufs[0]
+        else:
+            if (obs_out.shape != self.obs.shape or obs_out.dtype != torch.float32 or obs_out.device != self.device
+                    or not obs_out.is_contiguous()):
+                raise ValueError("step: obs_out must be a contiguous float32 %s tensor on %s"
+                                 % (tuple(self.obs.shape), self.device))
+            obs, optr = obs_out, obs_out.data_ptr()
+        L = nat.lib()
+        if torch.cuda.current_device() == self.device.index:
+            rc = L.heist_step(self._h, a.data_ptr(), optr, *self._bufs[1:], 1 if ar else 0,
+                              torch.cuda.current_stream(self.device).cuda_stream)
+        else:
+            with torch.cuda.device(self.device):
+                rc = L.heist_step(self._h, a.data_ptr(), optr, *self._bufs[1:], 1 if ar else 0,
+                                  torch.cuda.current_stream(self.device).cuda_stream)
+        nat.check(rc, "heist_step")
+        return obs, self.reward, self._done_bool, self.status
 
     # -- introspection -------------------------------------------------------------
     def export(self, grid: bool = False) -> dict:
@@ -239,11 +260,11 @@ class HeistEnv:
 
     def count_samples(self, counter: Optional[torch.Tensor]) -> None:
         """Instrumentation (no reference counterpart): later step/reset calls add the number of
-        ray samples they evaluate to ``counter`` (one int64 on this device, zeroed by the
-        caller) -- the ALU work figure of SURVEY 8(d).  ``None`` switches counting off."""
-        if counter is not None and (counter.dtype != torch.int64 or counter.numel() != 1
-                                    or counter.device != self.device):
-            raise ValueError("count_samples: need a one-element int64 tensor on %s" % self.device)
+        ray samples env e evaluates to ``counter[e]`` (int64 [n_envs] on this device, zeroed by
+        the caller) -- the ALU work figure of SURVEY 8(d).  ``None`` switches counting off."""
+        if counter is not None and (counter.dtype != torch.int64 or counter.numel() != self.n_envs
+                                    or counter.device != self.device or not counter.is_contiguous()):
+            raise ValueError("count_samples: need a contiguous int64 [%d] tensor on %s" % (self.n_envs, self.device))
         nat.check(nat.lib().heist_count_samples(self._h, nat.ptr(counter)), "heist_count_samples")
         self._counter = counter  # keep the buffer alive while the library holds its pointer
 

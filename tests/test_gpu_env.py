@@ -184,9 +184,9 @@ def test_sample_counter_work_figure(gpu_device):
     envs = [HeistEnv(2, cfg, device=gpu_device) for _ in range(2)]
     for e in envs:
         e.set_layouts([lay, lay], budget=40)
-    cnt = torch.zeros(1, dtype=torch.int64, device=gpu_device)
+    cnt = torch.zeros(2, dtype=torch.int64, device=gpu_device)
     envs[0].count_samples(cnt)
-    per_pass = 2 * ((max(int(fov * 2), 30) + 1) * 12 + (max(int(90.0 * 2), 30) + 1) * 4)
+    per_pass = (max(int(fov * 2), 30) + 1) * 12 + (max(int(90.0 * 2), 30) + 1) * 4
     outs = []
     for e in envs:
         e.reset()
@@ -196,9 +196,9 @@ def test_sample_counter_work_figure(gpu_device):
             assert not bool(done.any())  # no auto-reset pass in the count
             seq.append(obs.clone())
         outs.append(seq)
-    assert int(cnt.item()) == 4 * per_pass
+    assert cnt.tolist() == [4 * per_pass] * 2
     for a, b in zip(*outs):
         assert torch.equal(a, b)
     envs[0].count_samples(None)
     envs[0].step(torch.tensor([0, 0]))
-    assert int(cnt.item()) == 4 * per_pass
+    assert cnt.tolist() == [4 * per_pass] * 2

@@ -1,0 +1,54 @@
+"""Turn the rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py into the per-launch
+HBM traffic figure bench.py reports as roofline.traffic (profiles/heist_step_traffic.json).
+
+gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts 128-B requests at
+64 B, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane streaming stores.  Counters
+are in KB (rocprofv3 derived metrics).  Only heist::step_kernel dispatches are used.
+
+    python tools/pmc_traffic.py gpurun_out/<tag>/pmc_fetch gpurun_out/<tag>/pmc_write [--envs 4096]
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import statistics
+
+
+def per_dispatch(d, counter):
+    vals = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "step_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                key = r.get("Dispatch_Id") or r.get("Correlation_Id")
+                vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                  "profiles", "heist_step_traffic.json"))
+    a = ap.parse_args()
+    fetch = per_dispatch(a.fetch_dir, "FETCH_SIZE")
+    write = per_dispatch(a.write_dir, "WRITE_SIZE")
+    f_kb, w_kb = statistics.median(fetch), statistics.median(write)
+    fetch_b = 2 * f_kb * 1024.0
+    write_b = w_kb * 1024.0
+    out = {"kernel": "heist::step_kernel", "envs": a.envs, "dispatches": [len(fetch), len(write)],
+           "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
+           "fetch_bytes_corrected": fetch_b, "write_bytes": write_b,
+           "hbm_bytes_per_launch": fetch_b + write_b,
+           "hbm_bytes_per_env_step": (fetch_b + write_b) / a.envs,
+           "note": "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B); Infinity-Cache hits are "
+                   "counted by these memory-side counters"}
+    with open(a.out, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -21,8 +21,6 @@ namespace heist {
 
 __constant__ double kSinCosTab[4 * HEIST_SINCOS_TAB_ROWS] = HEIST_SINCOS_TAB_INIT;
 constexpr int kTabDoubles = 4 * HEIST_SINCOS_TAB_ROWS;
-__constant__ int kActDR[5] = {0, -1, 1, 0, 0};  // environment.py:52-58
-__constant__ int kActDC[5] = {0, 0, 0, -1, 1};
 
 __device__ __forceinline__ int iabs_(int a) { return a < 0 ? -a : a; }
 __device__ __forceinline__ int unpack_r(uint16_t v) { return v & 0xff; }
@@ -89,7 +87,7 @@ __device__ __forceinline__ EnvLds carve(unsigned char* smem, int R, int C, int n
   return L;
 }
 
-// The padded stop map for tile grid g (any stride-C byte array: LDS or HBM).
+// The padded stop map for tile grid g (stride C bytes in LDS).
 template <int NT, int U>
 __device__ __forceinline__ void build_wall_map(const uint8_t* g, const EnvLds& L, int R, int C) {
   const int PC = L.PC;
@@ -278,27 +276,39 @@ __device__ __forceinline__ Cam as_cam(const EmitterRaw& r) { return __builtin_bi
 __device__ __forceinline__ Guard as_guard(const EmitterRaw& r) { return __builtin_bit_cast(Guard, r); }
 
 // Issue every per-env HBM read before the first barrier: sin/cos table, grid, guard
-// paths and the static position plane into LDS; this thread's camera/guard record into
-// registers.  EnvScalars come in through scalar loads.
-template <int NT, int U>
+// paths and the static position plane (for LDS), this thread's camera/guard record (for
+// registers).  Each thread's first element of every array is loaded before anything is
+// stored, so the whole prefetch is one memory round trip; the loops only cover what one
+// pass of NT threads cannot (W < 4, grids above 32 x 32, long patrol paths).  EnvScalars
+// come in through scalar loads.  The stop map is built from the LDS grid after the barrier.
+template <int NT>
 __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds& L, int n_cams, int n_em,
                                          EmitterRaw& raw) {
   const int t = threadIdx.x;
+  const int RC = p.RC;
+  constexpr int kTab2 = kTabDoubles / 2;
   const double2* tab2 = reinterpret_cast<const double2*>(kSinCosTab);
   double2* ltab2 = reinterpret_cast<double2*>(L.tab);
-  for (int i = t; i < kTabDoubles / 2; i += NT) ltab2[i] = tab2[i];
-  const uint8_t* src = p.grid + (size_t)e * p.RC;
-  if ((p.RC & 3) == 0) {
-    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
-    uint32_t* d4 = reinterpret_cast<uint32_t*>(L.grid);
-    for (int i = t; i < p.RC / 4; i += NT) d4[i] = s4[i];
-  } else {
-    for (int i = t; i < p.RC; i += NT) L.grid[i] = src[i];
-  }
-  build_wall_map<NT, U>(src, L, p.R, p.C);
+  const uint8_t* src = p.grid + (size_t)e * RC;
   const int pw = p.max_guards * p.max_path;
   const uint16_t* ps = p.paths + (size_t)e * pw;
-  for (int i = t; i < pw; i += NT) L.path[i] = ps[i];
+  const bool vec = (RC & 3) == 0;
+  const int n4 = vec ? RC / 4 : 0;
+  const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
+  const float4* pl0 = reinterpret_cast<const float4*>(p.plane0);
+  uint32_t* d4 = reinterpret_cast<uint32_t*>(L.grid);
+  float4* lp = reinterpret_cast<float4*>(L.plane);
+
+  double2 tv = make_double2(0.0, 0.0);
+  uint32_t gv = 0u;
+  float4 pv = make_float4(0.f, 0.f, 0.f, 0.f);
+  uint16_t wv = 0;
+  if (t < kTab2) tv = tab2[t];
+  if (t < n4) {
+    gv = s4[t];
+    pv = pl0[t];
+  }
+  if (t < pw) wv = ps[t];
   raw.a = make_uint4(0u, 0u, 0u, 0u);
   raw.b = raw.a;
   if (t < n_em) {
@@ -307,13 +317,24 @@ __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds
     raw.a = rs[0];
     raw.b = rs[1];
   }
-  if ((p.RC & 3) == 0) {
-    const float4* pl0 = reinterpret_cast<const float4*>(p.plane0);
-    float4* lp = reinterpret_cast<float4*>(L.plane);
-    for (int i = t; i < p.RC / 4; i += NT) lp[i] = pl0[i];
-  } else {
-    for (int i = t; i < p.RC; i += NT) L.plane[i] = p.plane0[i];
+  if (t < kTab2) ltab2[t] = tv;
+  if (t < n4) {
+    d4[t] = gv;
+    lp[t] = pv;
   }
+  if (t < pw) L.path[t] = wv;
+  for (int i = t + NT; i < kTab2; i += NT) ltab2[i] = tab2[i];
+  for (int i = t + NT; i < n4; i += NT) {
+    d4[i] = s4[i];
+    lp[i] = pl0[i];
+  }
+  if (!vec) {
+    for (int i = t; i < RC; i += NT) {
+      L.grid[i] = src[i];
+      L.plane[i] = p.plane0[i];
+    }
+  }
+  for (int i = t + NT; i < pw; i += NT) L.path[i] = ps[i];
 }
 
 // Set lane m (0..3) of v; m outside 0..3 leaves v unchanged (no dynamic indexing:
@@ -336,7 +357,7 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
   float* o = obs + (size_t)e * 3 * RC;
   const int solver = s.pos_r * C + s.pos_c;
   const int vault = p.vr * C + p.vc;
-  const float sv = p.plane1[solver];
+  const float sv = 1.0f + L.plane[solver];  // == plane1[solver]: fl32(1 + g) (see heist_create)
   if ((C & 3) == 0) {  // a float4 never crosses a row; padded vis rows are 4-byte aligned for U = 4
     const int n4 = RC / 4, c4 = C / 4;
     float4* o0 = reinterpret_cast<float4*>(o);
@@ -411,18 +432,20 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   EnvScalars s = p.scal[e];
   const int n_cams = s.n_cams, n_em = s.n_cams + s.n_guards;
   EmitterRaw raw;
-  prefetch<NT, U>(p, e, L, n_cams, n_em, raw);
+  prefetch<NT>(p, e, L, n_cams, n_em, raw);
   const int a_raw = (int)actions[e];
   clear_vis<NT, U>(p, L);
   const bool act = !s.done;
   __syncthreads();  // grid, paths, table in LDS
+  build_wall_map<NT, U>(L.grid, L, p.R, p.C);  // read by the raycast after its first barrier
 
   double reward = 0.0;
   int status = kAlreadyDone;
   if (act) {
     // 1. move (environment.py:239-246)
     const int a = (a_raw < 0 || a_raw > 4) ? 0 : a_raw;
-    const int nr = s.pos_r + kActDR[a], nc = s.pos_c + kActDC[a];
+    // environment.py:52-58: 0 stay, 1 up, 2 down, 3 left, 4 right
+    const int nr = s.pos_r + (a == 1 ? -1 : (a == 2 ? 1 : 0)), nc = s.pos_c + (a == 3 ? -1 : (a == 4 ? 1 : 0));
     if (nr >= 0 && nr < p.R && nc >= 0 && nc < p.C && L.grid[nr * p.C + nc] != kWall) {
       s.pos_r = nr;
       s.pos_c = nc;
@@ -526,8 +549,10 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   EnvScalars s = p.scal[e];
   const int n_cams = s.n_cams, n_em = s.n_cams + s.n_guards;
   EmitterRaw raw;
-  prefetch<NT, U>(p, e, L, n_cams, n_em, raw);
+  prefetch<NT>(p, e, L, n_cams, n_em, raw);
   clear_vis<NT, U>(p, L);
+  __syncthreads();  // grid in LDS
+  build_wall_map<NT, U>(L.grid, L, p.R, p.C);
   reset_solver(p, s);
   if (t < n_cams) {
     L.em[t] = cam_emit(as_cam(raw));

@@ -204,17 +204,29 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, const unsigned l
   if (counter) atomicAdd(reinterpret_cast<unsigned int*>(&L.meta[2]), (unsigned int)n_eval);
 }
 
-// One thread turns per-emitter ray counts into the flattened ray index.
-__device__ __forceinline__ void index_rays(const EnvLds& L, int n_em) {
-  if (threadIdx.x == 0) {
-    int t = 0;
-    for (int k = 0; k < n_em; ++k) {
-      L.em[k].first = t;
-      t += L.em[k].num_rays + 1;
+// Publish this tick's emitter table: thread t < n_em holds emitter t in E.  Every
+// emitter lives in wave 0 (at most 64 of them), where an exclusive lane scan of the ray
+// counts gives each emitter its first flattened ray index.
+static_assert(kMaxEmitters <= 64, "publish_emitters keeps every emitter in wave 0");
+__device__ __forceinline__ void publish_emitters(const EnvLds& L, Emit E, int n_em) {
+  const int t = threadIdx.x;
+  if (t < 64) {
+    const int cnt = t < n_em ? E.num_rays + 1 : 0;
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(incl, d, 64);
+      if (t >= d) incl += v;
     }
-    L.meta[0] = n_em;
-    L.meta[1] = t;
-    L.meta[2] = 0;
+    if (t < n_em) {
+      E.first = incl - cnt;
+      L.em[t] = E;
+    }
+    if (t == 63) {
+      L.meta[0] = n_em;
+      L.meta[1] = incl;
+      L.meta[2] = 0;
+    }
   }
 }
 
@@ -240,18 +252,15 @@ __device__ __forceinline__ Emit guard_emit(const Guard& gd) {
 template <int NT, int U, int D>
 __device__ __forceinline__ void raycast_pass(const EnvParams& p, unsigned char* smem, const EnvLds& L, int n_em,
                                              int n_cams) {
-  __syncthreads();
-  index_rays(L, n_em);
-  __syncthreads();
-  cast_rays<NT, U, D>(smem, L, p.sample_counter);
-  __syncthreads();
+  __syncthreads();  // emitter table, stop map and cleared vis in place
   const int t = threadIdx.x;
-  if (t >= n_cams && t < n_em) {  // a guard's own tile (visibility.py:59)
+  if (t >= n_cams && t < n_em) {  // a guard's own tile (visibility.py:59); rays only ever add tiles
     const Emit E = L.em[t];
     L.vis[L.at(E.row, E.col)] = 1;
   }
-  if (p.sample_counter && t == 0) p.sample_counter[blockIdx.x] += (unsigned int)L.meta[2];
+  cast_rays<NT, U, D>(smem, L, p.sample_counter);
   __syncthreads();
+  if (p.sample_counter && t == 0) p.sample_counter[blockIdx.x] += (unsigned int)L.meta[2];
 }
 
 template <int NT, int U>
@@ -453,13 +462,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   }
   // 2. cameras rotate, guards patrol (security.py:49-51, :145-159) -- in registers
   uint16_t pos0 = 0;  // a guard thread's patrol start, for the auto-reset below
+  Emit E;
   if (t < n_cams) {
     Cam cm = as_cam(raw);
     if (act) {
       cm.heading = py_mod360(cm.heading + cm.speed * 1.0);
       p.cams[(size_t)e * p.max_cams + t].heading = cm.heading;
     }
-    L.em[t] = cam_emit(cm);
+    E = cam_emit(cm);
   } else if (t < n_em) {
     const int g = t - n_cams;
     Guard gd = as_guard(raw);
@@ -477,8 +487,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
       gp->idx = gd.idx;
       gp->pos = gd.pos;
     }
-    L.em[t] = guard_emit(gd);
+    E = guard_emit(gd);
   }
+  publish_emitters(L, E, n_em);
   // 3. visibility (environment.py:257-258); an already-done env recomputes the same plane
   raycast_pass<NT, U, D>(p, smem, L, n_em, n_cams);
 
@@ -515,15 +526,16 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   if (auto_reset && done_now) {  // block-uniform: the barriers inside are safe
     __syncthreads();  // every wave has read vis (detection) before it is cleared
     reset_solver(p, s);
+    Emit E2;
+    if (t < n_em) E2 = L.em[t];  // this tick's headings, fov and range stay
     if (t >= n_cams && t < n_em) {  // guards back to patrol point 0, headings carry over (environment.py:204-208)
       Guard* gp = p.guards + (size_t)e * p.max_guards + (t - n_cams);
       gp->idx = 0;
       gp->pos = pos0;
-      Emit E = L.em[t];  // this tick's heading, fov and range stay
-      E.row = unpack_r(pos0);
-      E.col = unpack_c(pos0);
-      L.em[t] = E;
+      E2.row = unpack_r(pos0);
+      E2.col = unpack_c(pos0);
     }
+    publish_emitters(L, E2, n_em);
     clear_vis<NT, U>(p, L);
     raycast_pass<NT, U, D>(p, smem, L, n_em, n_cams);
   }
@@ -554,8 +566,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   __syncthreads();  // grid in LDS
   build_wall_map<NT, U>(L.grid, L, p.R, p.C);
   reset_solver(p, s);
+  Emit E;
   if (t < n_cams) {
-    L.em[t] = cam_emit(as_cam(raw));
+    E = cam_emit(as_cam(raw));
   } else if (t < n_em) {
     Guard gd = as_guard(raw);
     gd.idx = 0;
@@ -563,8 +576,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     Guard* gp = p.guards + (size_t)e * p.max_guards + (t - n_cams);
     gp->idx = 0;
     gp->pos = gd.pos0;
-    L.em[t] = guard_emit(gd);
+    E = guard_emit(gd);
   }
+  publish_emitters(L, E, n_em);
   raycast_pass<NT, U, D>(p, smem, L, n_em, n_cams);
   write_obs<NT, U>(p, e, s, L, obs);
   if (t == 0) p.scal[e] = s;

@@ -140,46 +140,68 @@ HEIST_HD double cos(double x, const double* tab) {
   return (n & 2) ? -r : r;
 }
 
-// sin(x) and cos(x) together, bit-identical to sin() and cos() above, without
-// per-branch divergence.  In every glibc branch one of the two values comes from a
-// sin-type kernel (taylor_sin or do_sin) and the other from do_cos, on arguments that
-// depend on the branch; so the arguments are selected per lane, each kernel runs once,
-// and the results are routed and negated afterwards:
-//   |x| < 0.855 (k < 0x3feb6000):  sin = sin_type(x, 0)            cos = do_cos(x, 0)
-//   |x| < 2.426:   t = hp0 - |x|   sin = copysign(do_cos(t, hp1), x)  cos = sin_type(t + hp1, da)
-//   otherwise:     x = n pi/2 + a  sin = (n odd ? do_cos : sin_type)(a, da), cos uses n + 1
-// plus the tiny-argument early returns (sin x = x, cos x = 1).
+// sin-type kernel and do_cos on the SAME argument (a, da), |a| < 0.855: one table row and
+// one r0 = |a| - (u - big) serve both (do_sin / do_cos above, unchanged op for op).
+HEIST_HD void sin_cos_same(double a, double da, const double* tab, double* S, double* D) {
+  const double ax = fabs(a);
+  const double u = kBig + ax;
+  const double* e = tab + 4 * lo_index(u);
+  const double r0 = ax - (u - kBig);
+  {  // do_cos(a, da)
+    const double dxc = a < 0 ? -da : da;
+    const double r = r0 + dxc;
+    const double xx = r * r;
+    const double s = fma(r * xx, fma(xx, kSn5, kSn3), r);
+    const double c = xx * fma(xx, fma(xx, kCs6, kCs4), kCs2);
+    const double cor = fma(-s, e[0], fma(-c, e[2], fma(-s, e[1], e[3])));
+    *D = e[2] + cor;
+  }
+  if (ax < kTaylorMax) {
+    *S = taylor_sin(a, da);
+  } else {  // do_sin(a, da)
+    const double dxs = a <= 0 ? -da : da;
+    const double r = r0;
+    const double xx = r * r;
+    const double s = r + fma(r * xx, fma(xx, kSn5, kSn3), dxs);
+    const double c = fma(r, dxs, xx * fma(xx, fma(xx, kCs6, kCs4), kCs2));
+    const double cor = fma(s, e[2], fma(-c, e[0], fma(s, e[3], e[1])));
+    *S = copysign(e[0] + cor, a);
+  }
+}
+
+// sin(x) and cos(x) together, bit-identical to sin() and cos() above.  In every glibc
+// branch one value comes from a sin-type kernel (taylor_sin or do_sin) and the other from
+// do_cos:
+//   A |x| < 0.855 (k < 0x3feb6000):  sin = sin_type(x, 0)             cos = do_cos(x, 0)
+//   B |x| < 2.426:   t = hp0 - |x|   sin = copysign(do_cos(t, hp1), x)  cos = sin_type(t + hp1, da)
+//   C otherwise:     x = n pi/2 + a  sin = (n odd ? do_cos : sin_type)(a, da), cos uses n + 1
+// plus the tiny-argument early returns (sin x = x, cos x = 1).  In A and C both kernels see
+// the same argument, so they share one table lookup (sin_cos_same); the branches are real
+// branches because neighbouring rays (a wavefront) almost always take the same one.
 HEIST_HD void sincos(double x, const double* tab, double* s_out, double* c_out) {
   const uint32_t k = hiword_abs(x);
-  const double ax = fabs(x);
-  const bool in_a = k < 0x3feb6000u;
-  const bool in_b = !in_a && k < 0x400368fdu;
-  double a = x, da = 0.0;
-  int n = 0;
-  if (!in_a && !in_b) n = reduce(x, &a, &da);
-  const double t = kHp0 - ax;                 // branch B
-  const double ab = t + kHp1;
-  const double dab = (t - ab) + kHp1;
-  const double sa = in_a ? x : (in_b ? ab : a);      // sin-type argument
-  const double sda = in_a ? 0.0 : (in_b ? dab : da);
-  const double ca = in_a ? x : (in_b ? t : a);       // do_cos argument
-  const double cdx = in_a ? 0.0 : (in_b ? kHp1 : da);
-  const double ts = taylor_sin(sa, sda);
-  const double ds = do_sin(sa, sda, tab);
-  const double S = fabs(sa) < kTaylorMax ? ts : ds;
-  const double D = do_cos(ca, cdx, tab);
   double sv, cv;
-  if (in_a) {
-    sv = S;
-    cv = D;
-  } else if (in_b) {
-    sv = copysign(D, x);
-    cv = S;
+  if (k < 0x3feb6000u || k >= 0x400368fdu) {
+    double a = x, da = 0.0;
+    int n = 0;
+    if (k >= 0x400368fdu) n = reduce(x, &a, &da);
+    double S, D;
+    sin_cos_same(a, da, tab, &S, &D);
+    if (k < 0x3feb6000u) {
+      sv = S;
+      cv = D;
+    } else {
+      const double s0 = (n & 1) ? D : S;
+      const double c0 = (n & 1) ? S : D;
+      sv = (n & 2) ? -s0 : s0;
+      cv = ((n + 1) & 2) ? -c0 : c0;
+    }
   } else {
-    const double s0 = (n & 1) ? D : S;
-    const double c0 = (n & 1) ? S : D;
-    sv = (n & 2) ? -s0 : s0;
-    cv = ((n + 1) & 2) ? -c0 : c0;
+    const double t = kHp0 - fabs(x);
+    const double ab = t + kHp1;
+    const double dab = (t - ab) + kHp1;
+    sv = copysign(do_cos(t, kHp1, tab), x);
+    cv = sin_of_reduced(ab, dab, tab);
   }
   *s_out = k < 0x3e500000u ? x : sv;
   *c_out = k < 0x3e400000u ? 1.0 : cv;

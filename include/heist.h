@@ -152,6 +152,21 @@ int heist_ppo_loss(const float* logits, const float* values, const int64_t* acti
                    const float* adv, const float* ret, int M, int A, double clip, double vcoef, double ecoef,
                    float* loss_parts, float* dlogits, float* dvalues, double* scratch, heist_stream_t stream);
 
+/* Fused batched SolverNetwork backbone (networks.py:93-100: relu(conv1) -> relu(conv2) ->
+ * relu(conv3) -> AdaptiveAvgPool2d(4,4) -> flatten) on bf16 MFMA with fp32 accumulation,
+ * for SolverAgent.select_action (agents/solver.py:75-99) over a batch.
+ * heist_solver_pack converts the float32 torch parameters conv{1,2,3}.weight [co][ci][3][3]
+ * and .bias [co] (3->32->64->64) into the kernel's fragment layout in `packed`
+ * (heist_solver_packed_bytes() bytes, 16-byte aligned); call it after every weight update.
+ * heist_solver_features: obs [n][3][rows][cols] float32 -> feat_out [n][1024] float32
+ * (channel-major 64 x 4 x 4, the x.view(batch, -1) order).  rows x cols in {20x20, 10x10};
+ * other sizes return HEIST_EINVAL (callers use the PyTorch path). */
+int heist_solver_packed_bytes(void);
+int heist_solver_pack(const float* conv1_w, const float* conv1_b, const float* conv2_w, const float* conv2_b,
+                      const float* conv3_w, const float* conv3_b, void* packed, heist_stream_t stream);
+int heist_solver_features(const float* obs, int n, int rows, int cols, const void* packed, float* feat_out,
+                          heist_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

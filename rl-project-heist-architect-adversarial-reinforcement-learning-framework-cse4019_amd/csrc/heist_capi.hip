@@ -34,6 +34,12 @@ hipError_t launch_arch_decode(const int64_t* amap, int n, int R, int C, const fl
                               int32_t* n_cams, int32_t* guard_paths, int32_t* guard_meta, double* guard_fov,
                               int32_t* n_guards, hipStream_t st);
 hipError_t launch_sincos(const double* x, int64_t n, double* so, double* co, hipStream_t st);
+int solver_packed_bytes();
+bool solver_conv_supported(int R, int C);
+hipError_t launch_solver_pack(const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
+                              const float* b3, void* packed, hipStream_t st);
+hipError_t launch_solver_conv(const float* obs, int n, int R, int C, const void* packed, float* feat, int n_cu,
+                              hipStream_t st);
 hipError_t launch_gae(const float* r, const float* v, const uint8_t* d, const float* last_value, int T, int N,
                       double gamma, double lam, float* adv, float* ret, hipStream_t st);
 hipError_t launch_adv_moments(const float* x, int64_t n, int phase, double* acc, hipStream_t st);
@@ -364,3 +370,31 @@ int heist_ppo_loss(const float* logits, const float* values, const int64_t* acti
 }
 
 }  // extern "C"
+
+int heist_solver_packed_bytes(void) { return heist::solver_packed_bytes(); }
+
+int heist_solver_pack(const float* conv1_w, const float* conv1_b, const float* conv2_w, const float* conv2_b,
+                      const float* conv3_w, const float* conv3_b, void* packed, heist_stream_t stream) {
+  HEIST_REQUIRE(conv1_w && conv1_b && conv2_w && conv2_b && conv3_w && conv3_b && packed,
+                "heist_solver_pack: null pointer");
+  return check_hip(heist::launch_solver_pack(conv1_w, conv1_b, conv2_w, conv2_b, conv3_w, conv3_b, packed,
+                                             (hipStream_t)stream),
+                   "heist_solver_pack");
+}
+
+int heist_solver_features(const float* obs, int n, int rows, int cols, const void* packed, float* feat_out,
+                          heist_stream_t stream) {
+  HEIST_REQUIRE(obs && packed && feat_out, "heist_solver_features: null pointer");
+  HEIST_REQUIRE(n >= 0, "heist_solver_features: n < 0");
+  HEIST_REQUIRE(heist::solver_conv_supported(rows, cols),
+                "heist_solver_features: grid " + std::to_string(rows) + "x" + std::to_string(cols) +
+                    " not supported (20x20, 10x10)");
+  if (n == 0) return 0;
+  int dev = 0, n_cu = 0;
+  if (int rc = check_hip(hipGetDevice(&dev), "hipGetDevice")) return rc;
+  if (int rc = check_hip(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev),
+                         "hipDeviceGetAttribute"))
+    return rc;
+  return check_hip(heist::launch_solver_conv(obs, n, rows, cols, packed, feat_out, n_cu, (hipStream_t)stream),
+                   "heist_solver_features");
+}

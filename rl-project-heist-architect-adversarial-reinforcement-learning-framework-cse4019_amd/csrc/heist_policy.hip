@@ -1,0 +1,357 @@
+// heist_policy.hip -- fused batched SolverNetwork conv stack on CDNA4 bf16 MFMA.
+//
+// Replaces the backbone of SolverNetwork.forward (heist_architect/networks.py:93-100):
+//   relu(conv1 3->32) -> relu(conv2 32->64) -> relu(conv3 64->64) -> AdaptiveAvgPool(4,4)
+//   -> flatten [N, 64*16]
+// for a batch of [N,3,R,C] float32 observations, the hot op of every rollout step
+// (agents/solver.py:75-99 select_action, batched).  The MLP tail (fc_spatial, LSTM,
+// heads) stays on PyTorch-ROCm GEMMs.
+//
+// Design (one 256-thread workgroup per CU, persistent over envs):
+//   * every conv weight lives in VGPRs for the whole kernel as ready-made MFMA fragments
+//     (conv1 12, conv2 72, conv3 144 VGPRs per lane; packed once per weight update by
+//     heist_solver_pack), so the loop touches HBM only for the observation (4.8 KB/env)
+//     and the pooled features (4 KB/env);
+//   * one env at a time sits in LDS as zero-padded NHWC bf16 planes: input [P][4],
+//     act1 [P][32+8], act2 [P][64+8] (P = (R+2)(C+2); the +8 channel pad makes the
+//     16-byte fragment reads of 16 consecutive positions bank-conflict free);
+//   * each conv is an implicit GEMM on v_mfma_f32_32x32x16_bf16 (fp32 accumulate) whose
+//     A/B fragments are single 16-byte LDS reads at compile-time tap offsets;
+//     conv1/conv2 compute D[channel][position] so the epilogue writes 4 channels of a
+//     position per 8-byte store; conv3 computes D[position][channel] so that the 4x4
+//     average pool is one more MFMA, Y[cell][ch] += P[cell][pos] . relu(D)[pos][ch],
+//     with the accumulator fed back as the B operand (no LDS round trip, no atomics);
+//   * the next env's observation is loaded into registers while conv2/conv3 run.
+// Waves: w = 2*mh + nh; conv1 splits position tiles 4 ways, conv2/conv3 split output
+// channels by nh (32 each) and position tiles by mh.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace heist {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// Packed blob (16-byte units): W1 [3][64], W2 [2][18][64], W3 [2][36][64] MFMA fragments,
+// then float biases b1[32], b2[64], b3[64].
+constexpr int kW1Steps = 3, kW2Steps = 18, kW3Steps = 36;
+constexpr int kOffW1 = 0;
+constexpr int kOffW2 = kOffW1 + kW1Steps * 64;
+constexpr int kOffW3 = kOffW2 + 2 * kW2Steps * 64;
+constexpr int kOffBias = kOffW3 + 2 * kW3Steps * 64;  // in uint4 units
+constexpr int kPackedBytes = kOffBias * 16 + (32 + 64 + 64) * 4;
+
+__host__ __device__ constexpr int align16c(int x) { return (x + 15) & ~15; }
+
+template <int R, int C>
+struct ConvGeom {
+  static constexpr int PC = C + 2, PR = R + 2, NP = PR * PC, RC = R * C, MT = (RC + 31) / 32;
+  static constexpr int S0 = 8, S1 = 80, S2 = 144;  // bytes per padded position
+  static constexpr int IN = 0;
+  static constexpr int A1 = align16c(IN + NP * S0);
+  static constexpr int A2 = align16c(A1 + NP * S1);
+  static constexpr int ZERO_END = align16c(A2 + NP * S2);  // zeroed once (padding borders)
+  static constexpr int POOL = ZERO_END;                    // [64][16] f32
+  static constexpr int BIAS = POOL + 64 * 16 * 4;          // b1[32] b2[64] b3[64]
+  static constexpr int INVA = BIAS + 160 * 4;              // [16] f32 1/area
+  static constexpr int PM = INVA + 16 * 4;                 // [MT][2][64] pool-membership bytes
+  static constexpr int LDS = align16c(PM + MT * 128);
+  static constexpr int QI = (RC + 255) / 256;              // obs cells per thread
+};
+
+// torch adaptive_avg_pool2d window of output index i over n inputs into 4.
+__host__ __device__ constexpr int pool_lo(int i, int n) { return (i * n) / 4; }
+__host__ __device__ constexpr int pool_hi(int i, int n) { return ((i + 1) * n + 3) / 4; }
+
+__device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
+
+template <int R, int C>
+__device__ __forceinline__ int padded_pos(int m) {  // output position m -> padded index
+  using G = ConvGeom<R, C>;
+  const int mc = m < G::RC ? m : G::RC - 1;
+  const int oy = mc / C;
+  return (oy + 1) * G::PC + (mc - oy * C) + 1;
+}
+
+template <int R, int C>
+__device__ __forceinline__ void load_obs(const float* __restrict__ obs, int e, float (&v)[ConvGeom<R, C>::QI][3]) {
+  using G = ConvGeom<R, C>;
+  const float* o = obs + (size_t)e * 3 * G::RC;
+#pragma unroll
+  for (int i = 0; i < G::QI; ++i) {
+    const int q = threadIdx.x + 256 * i;
+    if (q < G::RC) {
+      v[i][0] = o[q];
+      v[i][1] = o[G::RC + q];
+      v[i][2] = o[2 * G::RC + q];
+    }
+  }
+}
+
+template <int R, int C>
+__device__ __forceinline__ void stage_obs(unsigned char* smem, const float (&v)[ConvGeom<R, C>::QI][3]) {
+  using G = ConvGeom<R, C>;
+#pragma unroll
+  for (int i = 0; i < G::QI; ++i) {
+    const int q = threadIdx.x + 256 * i;
+    if (q < G::RC) {
+      const int oy = q / C;
+      const int p = (oy + 1) * G::PC + (q - oy * C) + 1;
+      bf16x4 b;
+      b[0] = (__bf16)v[i][0];
+      b[1] = (__bf16)v[i][1];
+      b[2] = (__bf16)v[i][2];
+      b[3] = (__bf16)0.f;
+      *reinterpret_cast<bf16x4*>(smem + G::IN + p * G::S0) = b;
+    }
+  }
+}
+
+// Epilogue of a D[channel][position] tile: lane holds position m = 32t + (l & 31) and, in
+// register 4g + i, channel n0 + i with n0 = 8g + 4h; relu(acc + bias) -> 4 bf16 -> 8 bytes.
+template <int R, int C, int S>
+__device__ __forceinline__ void store_chan_major(unsigned char* dst, const float* bias, int nbase, const f32x16& acc,
+                                                 int m, int h) {
+  using G = ConvGeom<R, C>;
+  if (m >= G::RC) return;
+  const int p = padded_pos<R, C>(m);
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int n0 = nbase + 8 * g + 4 * h;
+    const float4 b = *reinterpret_cast<const float4*>(bias + n0);
+    bf16x4 o;
+    o[0] = (__bf16)relu(acc[4 * g + 0] + b.x);
+    o[1] = (__bf16)relu(acc[4 * g + 1] + b.y);
+    o[2] = (__bf16)relu(acc[4 * g + 2] + b.z);
+    o[3] = (__bf16)relu(acc[4 * g + 3] + b.w);
+    *reinterpret_cast<bf16x4*>(dst + p * S + n0 * 2) = o;
+  }
+}
+
+template <int R, int C>
+__global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __restrict__ obs, int n,
+                                                             const uint4* __restrict__ packed,
+                                                             float* __restrict__ feat) {
+  using G = ConvGeom<R, C>;
+  constexpr int PC = G::PC;
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63, h = l >> 5, lr = l & 31;
+  const int nh = w & 1, mh = w >> 1;
+
+  // ---- weights -> registers (MFMA fragments), tables -> LDS
+  bf16x8 w1[kW1Steps], w2[kW2Steps], w3[kW3Steps];
+#pragma unroll
+  for (int s = 0; s < kW1Steps; ++s) w1[s] = __builtin_bit_cast(bf16x8, packed[kOffW1 + s * 64 + l]);
+#pragma unroll
+  for (int s = 0; s < kW2Steps; ++s) w2[s] = __builtin_bit_cast(bf16x8, packed[kOffW2 + (nh * kW2Steps + s) * 64 + l]);
+#pragma unroll
+  for (int s = 0; s < kW3Steps; ++s) w3[s] = __builtin_bit_cast(bf16x8, packed[kOffW3 + (nh * kW3Steps + s) * 64 + l]);
+  const float* gbias = reinterpret_cast<const float*>(packed + kOffBias);
+  float* bias = reinterpret_cast<float*>(smem + G::BIAS);
+  const float b3v = gbias[96 + 32 * nh + lr];
+  if (tid < 160) bias[tid] = gbias[tid];
+  for (int i = tid; i < G::ZERO_END / 16; i += 256) reinterpret_cast<uint4*>(smem)[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (tid < 16) {
+    const int ci = tid >> 2, cj = tid & 3;
+    const int area = (pool_hi(ci, R) - pool_lo(ci, R)) * (pool_hi(cj, C) - pool_lo(cj, C));
+    reinterpret_cast<float*>(smem + G::INVA)[tid] = 1.0f / (float)area;
+  }
+  for (int i = tid; i < G::MT * 128; i += 256) {  // pool membership of the P fragment bits
+    const int t = i >> 7, s = (i >> 6) & 1, ll = i & 63;
+    const int cell = ll & 31, hh = ll >> 5;
+    unsigned bits = 0;
+    if (cell < 16) {
+      const int ci = cell >> 2, cj = cell & 3;
+      for (int j = 0; j < 8; ++j) {
+        const int m = 32 * t + 16 * s + 8 * (j >> 2) + 4 * hh + (j & 3);
+        if (m < G::RC) {
+          const int oy = m / C, ox = m - (m / C) * C;
+          if (oy >= pool_lo(ci, R) && oy < pool_hi(ci, R) && ox >= pool_lo(cj, C) && ox < pool_hi(cj, C))
+            bits |= 1u << j;
+        }
+      }
+    }
+    smem[G::PM + i] = (unsigned char)bits;
+  }
+
+  // conv1 per-lane tap offsets: k-step s covers taps 4s + 2h, 4s + 2h + 1 (taps >= 9 have
+  // zero weights; they read the centre tap)
+  int off1a[kW1Steps], off1b[kW1Steps];
+#pragma unroll
+  for (int s = 0; s < kW1Steps; ++s) {
+    int ta = 4 * s + 2 * h, tb = ta + 1;
+    ta = ta < 9 ? ta : 4;
+    tb = tb < 9 ? tb : 4;
+    off1a[s] = ((ta / 3) * PC + (ta % 3)) * G::S0;
+    off1b[s] = ((tb / 3) * PC + (tb % 3)) * G::S0;
+  }
+
+  float pre[G::QI][3];
+  int e = blockIdx.x;
+  if (e < n) load_obs<R, C>(obs, e, pre);
+  __syncthreads();
+
+  for (; e < n; e += gridDim.x) {
+    stage_obs<R, C>(smem, pre);
+    __syncthreads();  // B1: input plane ready (and last env's pool reads done)
+
+    // ---- conv1: D[32 ch][pos] = W1 . im2col(in), position tiles split 4 ways
+#pragma unroll 1
+    for (int t = w; t < G::MT; t += 4) {
+      const int m = 32 * t + lr;
+      const unsigned char* base = smem + G::IN + (padded_pos<R, C>(m) - PC - 1) * G::S0;
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < kW1Steps; ++s) {
+        const uint2 a = *reinterpret_cast<const uint2*>(base + off1a[s]);
+        const uint2 b = *reinterpret_cast<const uint2*>(base + off1b[s]);
+        const bf16x8 f = __builtin_bit_cast(bf16x8, make_uint4(a.x, a.y, b.x, b.y));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1[s], f, acc, 0, 0, 0);
+      }
+      store_chan_major<R, C, G::S1>(smem + G::A1, bias, 0, acc, m, h);
+    }
+    __syncthreads();  // B2: act1 ready
+
+    const int en = e + gridDim.x;
+    if (en < n) load_obs<R, C>(obs, en, pre);  // next env's observation in flight during conv2/3
+
+    // ---- conv2: D[32 ch of nh][pos] = W2 . im2col(act1)
+#pragma unroll 1
+    for (int t = mh; t < G::MT; t += 2) {
+      const int m = 32 * t + lr;
+      const unsigned char* base = smem + G::A1 + (padded_pos<R, C>(m) - PC - 1) * G::S1 + 16 * h;
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < kW2Steps; ++s) {
+        const int tap = s >> 1;
+        const int off = ((tap / 3) * PC + (tap % 3)) * G::S1 + (s & 1) * 32;
+        const bf16x8 f = *reinterpret_cast<const bf16x8*>(base + off);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2[s], f, acc, 0, 0, 0);
+      }
+      store_chan_major<R, C, G::S2>(smem + G::A2, bias + 32, 32 * nh, acc, m, h);
+    }
+    __syncthreads();  // B3: act2 ready
+
+    // ---- conv3: D[pos][32 ch of nh] = im2col(act2) . W3, then Y[cell][ch] += P . relu(D)
+    f32x16 Y = {};
+#pragma unroll 1
+    for (int t = mh; t < G::MT; t += 2) {
+      const int m = 32 * t + lr;
+      const unsigned char* base = smem + G::A2 + (padded_pos<R, C>(m) - PC - 1) * G::S2 + 16 * h;
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < kW3Steps; ++s) {
+        const int tap = s >> 2;
+        const int off = ((tap / 3) * PC + (tap % 3)) * G::S2 + (s & 3) * 32;
+        const bf16x8 f = *reinterpret_cast<const bf16x8*>(base + off);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, w3[s], acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 x, p;
+        const unsigned bits = smem[G::PM + (t * 2 + s) * 64 + l];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          x[j] = (__bf16)relu(acc[8 * s + j] + b3v);
+          p[j] = ((bits >> j) & 1u) ? (__bf16)1.0f : (__bf16)0.0f;
+        }
+        Y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p, x, Y, 0, 0, 0);
+      }
+    }
+    // Y: lane = channel 32nh + lr, register r < 8 = cell (r & 3) + 8 (r >> 2) + 4h
+    float* pool = reinterpret_cast<float*>(smem + G::POOL) + (32 * nh + lr) * 16 + 4 * h;
+    if (mh == 1) {
+      *reinterpret_cast<float4*>(pool) = make_float4(Y[0], Y[1], Y[2], Y[3]);
+      *reinterpret_cast<float4*>(pool + 8) = make_float4(Y[4], Y[5], Y[6], Y[7]);
+    }
+    __syncthreads();  // B4: partner half of the pool sums in LDS
+    if (mh == 0) {
+      const float4 p0 = *reinterpret_cast<const float4*>(pool);
+      const float4 p1 = *reinterpret_cast<const float4*>(pool + 8);
+      const float* inva = reinterpret_cast<const float*>(smem + G::INVA) + 4 * h;
+      const float4 i0 = *reinterpret_cast<const float4*>(inva);
+      const float4 i1 = *reinterpret_cast<const float4*>(inva + 8);
+      float* out = feat + (size_t)e * 1024 + (32 * nh + lr) * 16 + 4 * h;
+      *reinterpret_cast<float4*>(out) =
+          make_float4((Y[0] + p0.x) * i0.x, (Y[1] + p0.y) * i0.y, (Y[2] + p0.z) * i0.z, (Y[3] + p0.w) * i0.w);
+      *reinterpret_cast<float4*>(out + 8) =
+          make_float4((Y[4] + p1.x) * i1.x, (Y[5] + p1.y) * i1.y, (Y[6] + p1.z) * i1.z, (Y[7] + p1.w) * i1.w);
+    }
+  }
+}
+
+// Weight packing: fragment element j of lane l, k-step s, output tile nt holds
+// W[co = 32 nt + (l & 31)][k = 16 s + 8 (l >> 5) + j] with k = tap * CinP + ci,
+// tap = 3 ky + kx; zero where ci >= Cin or tap >= 9.  bf16 round-to-nearest-even.
+__global__ void solver_pack_kernel(const float* __restrict__ w1, const float* __restrict__ b1,
+                                   const float* __restrict__ w2, const float* __restrict__ b2,
+                                   const float* __restrict__ w3, const float* __restrict__ b3,
+                                   uint4* __restrict__ packed) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // one fragment (8 elements) per thread
+  const int nfrag = kOffBias;
+  if (i < nfrag) {
+    int layer, rem;
+    if (i < kOffW2) { layer = 0; rem = i - kOffW1; }
+    else if (i < kOffW3) { layer = 1; rem = i - kOffW2; }
+    else { layer = 2; rem = i - kOffW3; }
+    const int steps = layer == 0 ? kW1Steps : (layer == 1 ? kW2Steps : kW3Steps);
+    const int cinp = layer == 0 ? 4 : (layer == 1 ? 32 : 64);
+    const int cin = layer == 0 ? 3 : cinp;
+    const float* W = layer == 0 ? w1 : (layer == 1 ? w2 : w3);
+    const int l = rem & 63, s = (rem >> 6) % steps, nt = (rem >> 6) / steps;
+    const int co = 32 * nt + (l & 31);
+    bf16x8 f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * s + 8 * (l >> 5) + j;
+      const int tap = k / cinp, ci = k % cinp;
+      const float v = (tap < 9 && ci < cin) ? W[((size_t)co * cin + ci) * 9 + tap] : 0.0f;
+      f[j] = (__bf16)v;
+    }
+    packed[i] = __builtin_bit_cast(uint4, f);
+  } else if (i < nfrag + 160) {
+    const int k = i - nfrag;
+    const float v = k < 32 ? b1[k] : (k < 96 ? b2[k - 32] : b3[k - 96]);
+    reinterpret_cast<float*>(packed + kOffBias)[k] = v;
+  }
+}
+
+int solver_packed_bytes() { return kPackedBytes; }
+
+hipError_t launch_solver_pack(const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
+                              const float* b3, void* packed, hipStream_t st) {
+  const int total = kOffBias + 160;
+  hipLaunchKernelGGL(solver_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w1, b1, w2, b2, w3, b3,
+                     reinterpret_cast<uint4*>(packed));
+  return hipGetLastError();
+}
+
+template <int R, int C>
+static hipError_t launch_conv_rc(const float* obs, int n, const void* packed, float* feat, int n_cu, hipStream_t st) {
+  using G = ConvGeom<R, C>;
+  static bool attr_set = false;  // per process; the attribute is per function, not per device
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&solver_conv_kernel<R, C>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int grid = n < n_cu ? n : n_cu;
+  hipLaunchKernelGGL((solver_conv_kernel<R, C>), dim3(grid), dim3(256), G::LDS, st, obs, n,
+                     reinterpret_cast<const uint4*>(packed), feat);
+  return hipGetLastError();
+}
+
+bool solver_conv_supported(int R, int C) { return (R == 20 && C == 20) || (R == 10 && C == 10); }
+
+hipError_t launch_solver_conv(const float* obs, int n, int R, int C, const void* packed, float* feat, int n_cu,
+                              hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (R == 20 && C == 20) return launch_conv_rc<20, 20>(obs, n, packed, feat, n_cu, st);
+  if (R == 10 && C == 10) return launch_conv_rc<10, 10>(obs, n, packed, feat, n_cu, st);
+  return hipErrorInvalidValue;
+}
+
+}  // namespace heist

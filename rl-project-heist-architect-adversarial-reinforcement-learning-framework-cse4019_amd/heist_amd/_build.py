@@ -16,7 +16,7 @@ INCLUDE = os.path.join(REPO_ROOT, "include")
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libheist_hip.so")
 BUILD_DIR = os.path.join(PKG_ROOT, "build")
 ARCH = os.environ.get("HEIST_OFFLOAD_ARCH", "gfx950")
-SOURCES = ["heist_env.hip", "heist_arch.hip", "heist_ppo.hip", "heist_capi.hip"]
+SOURCES = ["heist_env.hip", "heist_arch.hip", "heist_ppo.hip", "heist_policy.hip", "heist_capi.hip"]
 HEADERS = ["heist_device.h", "heist_trig.h", "heist_sincos_table.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",

@@ -42,6 +42,9 @@ SIGNATURES = {
     "heist_adv_apply": (_i, [_vp, _i64, _vp, _f, _vp]),
     "heist_adv_normalize": (_i, [_vp, _i64, _vp, _f, _vp]),
     "heist_ppo_loss": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _d, _d, _d, _vp, _vp, _vp, _vp, _vp]),
+    "heist_solver_packed_bytes": (_i, []),
+    "heist_solver_pack": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "heist_solver_features": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp]),
 }
 
 

@@ -56,7 +56,7 @@ class SolverAgent:  # agents/solver.py:18-259
     def __init__(self, grid_rows: int = 20, grid_cols: int = 20, num_actions: int = 5, lr: float = 3e-4,
                  gamma: float = 0.99, gae_lambda: float = 0.95, clip_epsilon: float = 0.2,
                  entropy_coeff: float = 0.05, value_coeff: float = 0.5, max_grad_norm: float = 0.5,
-                 ppo_epochs: int = 3, batch_size: int = 64, device=None):
+                 ppo_epochs: int = 3, batch_size: int = 64, device=None, fused_inference: bool = True):
         self.grid_rows = grid_rows
         self.grid_cols = grid_cols
         self.num_actions = num_actions
@@ -68,6 +68,7 @@ class SolverAgent:  # agents/solver.py:18-259
         self.max_grad_norm = max_grad_norm
         self.ppo_epochs = ppo_epochs
         self.batch_size = batch_size
+        self.fused_inference = fused_inference  # batched act(): bf16-MFMA backbone kernel
         self.device = torch.device(device) if device is not None else DEVICE
         self.network = SolverNetwork(grid_rows=grid_rows, grid_cols=grid_cols, num_actions=num_actions).to(self.device)
         self.optimizer = torch.optim.Adam(self.network.parameters(), lr=lr)
@@ -160,10 +161,19 @@ class SolverAgent:  # agents/solver.py:18-259
 
     # -- batched API ------------------------------------------------------------------
     @torch.no_grad()
-    def act(self, obs: torch.Tensor, hidden=None, generator: Optional[torch.Generator] = None):
-        """Batched select_action: (action [N], log_prob [N], value [N], hidden)."""
+    def act(self, obs: torch.Tensor, hidden=None, generator: Optional[torch.Generator] = None,
+            fused: Optional[bool] = None):
+        """Batched select_action: (action [N], log_prob [N], value [N], hidden).
+
+        fused (default self.fused_inference): run the conv backbone on the fused bf16-MFMA
+        HIP kernel (heist_solver_features) where the grid is supported; False keeps the
+        reference fp32 forward."""
         self.network.eval()
-        logits, value, hidden = self.network(obs, hidden)
+        use = self.fused_inference if fused is None else fused
+        if use and self.network.fused_supported(obs):
+            logits, value, hidden = self.network.forward_fused(obs, hidden)
+        else:
+            logits, value, hidden = self.network(obs, hidden)
         logp_all = F.log_softmax(logits.float(), dim=-1)
         action = torch.multinomial(logp_all.exp(), 1, generator=generator).reshape(-1)
         # Categorical(probs).log_prob = log(clamp(p / sum p, eps, 1 - eps))

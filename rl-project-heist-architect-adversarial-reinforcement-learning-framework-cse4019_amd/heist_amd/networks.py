@@ -72,6 +72,53 @@ class SolverNetwork(nn.Module):  # networks.py:13-131
         out, new_hidden = self.lstm_step(spatial, hidden)
         return self.policy_head(out), self.value_head(out), new_hidden
 
+    # -- fused backbone (heist_solver_features, bf16 MFMA) -----------------------------
+    def fused_supported(self, state: torch.Tensor) -> bool:
+        """The HIP backbone covers 20x20 and 10x10 grids on a HIP device."""
+        return state.is_cuda and state.dim() == 4 and tuple(state.shape[1:]) in ((3, 20, 20), (3, 10, 10))
+
+    def _packed_backbone(self) -> torch.Tensor:
+        """conv1-3 weights in the kernel's MFMA fragment layout, re-packed (one small launch)
+        whenever a conv parameter changed (optimizer steps bump the tensor versions)."""
+        from . import _native
+        convs = (self.conv1, self.conv2, self.conv3)
+        key = tuple((m.weight.data_ptr(), m.weight._version, m.bias.data_ptr(), m.bias._version) for m in convs)
+        cache = getattr(self, "_pack_cache", None)
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        dev = self.conv1.weight.device
+        L = _native.lib()
+        buf = torch.empty(L.heist_solver_packed_bytes(), dtype=torch.uint8, device=dev)
+        ws = [t.detach().float().contiguous() for m in convs for t in (m.weight, m.bias)]
+        _native.check(L.heist_solver_pack(*(_native.ptr(t) for t in ws), _native.ptr(buf), _native.stream(dev)),
+                      "heist_solver_pack")
+        self._pack_cache = (key, buf, ws)  # ws keeps the fp32 sources alive until the pack ran
+        return buf
+
+    def features_fused(self, state: torch.Tensor) -> torch.Tensor:
+        """Pooled conv features [B, 1024] (networks.py:93-100) from the HIP kernel:
+        bf16 operands, fp32 accumulation; inference only (no autograd)."""
+        from . import _native
+        if not self.fused_supported(state):
+            raise _native.HeistError("fused Solver backbone needs [B,3,20,20] or [B,3,10,10] on a HIP device")
+        x = state.detach().float().contiguous()
+        packed = self._packed_backbone()
+        out = torch.empty(x.shape[0], 1024, dtype=torch.float32, device=x.device)
+        _native.check(_native.lib().heist_solver_features(_native.ptr(x), x.shape[0], x.shape[2], x.shape[3],
+                                                          _native.ptr(packed), _native.ptr(out),
+                                                          _native.stream(x.device)), "heist_solver_features")
+        return out
+
+    @torch.no_grad()
+    def forward_fused(self, state: torch.Tensor, hidden: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+        """forward() with the conv backbone on the fused HIP kernel (rollout inference)."""
+        b = state.shape[0]
+        spatial = F.relu(self.fc_spatial(self.features_fused(state)))
+        if hidden is None:
+            hidden = self._init_hidden(b, state.device)
+        out, new_hidden = self.lstm_step(spatial, hidden)
+        return self.policy_head(out), self.value_head(out), new_hidden
+
     def get_action(self, state: torch.Tensor, hidden=None):  # networks.py:124-131
         logits, value, new_hidden = self.forward(state, hidden)
         dist = torch.distributions.Categorical(F.softmax(logits, dim=-1))

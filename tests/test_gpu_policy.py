@@ -1,0 +1,165 @@
+"""GPU parity of the fused Solver backbone (heist_solver_features, bf16 MFMA) against
+SolverNetwork's conv stack (reference networks.py:93-100).
+
+Two references:
+  * an emulation in float64 on the CPU that rounds exactly where the kernel rounds
+    (bf16 input, bf16 conv weights, bf16 activations after each ReLU, fp32 biases and
+    accumulation): the kernel must agree to accumulation-order noise;
+  * the plain fp32 torch forward (what the reference computes): agreement within the
+    bf16 precision of the operands (tolerances stated per test).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from heist_amd import EnvironmentConfig, HeistEnv
+from heist_amd.agents import SolverAgent
+from heist_amd.layouts import synthetic_layouts
+from heist_amd.networks import SolverNetwork
+
+pytestmark = pytest.mark.gpu
+
+# bf16 has an 8-bit significand: one rounding is <= 2^-9 relative.  Against the emulation
+# only accumulation order differs, which can flip a bf16 rounding of an activation
+# (one ulp, 2^-8) on rare elements; pooling averages those.
+TOL_EMU_MAX = 4e-3    # max |kernel - emulation| / max |emulation|
+TOL_EMU_MEAN = 2e-4   # mean |kernel - emulation| / max |emulation|
+TOL_F32_MAX = 3e-2    # max |kernel - fp32 torch| / max |fp32 torch|
+
+
+def _bf(x):
+    return x.to(torch.bfloat16).to(x.dtype)
+
+
+def emulate_backbone(net, obs):
+    """float64 CPU restatement of the kernel's arithmetic (rounding points as the kernel)."""
+    x = _bf(obs.detach().double().cpu())
+    convs = (net.conv1, net.conv2, net.conv3)
+    for conv in convs:
+        w = _bf(conv.weight.detach().double().cpu())
+        b = conv.bias.detach().float().double().cpu()
+        x = _bf(F.relu(F.conv2d(x, w, b, padding=1)))
+    return F.adaptive_avg_pool2d(x, (4, 4)).reshape(x.shape[0], -1)
+
+
+def torch_backbone(net, obs):
+    with torch.no_grad():
+        x = F.relu(net.conv1(obs))
+        x = F.relu(net.conv2(x))
+        x = F.relu(net.conv3(x))
+        return net.pool(x).reshape(obs.shape[0], -1)
+
+
+def env_obs(n, R, device, seed=0, steps=5):
+    cfg = EnvironmentConfig(grid_rows=R, grid_cols=R)
+    env = HeistEnv(n, cfg, device=device)
+    env.set_layouts(synthetic_layouts(n, R, R, 15 if R >= 20 else 5, seed=seed))
+    env.reset()
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    for _ in range(steps):
+        env.step(torch.randint(0, 5, (n,), device=device, generator=g))
+    return env.obs.clone()
+
+
+def _rel(a, b):
+    d = (a.double().cpu() - b.double().cpu()).abs()
+    m = b.double().abs().max().item()
+    return d.max().item() / m, d.mean().item() / m
+
+
+@pytest.mark.parametrize("R,n", [(20, 64), (20, 1), (20, 300), (10, 77)])
+def test_features_match_emulation(gpu_device, R, n):
+    torch.manual_seed(R * 1000 + n)
+    net = SolverNetwork(R, R).to(gpu_device)
+    for conv in (net.conv1, net.conv2, net.conv3):  # non-trivial biases of both signs
+        torch.nn.init.uniform_(conv.bias, -0.3, 0.3)
+    obs = env_obs(n, R, gpu_device, seed=n)
+    got = net.features_fused(obs)
+    ref = emulate_backbone(net, obs)
+    assert got.shape == (n, 1024) and torch.isfinite(got).all()
+    mx, mean = _rel(got, ref)
+    assert mx < TOL_EMU_MAX and mean < TOL_EMU_MEAN, (mx, mean)
+
+
+def test_features_random_inputs_and_weights(gpu_device):
+    """Inputs outside the env's value set (normal noise), negative pre-activations."""
+    torch.manual_seed(7)
+    net = SolverNetwork().to(gpu_device)
+    obs = torch.randn(48, 3, 20, 20, device=gpu_device)
+    mx, mean = _rel(net.features_fused(obs), emulate_backbone(net, obs))
+    assert mx < TOL_EMU_MAX and mean < TOL_EMU_MEAN, (mx, mean)
+
+
+def test_features_close_to_fp32_full_batch(gpu_device):
+    """4096 envs (the bench batch: 16 envs per workgroup) against the fp32 torch path."""
+    torch.manual_seed(3)
+    net = SolverNetwork().to(gpu_device)
+    obs = env_obs(4096, 20, gpu_device, seed=11, steps=3)
+    got = net.features_fused(obs)
+    ref = torch_backbone(net, obs)
+    mx, _ = _rel(got, ref)
+    assert mx < TOL_F32_MAX, mx
+    # every env row was written (rows are independent: compare a spread of them exactly
+    # against the emulation too)
+    rows = torch.tensor([0, 1, 255, 256, 257, 1023, 2048, 4095], device=gpu_device)
+    mx, mean = _rel(got[rows], emulate_backbone(net, obs[rows]))
+    assert mx < TOL_EMU_MAX and mean < TOL_EMU_MEAN, (mx, mean)
+
+
+def test_repack_after_weight_update(gpu_device):
+    torch.manual_seed(5)
+    net = SolverNetwork().to(gpu_device)
+    obs = env_obs(16, 20, gpu_device)
+    a = net.features_fused(obs)
+    with torch.no_grad():
+        net.conv2.weight.mul_(0.5)  # in-place, as an optimizer step does
+    b = net.features_fused(obs)
+    assert not torch.allclose(a, b)
+    mx, mean = _rel(b, emulate_backbone(net, obs))
+    assert mx < TOL_EMU_MAX and mean < TOL_EMU_MEAN, (mx, mean)
+
+
+def test_forward_fused_matches_forward(gpu_device):
+    torch.manual_seed(9)
+    net = SolverNetwork().to(gpu_device)
+    for m in net.modules():  # larger head weights than the 0.01-gain init so logits are not ~0
+        if isinstance(m, torch.nn.Linear):
+            torch.nn.init.orthogonal_(m.weight, gain=1.0)
+    obs = env_obs(256, 20, gpu_device, seed=4)
+    h = torch.randn(1, 256, 128, device=gpu_device) * 0.1
+    c = torch.randn(1, 256, 128, device=gpu_device) * 0.1
+    with torch.no_grad():
+        l_ref, v_ref, (h_ref, c_ref) = net(obs, (h, c))
+    l_got, v_got, (h_got, c_got) = net.forward_fused(obs, (h, c))
+    for got, ref in ((l_got, l_ref), (v_got, v_ref), (h_got, h_ref), (c_got, c_ref)):
+        mx, _ = _rel(got, ref)
+        assert mx < TOL_F32_MAX, mx
+
+
+def test_agent_act_uses_fused_path_and_fallback(gpu_device):
+    """act() takes the kernel for 20x20 and the fp32 torch path where it does not apply."""
+    torch.manual_seed(1)
+    ag = SolverAgent(20, 20, device=gpu_device)
+    obs = env_obs(32, 20, gpu_device)
+    a, lp, v, (h, c) = ag.act(obs)
+    assert a.shape == (32,) and ((a >= 0) & (a < 5)).all() and torch.isfinite(lp).all()
+    assert hasattr(ag.network, "_pack_cache")
+    ag32 = SolverAgent(32, 32, device=gpu_device)
+    o32 = torch.rand(4, 3, 32, 32, device=gpu_device)
+    a32, lp32, _, _ = ag32.act(o32)
+    assert not hasattr(ag32.network, "_pack_cache") and a32.shape == (4,)
+    # same logits both ways up to bf16 precision -> log-probs of the taken actions agree
+    a_ref, lp_ref, _, _ = ag.act(obs, fused=False)
+    logits_f, _, _ = ag.network.forward_fused(obs)
+    with torch.no_grad():
+        logits_r, _, _ = ag.network(obs)
+    assert (F.log_softmax(logits_f, -1) - F.log_softmax(logits_r, -1)).abs().max().item() < 1e-3
+
+
+def test_unsupported_grid_rejected(gpu_device):
+    from heist_amd import _native
+    net = SolverNetwork(16, 16).to(gpu_device)
+    with pytest.raises(_native.HeistError):
+        net.features_fused(torch.zeros(2, 3, 16, 16, device=gpu_device))

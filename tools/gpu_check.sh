@@ -31,6 +31,8 @@ for s in ${STEPS:-pytest smoke bench prof}; do
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary
          step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary ;;
     probe) step probe 600 python tools/probe_step.py ;;
+    ptest) step pytest_policy 600 python -m pytest tests/test_gpu_policy.py -x -q ;;
+    pprobe) step probe_policy 600 python tools/probe_policy.py ;;
     list) step counters 120 rocprofv3 -L ;;
     pmcsq) step pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS -d "$OUT/pmc_sq" -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary
            step pmc_sq2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU GRBM_GUI_ACTIVE -d "$OUT/pmc_sq2" -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary ;;

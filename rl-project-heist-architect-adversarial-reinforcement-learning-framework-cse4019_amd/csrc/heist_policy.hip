@@ -8,10 +8,11 @@
 // heads) stays on PyTorch-ROCm GEMMs.
 //
 // Design (one 256-thread workgroup per CU, persistent over envs):
-//   * every conv weight lives in VGPRs for the whole kernel as ready-made MFMA fragments
-//     (conv1 12, conv2 72, conv3 144 VGPRs per lane; packed once per weight update by
-//     heist_solver_pack), so the loop touches HBM only for the observation (4.8 KB/env)
-//     and the pooled features (4 KB/env);
+//   * the conv weights stay on chip for the whole kernel as ready-made MFMA fragments
+//     (packed once per weight update by heist_solver_pack): conv1 (12) and conv3 (144)
+//     in VGPRs, conv2 in LDS (36 KB, read once per k-step and reused over the wave's
+//     position tiles), so the loop touches HBM only for the observation (4.8 KB/env) and
+//     the pooled features (4 KB/env);
 //   * one env at a time sits in LDS as zero-padded NHWC bf16 planes: input [P][4],
 //     act1 [P][32+8], act2 [P][64+8] (P = (R+2)(C+2); the +8 channel pad makes the
 //     16-byte fragment reads of 16 consecutive positions bank-conflict free);
@@ -55,8 +56,10 @@ struct ConvGeom {
   static constexpr int POOL = ZERO_END;                    // [64][16] f32
   static constexpr int BIAS = POOL + 64 * 16 * 4;          // b1[32] b2[64] b3[64]
   static constexpr int INVA = BIAS + 160 * 4;              // [16] f32 1/area
-  static constexpr int PM = INVA + 16 * 4;                 // [MT][2][64] pool-membership bytes
-  static constexpr int LDS = align16c(PM + MT * 128);
+  static constexpr int PM = INVA + 16 * 4;                 // [2*NT2][2][64] pool-membership bytes
+  static constexpr int NT2 = (MT + 1) / 2;                 // position tiles per wave (conv2/conv3)
+  static constexpr int W2 = align16c(PM + 2 * NT2 * 128);  // conv2 fragments [2][18][64] x 16 B
+  static constexpr int LDS = W2 + 2 * 18 * 64 * 16;
   static constexpr int QI = (RC + 255) / 256;              // obs cells per thread
 };
 
@@ -141,13 +144,13 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
   const int nh = w & 1, mh = w >> 1;
 
   // ---- weights -> registers (MFMA fragments), tables -> LDS
-  bf16x8 w1[kW1Steps], w2[kW2Steps], w3[kW3Steps];
+  bf16x8 w1[kW1Steps], w3[kW3Steps];
 #pragma unroll
   for (int s = 0; s < kW1Steps; ++s) w1[s] = __builtin_bit_cast(bf16x8, packed[kOffW1 + s * 64 + l]);
 #pragma unroll
-  for (int s = 0; s < kW2Steps; ++s) w2[s] = __builtin_bit_cast(bf16x8, packed[kOffW2 + (nh * kW2Steps + s) * 64 + l]);
-#pragma unroll
   for (int s = 0; s < kW3Steps; ++s) w3[s] = __builtin_bit_cast(bf16x8, packed[kOffW3 + (nh * kW3Steps + s) * 64 + l]);
+  for (int i = tid; i < 2 * kW2Steps * 64; i += 256)  // conv2 fragments: LDS, read once per k-step
+    reinterpret_cast<uint4*>(smem + G::W2)[i] = packed[kOffW2 + i];
   const float* gbias = reinterpret_cast<const float*>(packed + kOffBias);
   float* bias = reinterpret_cast<float*>(smem + G::BIAS);
   const float b3v = gbias[96 + 32 * nh + lr];
@@ -158,7 +161,7 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
     const int area = (pool_hi(ci, R) - pool_lo(ci, R)) * (pool_hi(cj, C) - pool_lo(cj, C));
     reinterpret_cast<float*>(smem + G::INVA)[tid] = 1.0f / (float)area;
   }
-  for (int i = tid; i < G::MT * 128; i += 256) {  // pool membership of the P fragment bits
+  for (int i = tid; i < 2 * G::NT2 * 128; i += 256) {  // pool membership of the P fragment bits
     const int t = i >> 7, s = (i >> 6) & 1, ll = i & 63;
     const int cell = ll & 31, hh = ll >> 5;
     unsigned bits = 0;
@@ -191,73 +194,124 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
   float pre[G::QI][3];
   int e = blockIdx.x;
   if (e < n) load_obs<R, C>(obs, e, pre);
+  __builtin_amdgcn_s_waitcnt(0);  // weights landed: no conservative vmcnt waits inside the loop
   __syncthreads();
 
   for (; e < n; e += gridDim.x) {
     stage_obs<R, C>(smem, pre);
     __syncthreads();  // B1: input plane ready (and last env's pool reads done)
 
-    // ---- conv1: D[32 ch][pos] = W1 . im2col(in), position tiles split 4 ways
-#pragma unroll 1
-    for (int t = w; t < G::MT; t += 4) {
-      const int m = 32 * t + lr;
-      const unsigned char* base = smem + G::IN + (padded_pos<R, C>(m) - PC - 1) * G::S0;
-      f32x16 acc = {};
+    // ---- conv1: D[32 ch][pos] = W1 . im2col(in), position tiles split 4 ways; every
+    // read of the wave's tiles is issued before the first MFMA (a wave with fewer tiles
+    // repeats its last one, result not stored)
+    {
+      constexpr int NT1 = (G::MT + 3) / 4;
+      bf16x8 f1[NT1][kW1Steps];
 #pragma unroll
-      for (int s = 0; s < kW1Steps; ++s) {
-        const uint2 a = *reinterpret_cast<const uint2*>(base + off1a[s]);
-        const uint2 b = *reinterpret_cast<const uint2*>(base + off1b[s]);
-        const bf16x8 f = __builtin_bit_cast(bf16x8, make_uint4(a.x, a.y, b.x, b.y));
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1[s], f, acc, 0, 0, 0);
+      for (int i = 0; i < NT1; ++i) {
+        const unsigned char* base = smem + G::IN + (padded_pos<R, C>(32 * (w + 4 * i) + lr) - PC - 1) * G::S0;
+#pragma unroll
+        for (int s = 0; s < kW1Steps; ++s) {
+          const uint2 a = *reinterpret_cast<const uint2*>(base + off1a[s]);
+          const uint2 b = *reinterpret_cast<const uint2*>(base + off1b[s]);
+          f1[i][s] = __builtin_bit_cast(bf16x8, make_uint4(a.x, a.y, b.x, b.y));
+        }
       }
-      store_chan_major<R, C, G::S1>(smem + G::A1, bias, 0, acc, m, h);
+#pragma unroll
+      for (int i = 0; i < NT1; ++i) {
+        f32x16 acc = {};
+#pragma unroll
+        for (int s = 0; s < kW1Steps; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1[s], f1[i][s], acc, 0, 0, 0);
+        store_chan_major<R, C, G::S1>(smem + G::A1, bias, 0, acc, 32 * (w + 4 * i) + lr, h);
+      }
     }
     __syncthreads();  // B2: act1 ready
 
     const int en = e + gridDim.x;
     if (en < n) load_obs<R, C>(obs, en, pre);  // next env's observation in flight during conv2/3
 
-    // ---- conv2: D[32 ch of nh][pos] = W2 . im2col(act1)
-#pragma unroll 1
-    for (int t = mh; t < G::MT; t += 2) {
-      const int m = 32 * t + lr;
-      const unsigned char* base = smem + G::A1 + (padded_pos<R, C>(m) - PC - 1) * G::S1 + 16 * h;
-      f32x16 acc = {};
+    // ---- conv2: D[32 ch of nh][pos] = W2 . im2col(act1), k-outer: one LDS weight
+    // fragment per k-step feeds all of the wave's position tiles (accumulators in AGPRs);
+    // the (k-step, tile) reads run through a ring of kPre2 LDS reads in flight.  A wave with
+    // fewer tiles repeats its last one (clamped address, result not stored) instead of
+    // branching: its partner wave has the extra tile anyway.
+    {
+      constexpr int NT2 = G::NT2, NQ = kW2Steps * NT2, kPre2 = 6;
+      const unsigned char* base[NT2];
+      f32x16 acc[NT2];
 #pragma unroll
-      for (int s = 0; s < kW2Steps; ++s) {
-        const int tap = s >> 1;
-        const int off = ((tap / 3) * PC + (tap % 3)) * G::S1 + (s & 1) * 32;
-        const bf16x8 f = *reinterpret_cast<const bf16x8*>(base + off);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w2[s], f, acc, 0, 0, 0);
+      for (int i = 0; i < NT2; ++i) {
+        base[i] = smem + G::A1 + (padded_pos<R, C>(32 * (mh + 2 * i) + lr) - PC - 1) * G::S1 + 16 * h;
+        acc[i] = f32x16{};
       }
-      store_chan_major<R, C, G::S2>(smem + G::A2, bias + 32, 32 * nh, acc, m, h);
+      auto rd = [&](int q) {
+        const int s = q / NT2, tap = s >> 1;
+        return *reinterpret_cast<const bf16x8*>(base[q % NT2] + ((tap / 3) * PC + (tap % 3)) * G::S1 + (s & 1) * 32);
+      };
+      const bf16x8* wl = reinterpret_cast<const bf16x8*>(smem + G::W2) + nh * kW2Steps * 64 + l;
+      bf16x8 ring[kPre2];
+#pragma unroll
+      for (int q = 0; q < kPre2; ++q) ring[q] = rd(q);
+      bf16x8 wcur = wl[0], wnext = wcur;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int s = q / NT2, i = q % NT2;
+        if (i == 0 && s + 1 < kW2Steps) wnext = wl[(s + 1) * 64];
+        const bf16x8 f = ring[q % kPre2];
+        if (q + kPre2 < NQ) ring[q % kPre2] = rd(q + kPre2);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wcur, f, acc[i], 0, 0, 0);
+        if (i == NT2 - 1) wcur = wnext;
+      }
+#pragma unroll
+      for (int i = 0; i < NT2; ++i)
+        store_chan_major<R, C, G::S2>(smem + G::A2, bias + 32, 32 * nh, acc[i], 32 * (mh + 2 * i) + lr, h);
     }
     __syncthreads();  // B3: act2 ready
 
-    // ---- conv3: D[pos][32 ch of nh] = im2col(act2) . W3, then Y[cell][ch] += P . relu(D)
+    // ---- conv3: D[pos][32 ch of nh] = im2col(act2) . W3, then Y[cell][ch] += P . relu(D).
+    // The wave's (tile, k-step) sequence is one unrolled stream: A fragments run through a
+    // ring of kPre LDS reads in flight across tile boundaries, and a tile's pooling (VALU +
+    // 2 MFMAs) interleaves with the next tile's chain.  Tiles past MT (the shorter wave's
+    // last slot) have all-zero pool membership and add nothing.
     f32x16 Y = {};
-#pragma unroll 1
-    for (int t = mh; t < G::MT; t += 2) {
-      const int m = 32 * t + lr;
-      const unsigned char* base = smem + G::A2 + (padded_pos<R, C>(m) - PC - 1) * G::S2 + 16 * h;
-      f32x16 acc = {};
+    {
+      constexpr int NT2 = G::NT2, NQ = NT2 * kW3Steps, kPre = 7;
+      const unsigned char* base[NT2];
 #pragma unroll
-      for (int s = 0; s < kW3Steps; ++s) {
-        const int tap = s >> 2;
-        const int off = ((tap / 3) * PC + (tap % 3)) * G::S2 + (s & 3) * 32;
-        const bf16x8 f = *reinterpret_cast<const bf16x8*>(base + off);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, w3[s], acc, 0, 0, 0);
-      }
+      for (int i = 0; i < NT2; ++i)
+        base[i] = smem + G::A2 + (padded_pos<R, C>(32 * (mh + 2 * i) + lr) - PC - 1) * G::S2 + 16 * h;
+      auto rd = [&](int q) {
+        const int s = q % kW3Steps, tap = s >> 2;
+        return *reinterpret_cast<const bf16x8*>(base[q / kW3Steps] + ((tap / 3) * PC + (tap % 3)) * G::S2 +
+                                                (s & 3) * 32);
+      };
+      bf16x8 ring[kPre];
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        bf16x8 x, p;
-        const unsigned bits = smem[G::PM + (t * 2 + s) * 64 + l];
+      for (int q = 0; q < kPre; ++q) ring[q] = rd(q);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          x[j] = (__bf16)relu(acc[8 * s + j] + b3v);
-          p[j] = ((bits >> j) & 1u) ? (__bf16)1.0f : (__bf16)0.0f;
+      for (int i = 0; i < NT2; ++i) {
+        f32x16 acc = {};
+#pragma unroll
+        for (int s = 0; s < kW3Steps; ++s) {
+          const int q = i * kW3Steps + s;
+          const bf16x8 f = ring[q % kPre];
+          if (q + kPre < NQ) ring[q % kPre] = rd(q + kPre);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, w3[s], acc, 0, 0, 0);
         }
-        Y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p, x, Y, 0, 0, 0);
+        {
+          const int t = mh + 2 * i;
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            bf16x8 x, pf;
+            const unsigned bits = smem[G::PM + (t * 2 + k) * 64 + l];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              x[j] = (__bf16)relu(acc[8 * k + j] + b3v);
+              pf[j] = ((bits >> j) & 1u) ? (__bf16)1.0f : (__bf16)0.0f;
+            }
+            Y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf, x, Y, 0, 0, 0);
+          }
+        }
       }
     }
     // Y: lane = channel 32nh + lr, register r < 8 = cell (r & 3) + 8 (r >> 2) + 4h

@@ -167,6 +167,30 @@ int heist_solver_pack(const float* conv1_w, const float* conv1_b, const float* c
 int heist_solver_features(const float* obs, int n, int rows, int cols, const void* packed, float* feat_out,
                           heist_stream_t stream);
 
+/* Fused batched Solver head (networks.py:102-131 + agents/solver.py:75-99 select_action):
+ * x = relu(fc_spatial(feat)); one LSTM cell step (gate order i, f, g, o); logits =
+ * policy_head(h'), value = value_head(h'); action ~ Categorical(softmax(logits)) and its
+ * log_prob with torch's probs semantics.  GEMMs on bf16 MFMA (fp32 accumulate), cell
+ * update, last layers and sampling in fp32.  Requires hidden_dim 256, lstm_hidden 128,
+ * head width 128, 1 <= num_actions <= 7.
+ * heist_solver_head_pack: float32 parameters (torch layouts: fc_spatial.weight [256][1024],
+ * lstm.weight_ih_l0 [512][256], weight_hh_l0 [512][128], policy_head.0 / value_head.0
+ * .weight [128][128], policy_head.2.weight [A][128], value_head.2.weight [1][128], biases)
+ * -> packed (heist_solver_head_packed_bytes() bytes); call after every weight update.
+ * heist_solver_head: feat [n][1024] (heist_solver_features), h_in / c_in [n][128] or NULL
+ * (zero state); seed / counter select the sample (counter-based hash, one uniform per env);
+ * outputs logits [n][A] (may be NULL), value [n], action [n] int64, logp [n],
+ * h_out / c_out [n][128] (must not alias h_in / c_in). */
+int heist_solver_head_packed_bytes(void);
+int heist_solver_head_pack(const float* fc_w, const float* fc_b, const float* w_ih, const float* w_hh,
+                           const float* b_ih, const float* b_hh, const float* p1_w, const float* p1_b,
+                           const float* v1_w, const float* v1_b, const float* p2_w, const float* p2_b,
+                           const float* v2_w, const float* v2_b, int num_actions, void* packed,
+                           heist_stream_t stream);
+int heist_solver_head(const float* feat, const float* h_in, const float* c_in, int n, const void* packed,
+                      int num_actions, uint64_t seed, uint64_t counter, float* logits_out, float* value_out,
+                      int64_t* action_out, float* logp_out, float* h_out, float* c_out, heist_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -40,6 +40,11 @@ hipError_t launch_solver_pack(const float* w1, const float* b1, const float* w2,
                               const float* b3, void* packed, hipStream_t st);
 hipError_t launch_solver_conv(const float* obs, int n, int R, int C, const void* packed, float* feat, int n_cu,
                               hipStream_t st);
+int solver_head_packed_bytes();
+hipError_t launch_solver_head_pack(const float* const* w, int A, void* packed, hipStream_t st);
+hipError_t launch_solver_head(const float* feat, const float* h_in, const float* c_in, int n, const void* packed,
+                              int A, uint64_t seed, uint64_t counter, float* logits_out, float* value_out,
+                              int64_t* action_out, float* logp_out, float* h_out, float* c_out, hipStream_t st);
 hipError_t launch_gae(const float* r, const float* v, const uint8_t* d, const float* last_value, int T, int N,
                       double gamma, double lam, float* adv, float* ret, hipStream_t st);
 hipError_t launch_adv_moments(const float* x, int64_t n, int phase, double* acc, hipStream_t st);
@@ -397,4 +402,31 @@ int heist_solver_features(const float* obs, int n, int rows, int cols, const voi
     return rc;
   return check_hip(heist::launch_solver_conv(obs, n, rows, cols, packed, feat_out, n_cu, (hipStream_t)stream),
                    "heist_solver_features");
+}
+
+int heist_solver_head_packed_bytes(void) { return heist::solver_head_packed_bytes(); }
+
+int heist_solver_head_pack(const float* fc_w, const float* fc_b, const float* w_ih, const float* w_hh,
+                           const float* b_ih, const float* b_hh, const float* p1_w, const float* p1_b,
+                           const float* v1_w, const float* v1_b, const float* p2_w, const float* p2_b,
+                           const float* v2_w, const float* v2_b, int num_actions, void* packed,
+                           heist_stream_t stream) {
+  const float* w[14] = {fc_w, fc_b, w_ih, w_hh, b_ih, b_hh, p1_w, p1_b, v1_w, v1_b, p2_w, p2_b, v2_w, v2_b};
+  for (const float* x : w) HEIST_REQUIRE(x != nullptr, "heist_solver_head_pack: null pointer");
+  HEIST_REQUIRE(packed != nullptr, "heist_solver_head_pack: null packed");
+  HEIST_REQUIRE(num_actions >= 1 && num_actions <= 7, "heist_solver_head_pack: need 1 <= num_actions <= 7");
+  return check_hip(heist::launch_solver_head_pack(w, num_actions, packed, (hipStream_t)stream),
+                   "heist_solver_head_pack");
+}
+
+int heist_solver_head(const float* feat, const float* h_in, const float* c_in, int n, const void* packed,
+                      int num_actions, uint64_t seed, uint64_t counter, float* logits_out, float* value_out,
+                      int64_t* action_out, float* logp_out, float* h_out, float* c_out, heist_stream_t stream) {
+  HEIST_REQUIRE(feat && packed && value_out && action_out && logp_out && h_out && c_out,
+                "heist_solver_head: null pointer");
+  HEIST_REQUIRE(n >= 0, "heist_solver_head: n < 0");
+  HEIST_REQUIRE(num_actions >= 1 && num_actions <= 7, "heist_solver_head: need 1 <= num_actions <= 7");
+  return check_hip(heist::launch_solver_head(feat, h_in, c_in, n, packed, num_actions, seed, counter, logits_out,
+                                             value_out, action_out, logp_out, h_out, c_out, (hipStream_t)stream),
+                   "heist_solver_head");
 }

@@ -408,4 +408,294 @@ hipError_t launch_solver_conv(const float* obs, int n, int R, int C, const void*
   return hipErrorInvalidValue;
 }
 
+// ===========================================================================
+// Fused Solver head: fc_spatial + ReLU, one LSTM cell step, policy/value heads,
+// softmax, Categorical sample and log-prob (networks.py:102-131, agents/solver.py:75-99)
+// for blocks of 32 envs.  GEMMs on v_mfma_f32_32x32x16_bf16 (activations bf16 in LDS,
+// weights as packed fragments streamed from L2, fp32 accumulate); the LSTM elementwise
+// math, the last head layers (128 -> A, 128 -> 1) and the sampling in fp32.
+// ===========================================================================
+
+// Packed head blob, uint4 units: Wfc [8 nt][64 ks][64], Wg = [W_ih | W_hh] [16][24][64],
+// Wh1 = [policy_head.0 ; value_head.0] [8][8][64]; then floats.
+constexpr int kHFc = 0;
+constexpr int kHG = kHFc + 8 * 64 * 64;
+constexpr int kHH1 = kHG + 16 * 24 * 64;
+constexpr int kHF32 = kHH1 + 8 * 8 * 64;
+// float offsets inside the f32 area
+constexpr int kFBfc = 0, kFBg = 256, kFBh1 = 768, kFWp2 = 1024, kFBp2 = 1024 + 8 * 128, kFWv2 = kFBp2 + 8,
+              kFBv2 = kFWv2 + 128, kFEnd = kFBv2 + 4;
+constexpr int kHeadPackedBytes = kHF32 * 16 + kFEnd * 4;
+constexpr int kMaxActions = 7;
+
+struct HeadLds {  // byte offsets
+  static constexpr int X0S = 1032 * 2, X1S = 264 * 2, HS = 136 * 2, HVS = 260 * 4;
+  static constexpr int X0 = 0;
+  static constexpr int X1 = X0 + 32 * X0S;
+  static constexpr int HP = X1 + 32 * X1S;
+  static constexpr int HN = HP + 32 * HS;
+  static constexpr int HV = HN + 32 * HS;
+  static constexpr int OUT = HV + 32 * HVS;  // [32][8] f32
+  static constexpr int LDS = OUT + 32 * 8 * 4;
+};
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
+  z ^= z >> 30;
+  z *= 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 27;
+  z *= 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return z;
+}
+
+// acc[t] += A(LDS rows, k-steps [ks0, ks0+KS)) . B(fragments of n-tiles nts[t], from global)
+template <int NTL, int KS>
+__device__ __forceinline__ void head_gemm(f32x16 (&acc)[NTL], const unsigned char* abase, int astride_ks,
+                                          const uint4* __restrict__ bfr, const int (&bidx)[NTL], int l) {
+  constexpr int kPre = 4;
+  bf16x8 ring[kPre][NTL];
+#pragma unroll
+  for (int q = 0; q < kPre; ++q)
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) ring[q][t] = __builtin_bit_cast(bf16x8, bfr[bidx[t] + q * 64 + l]);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    const bf16x8 a = *reinterpret_cast<const bf16x8*>(abase + ks * astride_ks);
+#pragma unroll
+    for (int t = 0; t < NTL; ++t) {
+      const bf16x8 b = ring[ks % kPre][t];
+      if (ks + kPre < KS) ring[ks % kPre][t] = __builtin_bit_cast(bf16x8, bfr[bidx[t] + (ks + kPre) * 64 + l]);
+      acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[t], 0, 0, 0);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void solver_head_kernel(const float* __restrict__ feat,
+                                                             const float* __restrict__ h_in,
+                                                             const float* __restrict__ c_in, int n,
+                                                             const uint4* __restrict__ packed, int A, uint64_t seed,
+                                                             uint64_t counter, float* __restrict__ logits_out,
+                                                             float* __restrict__ value_out,
+                                                             int64_t* __restrict__ action_out,
+                                                             float* __restrict__ logp_out, float* __restrict__ h_out,
+                                                             float* __restrict__ c_out) {
+  using L = HeadLds;
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, h = l >> 5, lr = l & 31;
+  const int e0 = blockIdx.x * 32;
+  const float* fp = reinterpret_cast<const float*>(packed + kHF32);
+
+  // ---- stage 0: features and h_prev -> bf16 rows in LDS (rows past n repeat row n-1)
+  for (int i = tid; i < 32 * 256; i += 256) {
+    const int r = i >> 8, q = i & 255;
+    const int e = min(e0 + r, n - 1);
+    const float4 v = reinterpret_cast<const float4*>(feat + (size_t)e * 1024)[q];
+    bf16x4 b;
+    b[0] = (__bf16)v.x; b[1] = (__bf16)v.y; b[2] = (__bf16)v.z; b[3] = (__bf16)v.w;
+    *reinterpret_cast<bf16x4*>(smem + L::X0 + r * L::X0S + q * 8) = b;
+  }
+  for (int i = tid; i < 32 * 32; i += 256) {
+    const int r = i >> 5, q = i & 31;
+    const int e = min(e0 + r, n - 1);
+    const float4 v = h_in ? reinterpret_cast<const float4*>(h_in + (size_t)e * 128)[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    bf16x4 b;
+    b[0] = (__bf16)v.x; b[1] = (__bf16)v.y; b[2] = (__bf16)v.z; b[3] = (__bf16)v.w;
+    *reinterpret_cast<bf16x4*>(smem + L::HP + r * L::HS + q * 8) = b;
+  }
+  __syncthreads();
+
+  // ---- stage 1: x = relu(feat . Wfc^T + b) [32 x 256]; wave w: n-tiles w, w + 4
+  {
+    f32x16 acc[2] = {f32x16{}, f32x16{}};
+    const int bidx[2] = {(w * 64) * 64, ((w + 4) * 64) * 64};
+    head_gemm<2, 64>(acc, smem + L::X0 + lr * L::X0S + 16 * h, 32, packed + kHFc, bidx, l);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int nn = 32 * (w + 4 * t) + lr;
+      const float b = fp[kFBfc + nn];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        *reinterpret_cast<__bf16*>(smem + L::X1 + row * L::X1S + nn * 2) = (__bf16)relu(acc[t][r] + b);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- stage 2: gates = [x | h] . [W_ih | W_hh]^T + b_ih + b_hh; wave w owns hidden units
+  // 32w..32w+31 of all four gates (i, f, g, o), so the cell update stays in registers
+  {
+    f32x16 acc[4] = {f32x16{}, f32x16{}, f32x16{}, f32x16{}};
+    const int bidx[4] = {(w * 24) * 64, ((w + 4) * 24) * 64, ((w + 8) * 24) * 64, ((w + 12) * 24) * 64};
+    head_gemm<4, 16>(acc, smem + L::X1 + lr * L::X1S + 16 * h, 32, packed + kHG, bidx, l);
+    const int bidx2[4] = {bidx[0] + 16 * 64, bidx[1] + 16 * 64, bidx[2] + 16 * 64, bidx[3] + 16 * 64};
+    head_gemm<4, 8>(acc, smem + L::HP + lr * L::HS + 16 * h, 32, packed + kHG, bidx2, l);
+    const int j = 32 * w + lr;
+    const float bi = fp[kFBg + j], bf = fp[kFBg + 128 + j], bg = fp[kFBg + 256 + j], bo = fp[kFBg + 384 + j];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int e = e0 + row;
+      const float cprev = (c_in && e < n) ? c_in[(size_t)e * 128 + j] : 0.0f;
+      const float c1 = sigmoidf_(acc[1][r] + bf) * cprev + sigmoidf_(acc[0][r] + bi) * tanhf(acc[2][r] + bg);
+      const float h1 = sigmoidf_(acc[3][r] + bo) * tanhf(c1);
+      if (e < n) {
+        c_out[(size_t)e * 128 + j] = c1;
+        h_out[(size_t)e * 128 + j] = h1;
+      }
+      *reinterpret_cast<__bf16*>(smem + L::HN + row * L::HS + j * 2) = (__bf16)h1;
+    }
+  }
+  __syncthreads();
+
+  // ---- stage 3: head hidden layers relu(h' . [Wp1 ; Wv1]^T + b) [32 x 256] (f32 in LDS)
+  {
+    f32x16 acc[2] = {f32x16{}, f32x16{}};
+    const int bidx[2] = {(w * 8) * 64, ((w + 4) * 8) * 64};
+    head_gemm<2, 8>(acc, smem + L::HN + lr * L::HS + 16 * h, 32, packed + kHH1, bidx, l);
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int nn = 32 * (w + 4 * t) + lr;
+      const float b = fp[kFBh1 + nn];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
+        reinterpret_cast<float*>(smem + L::HV + row * L::HVS)[nn] = relu(acc[t][r] + b);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- stage 4: logits (128 -> A) and value (128 -> 1) in fp32; thread = (env, output)
+  {
+    const int row = tid >> 3, o = tid & 7;
+    const float* hv = reinterpret_cast<const float*>(smem + L::HV + row * L::HVS);
+    float acc = 0.f;
+    if (o < A) {
+      const float* wr = fp + kFWp2 + o * 128;
+      for (int k = 0; k < 128; ++k) acc += hv[k] * wr[k];
+      acc += fp[kFBp2 + o];
+    } else if (o == 7) {
+      const float* wr = fp + kFWv2;
+      for (int k = 0; k < 128; ++k) acc += hv[128 + k] * wr[k];
+      acc += fp[kFBv2];
+    }
+    reinterpret_cast<float*>(smem + L::OUT)[row * 8 + o] = acc;
+  }
+  __syncthreads();
+
+  // ---- stage 5: Categorical(probs = softmax(logits)): sample, log_prob (torch semantics:
+  // probs renormalised, log(clamp(p, eps, 1 - eps)))
+  if (tid < 32 && e0 + tid < n) {
+    const int e = e0 + tid;
+    const float* lg = reinterpret_cast<const float*>(smem + L::OUT) + tid * 8;
+    float mx = lg[0];
+    for (int a = 1; a < A; ++a) mx = fmaxf(mx, lg[a]);
+    float p[kMaxActions], s = 0.f;
+    for (int a = 0; a < A; ++a) {
+      p[a] = __expf(lg[a] - mx);
+      s += p[a];
+    }
+    float ps = 0.f;
+    for (int a = 0; a < A; ++a) {
+      p[a] = p[a] / s;
+      ps += p[a];
+    }
+    const uint64_t z = mix64(seed ^ (counter * 0xD1B54A32D192ED03ull) ^ ((uint64_t)e * 0x9E3779B97F4A7C15ull));
+    const float u = (float)(z >> 40) * 0x1p-24f * ps;
+    int act = A - 1;
+    float cum = 0.f;
+    for (int a = 0; a < A; ++a) {
+      cum += p[a];
+      if (u < cum) { act = a; break; }
+    }
+    const float eps = 1.1920928955078125e-07f;
+    float pa = p[act] / ps;
+    pa = fminf(fmaxf(pa, eps), 1.0f - eps);
+    if (logits_out)
+      for (int a = 0; a < A; ++a) logits_out[(size_t)e * A + a] = lg[a];
+    value_out[e] = lg[7];
+    action_out[e] = act;
+    logp_out[e] = __logf(pa);
+  }
+}
+
+// Fragment packing for the head: fragment (nt, ks, lane) element j = W[32 nt + (lane & 31)][k]
+// with k = 16 ks + 8 (lane >> 5) + j (bf16 RNE); f32 tail copied (b_ih + b_hh summed).
+__global__ void solver_head_pack_kernel(const float* __restrict__ fc_w, const float* __restrict__ fc_b,
+                                        const float* __restrict__ w_ih, const float* __restrict__ w_hh,
+                                        const float* __restrict__ b_ih, const float* __restrict__ b_hh,
+                                        const float* __restrict__ p1_w, const float* __restrict__ p1_b,
+                                        const float* __restrict__ v1_w, const float* __restrict__ v1_b,
+                                        const float* __restrict__ p2_w, const float* __restrict__ p2_b,
+                                        const float* __restrict__ v2_w, const float* __restrict__ v2_b, int A,
+                                        uint4* __restrict__ packed) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < kHF32) {
+    const int l = i & 63, f = i >> 6;
+    const int r = l & 31, hh = l >> 5;
+    const float* src;
+    int ld, nn, k0;
+    if (i < kHG) {
+      const int nt = f / 64, ks = f % 64;
+      src = fc_w; ld = 1024; nn = 32 * nt + r; k0 = 16 * ks + 8 * hh;
+    } else if (i < kHH1) {
+      const int g = f - kHG / 64, nt = g / 24, ks = g % 24;
+      nn = 32 * nt + r;
+      if (ks < 16) { src = w_ih; ld = 256; k0 = 16 * ks + 8 * hh; }
+      else { src = w_hh; ld = 128; k0 = 16 * (ks - 16) + 8 * hh; }
+    } else {
+      const int g = f - kHH1 / 64, nt = g / 8, ks = g % 8;
+      nn = 32 * nt + r;
+      ld = 128; k0 = 16 * ks + 8 * hh;
+      src = nn < 128 ? p1_w : v1_w;
+      if (nn >= 128) nn -= 128;
+    }
+    bf16x8 fr;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fr[j] = (__bf16)src[(size_t)nn * ld + k0 + j];
+    packed[i] = __builtin_bit_cast(uint4, fr);
+  } else if (i < kHF32 + kFEnd) {
+    const int k = i - kHF32;
+    float v = 0.f;
+    if (k < kFBg) v = fc_b[k];
+    else if (k < kFBh1) v = b_ih[k - kFBg] + b_hh[k - kFBg];
+    else if (k < kFWp2) v = (k - kFBh1) < 128 ? p1_b[k - kFBh1] : v1_b[k - kFBh1 - 128];
+    else if (k < kFBp2) { const int o = (k - kFWp2) / 128; v = o < A ? p2_w[(k - kFWp2)] : 0.f; }
+    else if (k < kFWv2) v = (k - kFBp2) < A ? p2_b[k - kFBp2] : 0.f;
+    else if (k < kFBv2) v = v2_w[k - kFWv2];
+    else v = k == kFBv2 ? v2_b[0] : 0.f;
+    reinterpret_cast<float*>(packed + kHF32)[k] = v;
+  }
+}
+
+int solver_head_packed_bytes() { return kHeadPackedBytes; }
+
+hipError_t launch_solver_head_pack(const float* const* w, int A, void* packed, hipStream_t st) {
+  const int total = kHF32 + kFEnd;
+  hipLaunchKernelGGL(solver_head_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w[0], w[1], w[2], w[3],
+                     w[4], w[5], w[6], w[7], w[8], w[9], w[10], w[11], w[12], w[13], A,
+                     reinterpret_cast<uint4*>(packed));
+  return hipGetLastError();
+}
+
+hipError_t launch_solver_head(const float* feat, const float* h_in, const float* c_in, int n, const void* packed,
+                              int A, uint64_t seed, uint64_t counter, float* logits_out, float* value_out,
+                              int64_t* action_out, float* logp_out, float* h_out, float* c_out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&solver_head_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, HeadLds::LDS);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(solver_head_kernel, dim3((n + 31) / 32), dim3(256), HeadLds::LDS, st, feat, h_in, c_in, n,
+                     reinterpret_cast<const uint4*>(packed), A, seed, counter, logits_out, value_out, action_out,
+                     logp_out, h_out, c_out);
+  return hipGetLastError();
+}
+
 }  // namespace heist

@@ -68,7 +68,9 @@ class SolverAgent:  # agents/solver.py:18-259
         self.max_grad_norm = max_grad_norm
         self.ppo_epochs = ppo_epochs
         self.batch_size = batch_size
-        self.fused_inference = fused_inference  # batched act(): bf16-MFMA backbone kernel
+        self.fused_inference = fused_inference  # batched act(): bf16-MFMA backbone + head kernels
+        self._act_seed = int(torch.initial_seed()) ^ 0x5EED
+        self._act_counter = 0
         self.device = torch.device(device) if device is not None else DEVICE
         self.network = SolverNetwork(grid_rows=grid_rows, grid_cols=grid_cols, num_actions=num_actions).to(self.device)
         self.optimizer = torch.optim.Adam(self.network.parameters(), lr=lr)
@@ -170,6 +172,16 @@ class SolverAgent:  # agents/solver.py:18-259
         reference fp32 forward."""
         self.network.eval()
         use = self.fused_inference if fused is None else fused
+        if use and self.network.fused_supported(obs) and self.network.head_supported():
+            # whole select_action on the fused kernels; the sample comes from a counter-based
+            # hash of (seed, call counter, env), so no generator state is consumed per call
+            if generator is not None:
+                seed = int(torch.randint(0, 2 ** 62, (1,), generator=generator, device=generator.device).item())
+            else:
+                seed = self._act_seed
+            self._act_counter += 1
+            action, logp, value, hidden, _ = self.network.act_fused(obs, hidden, seed, self._act_counter)
+            return action, logp, value, hidden
         if use and self.network.fused_supported(obs):
             logits, value, hidden = self.network.forward_fused(obs, hidden)
         else:

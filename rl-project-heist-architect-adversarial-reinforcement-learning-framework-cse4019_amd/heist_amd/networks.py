@@ -109,6 +109,60 @@ class SolverNetwork(nn.Module):  # networks.py:13-131
                                                           _native.stream(x.device)), "heist_solver_features")
         return out
 
+    def head_supported(self) -> bool:
+        """The fused head kernel's fixed widths (networks.py:38-60 defaults)."""
+        return (self.hidden_dim == 256 and self.lstm_hidden == 128 and self.policy_head[0].out_features == 128
+                and self.value_head[0].out_features == 128 and 1 <= self.policy_head[2].out_features <= 7)
+
+    def _packed_head(self) -> torch.Tensor:
+        from . import _native
+        mods = [self.fc_spatial.weight, self.fc_spatial.bias, self.lstm.weight_ih_l0, self.lstm.weight_hh_l0,
+                self.lstm.bias_ih_l0, self.lstm.bias_hh_l0, self.policy_head[0].weight, self.policy_head[0].bias,
+                self.value_head[0].weight, self.value_head[0].bias, self.policy_head[2].weight,
+                self.policy_head[2].bias, self.value_head[2].weight, self.value_head[2].bias]
+        key = tuple((t.data_ptr(), t._version) for t in mods)
+        cache = getattr(self, "_head_cache", None)
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        dev = self.fc_spatial.weight.device
+        L = _native.lib()
+        buf = torch.empty(L.heist_solver_head_packed_bytes(), dtype=torch.uint8, device=dev)
+        ws = [t.detach().float().contiguous() for t in mods]
+        _native.check(L.heist_solver_head_pack(*(_native.ptr(t) for t in ws), self.policy_head[2].out_features,
+                                               _native.ptr(buf), _native.stream(dev)), "heist_solver_head_pack")
+        self._head_cache = (key, buf, ws)
+        return buf
+
+    @torch.no_grad()
+    def act_fused(self, state: torch.Tensor, hidden: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                  seed: int = 0, counter: int = 0, want_logits: bool = False):
+        """get_action (networks.py:124-131) for a batch, entirely on the fused kernels:
+        backbone (heist_solver_features) + head (heist_solver_head: fc, LSTM cell, heads,
+        Categorical sample).  Returns (action [B] int64, log_prob [B], value [B],
+        (h, c) [1,B,128], logits [B,A] or None)."""
+        from . import _native
+        b = state.shape[0]
+        feat = self.features_fused(state)
+        dev = feat.device
+        A = self.policy_head[2].out_features
+        packed = self._packed_head()
+        h_in = c_in = None
+        if hidden is not None:
+            h_in = hidden[0].reshape(b, self.lstm_hidden).float().contiguous()
+            c_in = hidden[1].reshape(b, self.lstm_hidden).float().contiguous()
+        h1 = torch.empty(1, b, self.lstm_hidden, device=dev)
+        c1 = torch.empty(1, b, self.lstm_hidden, device=dev)
+        value = torch.empty(b, device=dev)
+        action = torch.empty(b, dtype=torch.int64, device=dev)
+        logp = torch.empty(b, device=dev)
+        logits = torch.empty(b, A, device=dev) if want_logits else None
+        _native.check(_native.lib().heist_solver_head(
+            _native.ptr(feat), _native.ptr(h_in), _native.ptr(c_in), b, _native.ptr(packed), A,
+            seed & 0xFFFFFFFFFFFFFFFF, counter & 0xFFFFFFFFFFFFFFFF, _native.ptr(logits), _native.ptr(value),
+            _native.ptr(action), _native.ptr(logp), _native.ptr(h1), _native.ptr(c1), _native.stream(dev)),
+            "heist_solver_head")
+        return action, logp, value, (h1, c1), logits
+
     @torch.no_grad()
     def forward_fused(self, state: torch.Tensor, hidden: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
         """forward() with the conv backbone on the fused HIP kernel (rollout inference)."""

@@ -163,3 +163,93 @@ def test_unsupported_grid_rejected(gpu_device):
     net = SolverNetwork(16, 16).to(gpu_device)
     with pytest.raises(_native.HeistError):
         net.features_fused(torch.zeros(2, 3, 16, 16, device=gpu_device))
+
+
+# ---------------------------------------------------------------------------------
+# fused head: fc_spatial + LSTM cell + heads + Categorical sample (heist_solver_head)
+# ---------------------------------------------------------------------------------
+
+def _big_heads(net):
+    """Head weights with gain 1 (the reference's 0.01-gain init makes logits ~0)."""
+    for m in (net.fc_spatial, net.policy_head[0], net.policy_head[2], net.value_head[0], net.value_head[2]):
+        torch.nn.init.orthogonal_(m.weight, gain=1.0)
+        torch.nn.init.uniform_(m.bias, -0.1, 0.1)
+    return net
+
+
+def emulate_head(net, feat, h, c):
+    """float64 CPU restatement of heist_solver_head's arithmetic (bf16 GEMM operands,
+    fp32 biases with b_ih + b_hh summed in fp32, fp32/fp64 elsewhere)."""
+    W = lambda t: t.detach().double().cpu()  # noqa: E731
+    Bf = lambda t: t.detach().float().double().cpu()  # noqa: E731
+    x = _bf(F.relu(_bf(feat.double().cpu()) @ _bf(W(net.fc_spatial.weight)).T + Bf(net.fc_spatial.bias)))
+    bg = (net.lstm.bias_ih_l0.detach().float() + net.lstm.bias_hh_l0.detach().float()).double().cpu()
+    gates = x @ _bf(W(net.lstm.weight_ih_l0)).T + _bf(h.double().cpu()) @ _bf(W(net.lstm.weight_hh_l0)).T + bg
+    i, f, g, o = gates.chunk(4, 1)
+    c1 = torch.sigmoid(f) * c.double().cpu() + torch.sigmoid(i) * torch.tanh(g)
+    h1 = torch.sigmoid(o) * torch.tanh(c1)
+    hn = _bf(h1)
+    hp = F.relu(hn @ _bf(W(net.policy_head[0].weight)).T + Bf(net.policy_head[0].bias))
+    hv = F.relu(hn @ _bf(W(net.value_head[0].weight)).T + Bf(net.value_head[0].bias))
+    logits = hp @ W(net.policy_head[2].weight).T + Bf(net.policy_head[2].bias)
+    value = (hv @ W(net.value_head[2].weight).T + Bf(net.value_head[2].bias)).reshape(-1)
+    return logits, value, h1, c1
+
+
+@pytest.mark.parametrize("n", [1, 33, 4096])
+def test_head_matches_emulation(gpu_device, n):
+    torch.manual_seed(n)
+    net = _big_heads(SolverNetwork().to(gpu_device))
+    obs = env_obs(n, 20, gpu_device, seed=n + 1)
+    feat = net.features_fused(obs)
+    h = torch.randn(1, n, 128, device=gpu_device) * 0.5
+    c = torch.randn(1, n, 128, device=gpu_device) * 0.5
+    a, lp, v, (h1, c1), lg = net.act_fused(obs, (h, c), seed=1, counter=2, want_logits=True)
+    rows = torch.arange(n) if n <= 64 else torch.tensor([0, 1, 31, 32, 1000, 2047, 4064, 4095])
+    r_lg, r_v, r_h, r_c = emulate_head(net, feat[rows.to(gpu_device)], h[0, rows], c[0, rows])
+    for got, ref in ((lg[rows.to(gpu_device)], r_lg), (v[rows.to(gpu_device)], r_v),
+                     (h1[0, rows.to(gpu_device)], r_h), (c1[0, rows.to(gpu_device)], r_c)):
+        mx, mean = _rel(got, ref)
+        assert mx < TOL_EMU_MAX and mean < TOL_EMU_MEAN, (mx, mean)
+    # log-prob of the sampled action under Categorical(softmax(logits)) (torch semantics)
+    ref_lp = torch.distributions.Categorical(F.softmax(lg, -1)).log_prob(a)
+    assert (lp - ref_lp).abs().max().item() < 1e-5
+    assert ((a >= 0) & (a < 5)).all()
+
+
+def test_head_zero_state_and_reference_forward(gpu_device):
+    """hidden=None is the zero state; the whole fused act tracks the fp32 forward over a
+    3-step LSTM rollout within bf16 precision."""
+    torch.manual_seed(21)
+    net = _big_heads(SolverNetwork().to(gpu_device))
+    obs = [env_obs(128, 20, gpu_device, seed=s) for s in range(3)]
+    hid_f = hid_r = None
+    for o in obs:
+        a, lp, v, hid_f, lg = net.act_fused(o, hid_f, want_logits=True)
+        with torch.no_grad():
+            l_ref, v_ref, hid_r = net(o, hid_r)
+        assert _rel(lg, l_ref)[0] < TOL_F32_MAX
+        assert _rel(v, v_ref.reshape(-1))[0] < TOL_F32_MAX
+        assert _rel(hid_f[0], hid_r[0])[0] < TOL_F32_MAX and _rel(hid_f[1], hid_r[1])[0] < TOL_F32_MAX
+
+
+def test_head_sampling_distribution(gpu_device):
+    """Actions follow softmax(logits): aggregated counts over 4096 envs x 16 draws match
+    the summed probabilities (chi-square, 4 dof); draws are deterministic in (seed,
+    counter) and differ across counters."""
+    torch.manual_seed(8)
+    net = _big_heads(SolverNetwork().to(gpu_device))
+    obs = env_obs(4096, 20, gpu_device, seed=3)
+    counts = torch.zeros(5, dtype=torch.float64)
+    expect = torch.zeros(5, dtype=torch.float64)
+    acts = []
+    for k in range(16):
+        a, lp, v, _, lg = net.act_fused(obs, None, seed=77, counter=k, want_logits=True)
+        counts += torch.bincount(a.cpu(), minlength=5).double()
+        expect += F.softmax(lg.double(), -1).sum(0).cpu()
+        acts.append(a)
+    chi2 = (((counts - expect) ** 2) / expect).sum().item()
+    assert chi2 < 25.0, (chi2, counts, expect)  # p ~ 5e-5 at 4 dof
+    a_again, *_ = net.act_fused(obs, None, seed=77, counter=3)
+    assert torch.equal(a_again, acts[3])
+    assert not torch.equal(acts[0], acts[1])

@@ -63,7 +63,7 @@ def cpu_baseline(layouts, cfg, budget, target_s=10.0, threads=1):
 
 
 def measure_rollout(env, dev, steps=20, warmup=3):
-    """env step + batched Solver forward (fp32, carried LSTM state) + action sampling."""
+    """env step + batched Solver select_action on the fused kernels (carried LSTM state)."""
     from heist_amd.agents import SolverAgent
     ag = SolverAgent(env.rows, env.cols, device=dev)
     h = c = torch.zeros(1, env.n_envs, 128, device=dev)
@@ -76,17 +76,55 @@ def measure_rollout(env, dev, steps=20, warmup=3):
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     return {"value": steps * env.n_envs / dt, "unit": "env-steps/s", "ms_per_step": dt / steps * 1e3,
-            "dtype": "fp32 policy", "note": "heist_step + SolverNetwork forward on PyTorch-ROCm + multinomial"}
+            "dtype": "bf16 MFMA policy (fp32 accumulate)",
+            "note": "heist_step + fused Solver select_action (backbone + head kernels), carried LSTM state"}
 
 
-def measure_train(cfg, dev, n_envs, rollout_len=32, minibatch=16384):
+SOLVER_BACKBONE_FLOP = 2 * 400 * (32 * 27 + 64 * 288 + 64 * 576)  # conv1..3 MACs x 2 at 20x20, per env
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
+
+
+def measure_policy(dev, n, iters=50, warmup=5):
+    """Batched Solver select_action on the fused kernels (heist_solver_features +
+    heist_solver_head) and the backbone kernel alone, timed with HIP events."""
+    from heist_amd.agents import SolverAgent
+    ag = SolverAgent(20, 20, device=dev)
+    net = ag.network
+    obs = torch.rand(n, 3, 20, 20, device=dev)
+    h = c = torch.zeros(1, n, 128, device=dev)
+    st = torch.cuda.current_stream(dev)
+
+    def timed(fn):
+        for _ in range(warmup):
+            fn()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        for _ in range(iters):
+            fn()
+        b.record(st)
+        torch.cuda.synchronize(dev)
+        return a.elapsed_time(b) / iters
+    ms_bb = timed(lambda: net.features_fused(obs))
+    ms_act = timed(lambda: ag.act(obs, (h, c)))
+    tf = SOLVER_BACKBONE_FLOP * n / (ms_bb * 1e-3) / 1e12
+    return {"value": n / (ms_act * 1e-3), "unit": "env-steps/s", "ms_per_step": ms_act,
+            "dtype": "bf16 MFMA (fp32 accumulate)",
+            "note": "batched SolverAgent.act: fused conv backbone + fc/LSTM/heads/sample kernels",
+            "backbone_roofline": {"bound": "mfma", "kernel": "heist::solver_conv_kernel<20,20>",
+                                  "kernel_ms": ms_bb, "achieved": tf, "peak": MFMA_BF16_PEAK_TFLOPS,
+                                  "unit": "TFLOP/s", "frac": tf / MFMA_BF16_PEAK_TFLOPS,
+                                  "flop_per_env": SOLVER_BACKBONE_FLOP}}
+
+
+def measure_train(cfg, dev, n_envs, rollout_len=32, minibatch=16384, update_precision="fp32"):
     """Batched AdversarialTrainer iteration: rollout + heist_gae + adv-norm + 3 PPO epochs
     (heist_ppo_loss, Adam) + Architect scoring/update/re-layout."""
     from heist_amd.training import AdversarialTrainer
     import tempfile
     d = tempfile.mkdtemp()
     tr = AdversarialTrainer(cfg, solver_episodes_per_layout=4, total_episodes=10 ** 9, save_dir=d, log_dir=d,
-                            n_envs=n_envs, rollout_len=rollout_len, minibatch=minibatch, device=dev, seed=0)
+                            n_envs=n_envs, rollout_len=rollout_len, minibatch=minibatch, device=dev, seed=0,
+                            update_precision=update_precision)
     tr._assign_layouts(np.arange(n_envs))
     tr.train_iteration()
     torch.cuda.synchronize(dev)
@@ -95,7 +133,8 @@ def measure_train(cfg, dev, n_envs, rollout_len=32, minibatch=16384):
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     return {"value": rollout_len * n_envs / dt, "unit": "env-steps/s", "s_per_iteration": dt,
-            "config": "T=%d x %d envs, 3 epochs, minibatch %d, fp32" % (rollout_len, n_envs, minibatch)}
+            "config": "T=%d x %d envs, 3 epochs, minibatch %d; rollout policy bf16 fused kernels, PPO update %s "
+                      "(NHWC MIOpen convs)" % (rollout_len, n_envs, minibatch, update_precision)}
 
 
 def main():
@@ -201,7 +240,9 @@ def main():
         }
         if not args.no_secondary:
             line["secondary"] = {"rollout": measure_rollout(env, dev),
-                                 "full_train": measure_train(cfg, dev, N)}
+                                 "policy_inference": measure_policy(dev, N),
+                                 "full_train": measure_train(cfg, dev, N),
+                                 "full_train_bf16_update": measure_train(cfg, dev, N, update_precision="bf16")}
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(layouts, cfg, args.budget, target_s=args.cpu_seconds, threads=1)
         print(json.dumps(line), flush=True)

@@ -56,7 +56,8 @@ class SolverAgent:  # agents/solver.py:18-259
     def __init__(self, grid_rows: int = 20, grid_cols: int = 20, num_actions: int = 5, lr: float = 3e-4,
                  gamma: float = 0.99, gae_lambda: float = 0.95, clip_epsilon: float = 0.2,
                  entropy_coeff: float = 0.05, value_coeff: float = 0.5, max_grad_norm: float = 0.5,
-                 ppo_epochs: int = 3, batch_size: int = 64, device=None, fused_inference: bool = True):
+                 ppo_epochs: int = 3, batch_size: int = 64, device=None, fused_inference: bool = True,
+                 update_precision: str = "fp32"):
         self.grid_rows = grid_rows
         self.grid_cols = grid_cols
         self.num_actions = num_actions
@@ -73,6 +74,12 @@ class SolverAgent:  # agents/solver.py:18-259
         self._act_counter = 0
         self.device = torch.device(device) if device is not None else DEVICE
         self.network = SolverNetwork(grid_rows=grid_rows, grid_cols=grid_cols, num_actions=num_actions).to(self.device)
+        if self.device.type == "cuda":  # NHWC convolutions: MIOpen's faster layout (same values, same state_dict)
+            self.network = self.network.to(memory_format=torch.channels_last)
+        if update_precision not in ("fp32", "bf16"):
+            raise ValueError("update_precision must be 'fp32' or 'bf16'")
+        # "fp32": the reference's arithmetic; "bf16": autocast forward/backward in the PPO update
+        self.update_precision = update_precision
         self.optimizer = torch.optim.Adam(self.network.parameters(), lr=lr)
         self.hidden = None
         self.states, self.actions, self.log_probs, self.values, self.rewards, self.dones = [], [], [], [], [], []
@@ -148,7 +155,12 @@ class SolverAgent:  # agents/solver.py:18-259
             idx = torch.as_tensor(perm_fn(n), device=self.device)
             for start in range(0, n, bs):
                 b = idx[start:start + bs]
-                logits, new_values, _ = self.network(states[b])
+                x = states[b]
+                if x.is_cuda:
+                    x = x.contiguous(memory_format=torch.channels_last)
+                with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.update_precision == "bf16" and x.is_cuda):
+                    logits, new_values, _ = self.network(x)
+                logits, new_values = logits.float(), new_values.float()
                 loss, parts = ppo_loss(logits, new_values.reshape(-1), actions[b], old_logp[b], adv[b], ret[b],
                                        self.clip_epsilon, self.value_coeff, self.entropy_coeff)
                 self.optimizer.zero_grad(set_to_none=False)

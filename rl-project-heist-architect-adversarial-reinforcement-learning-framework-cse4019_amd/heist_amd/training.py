@@ -103,7 +103,7 @@ class AdversarialTrainer:  # training.py:115-790
                  total_episodes: int = 500, save_dir: str = "checkpoints", log_dir: str = "logs",
                  architect_lr: float = 3e-4, solver_lr: float = 1e-3, n_envs: int = 256,
                  rollout_len: Optional[int] = None, minibatch: int = 4096, device=None, max_budget: Optional[int] = None,
-                 seed: Optional[int] = None):
+                 seed: Optional[int] = None, update_precision: str = "fp32"):
         self.config = config or EnvironmentConfig()
         self.solver_episodes = solver_episodes_per_layout
         self.total_episodes = total_episodes
@@ -123,7 +123,8 @@ class AdversarialTrainer:  # training.py:115-790
         R, C = self.config.grid_rows, self.config.grid_cols
         self.architect = ArchitectAgent(grid_rows=R, grid_cols=C, budget=self.config.architect_budget,
                                         lr=architect_lr, device=self.device)
-        self.solver = SolverAgent(grid_rows=R, grid_cols=C, lr=solver_lr, device=self.device)
+        self.solver = SolverAgent(grid_rows=R, grid_cols=C, lr=solver_lr, device=self.device,
+                                  update_precision=update_precision)
         self.reward_calc = RewardCalculator()
         self.metrics = TrainingMetrics()
         self.game_log: List[GameLogEntry] = []

@@ -175,6 +175,8 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   if (const char* u = getenv("HEIST_RAY_CHUNK")) p.ray_chunk = atoi(u);
   if (const char* o = getenv("HEIST_STEP_OCC")) p.step_occ = atoi(o);
   if (const char* w = getenv("HEIST_STEP_WAVES")) p.step_waves = atoi(w);
+  p.probe_mode = 0;
+  if (const char* m = getenv("HEIST_PROBE_MODE")) p.probe_mode = atoi(m);
   p.vis_gap = heist::vis_gap_for(R, C, p.ray_chunk == 2 ? 2 : 4);
   if (!heist::env_variant_exists(p.step_waves, p.ray_chunk, p.step_occ, p.vis_gap)) {
     p.step_waves = 4;

@@ -77,6 +77,9 @@ struct EnvParams {
   int step_occ;               // min waves per SIMD the step kernel is compiled for (1, 8)
   int vis_gap;                // LDS distance stop map -> vis plane (1024 or 5376), see heist_env.hip
   unsigned long long* sample_counter;  // optional [n_envs]: ray samples evaluated per env, else null
+  int probe_mode;             // profiling only (HEIST_PROBE_MODE): 0 normal, 1 no rays, 2 angles+sin/cos only,
+                              // 3 marches with a fixed direction (no sin/cos), 4 no observation write,
+                              // 5 neither rays nor observation; results are wrong for 1-5
 };
 
 // security.py:67 max(int(fov * 2), 30); capped at 32000 rays (fov 16000 deg) so the

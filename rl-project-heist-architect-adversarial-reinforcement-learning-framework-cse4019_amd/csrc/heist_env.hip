@@ -175,7 +175,7 @@ __device__ __forceinline__ int march(unsigned char* smem, int PC, int own, doubl
 // counter (optional): samples evaluated are summed in LDS meta[2] (the ALU work figure of
 // SURVEY 8(d)); raycast_pass adds the env's total to its slot.
 template <int NT, int U, int D>
-__device__ void cast_rays(unsigned char* smem, const EnvLds& L, const unsigned long long* counter) {
+__device__ void cast_rays(unsigned char* smem, const EnvLds& L, const unsigned long long* counter, int probe = 0) {
   static_assert(U == 2 || U == 4, "ring offset assumes an even chunk");
   const int n_em = L.meta[0];
   const int total = L.meta[1];
@@ -189,7 +189,16 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, const unsigned l
     const double angle = E.hmh + (E.fov * (double)i) / (double)E.num_rays;  // security.py:70
     const double rad = angle * kDegToRad;                                   // math.radians
     double sn, cs;
-    heist_trig::sincos(rad, L.tab, &sn, &cs);
+    if (probe == 3) {  // profiling: fixed direction, no sin/cos
+      sn = 0.3 + 1e-3 * (double)i;
+      cs = 0.7;
+    } else {
+      heist_trig::sincos(rad, L.tab, &sn, &cs);
+    }
+    if (probe == 2) {  // profiling: angles and sin/cos only
+      if (sn == 12345.0 && cs == 0.0) L.meta[3] = 1;  // keeps the sin/cos live
+      continue;
+    }
     // dist = stride * s with stride a power of two, so dx * dist == (dx * stride) * s
     // bit for bit; dy = -sin (security.py:72-75).
     const double col = (double)E.col, row = (double)E.row;
@@ -258,7 +267,7 @@ __device__ __forceinline__ void raycast_pass(const EnvParams& p, unsigned char* 
     const Emit E = L.em[t];
     L.vis[L.at(E.row, E.col)] = 1;
   }
-  cast_rays<NT, U, D>(smem, L, p.sample_counter);
+  if (p.probe_mode != 1 && p.probe_mode != 5) cast_rays<NT, U, D>(smem, L, p.sample_counter, p.probe_mode);
   __syncthreads();
   if (p.sample_counter && t == 0) p.sample_counter[blockIdx.x] += (unsigned int)L.meta[2];
 }
@@ -539,7 +548,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     clear_vis<NT, U>(p, L);
     raycast_pass<NT, U, D>(p, smem, L, n_em, n_cams);
   }
-  write_obs<NT, U>(p, e, s, L, obs);
+  if (p.probe_mode < 4) write_obs<NT, U>(p, e, s, L, obs);
   if (t == 0) {
     rew[e] = (float)reward;
     if (rew64) rew64[e] = reward;

@@ -35,6 +35,9 @@ for s in ${STEPS:-pytest smoke bench prof}; do
     pprobe) step probe_policy 600 python tools/probe_policy.py ;;
     tprobe) step probe_train 600 python tools/probe_train.py ;;
     uprobe) step probe_update 600 python tools/probe_update.py ;;
+    mprobe) step probe_modes 600 python tools/probe_step_modes.py ;;
+    vprobe) step probe_variants 600 python tools/probe_step_variants.py ;;
+    envtest) step pytest_env 900 python -m pytest tests/test_gpu_env.py -x -q ;;
     ppmc) for grp in "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS" \
                      "SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_MFMA_MOPS_BF16"; do
             i=$((i+1)); PROBE_N=4096 step pmc_policy$i 600 rocprofv3 --pmc $grp --kernel-include-regex solver_conv -d "$OUT/pp$i" -o pol --output-format csv -- python3 tools/probe_policy.py

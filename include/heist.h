@@ -181,6 +181,12 @@ int heist_solver_features(const float* obs, int n, int rows, int cols, const voi
  * (zero state); seed / counter select the sample (counter-based hash, one uniform per env);
  * outputs logits [n][A] (may be NULL), value [n], action [n] int64, logp [n],
  * h_out / c_out [n][128] (must not alias h_in / c_in). */
+/* Instrumentation, no reference counterpart: with buf a device array of
+ * n_workgroups * 4 * 10 uint64, later heist_solver_features launches record s_memtime at
+ * 10 phase points of each wave for its workgroup's second env (tools/probe_policy.py);
+ * NULL switches it off (default). */
+int heist_solver_stamps(uint64_t* buf);
+
 int heist_solver_head_packed_bytes(void);
 int heist_solver_head_pack(const float* fc_w, const float* fc_b, const float* w_ih, const float* w_hh,
                            const float* b_ih, const float* b_hh, const float* p1_w, const float* p1_b,

@@ -41,6 +41,7 @@ hipError_t launch_solver_pack(const float* w1, const float* b1, const float* w2,
 hipError_t launch_solver_conv(const float* obs, int n, int R, int C, const void* packed, float* feat, int n_cu,
                               hipStream_t st);
 int solver_head_packed_bytes();
+void set_solver_stamps(unsigned long long* p);
 hipError_t launch_solver_head_pack(const float* const* w, int A, void* packed, hipStream_t st);
 hipError_t launch_solver_head(const float* feat, const float* h_in, const float* c_in, int n, const void* packed,
                               int A, uint64_t seed, uint64_t counter, float* logits_out, float* value_out,
@@ -431,4 +432,9 @@ int heist_solver_head(const float* feat, const float* h_in, const float* c_in, i
   return check_hip(heist::launch_solver_head(feat, h_in, c_in, n, packed, num_actions, seed, counter, logits_out,
                                              value_out, action_out, logp_out, h_out, c_out, (hipStream_t)stream),
                    "heist_solver_head");
+}
+
+int heist_solver_stamps(uint64_t* buf) {
+  heist::set_solver_stamps(reinterpret_cast<unsigned long long*>(buf));
+  return 0;
 }

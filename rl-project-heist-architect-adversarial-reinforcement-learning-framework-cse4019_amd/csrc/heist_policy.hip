@@ -14,8 +14,9 @@
 //     position tiles), so the loop touches HBM only for the observation (4.8 KB/env) and
 //     the pooled features (4 KB/env);
 //   * one env at a time sits in LDS as zero-padded NHWC bf16 planes: input [P][4],
-//     act1 [P][32+8], act2 [P][64+8] (P = (R+2)(C+2); the +8 channel pad makes the
-//     16-byte fragment reads of 16 consecutive positions bank-conflict free);
+//     act1 [P][32+8], act2 [P][64+8] (P = (R+2)(C+2)); the +8 channel pad and a row pitch
+//     chosen modulo the 256-byte bank width (ConvGeom::PB1/PB2) make the 16-byte fragment
+//     reads of any 16 consecutive output positions bank-conflict free;
 //   * each conv is an implicit GEMM on v_mfma_f32_32x32x16_bf16 (fp32 accumulate) whose
 //     A/B fragments are single 16-byte LDS reads at compile-time tap offsets;
 //     conv1/conv2 compute D[channel][position] so the epilogue writes 4 channels of a
@@ -27,6 +28,8 @@
 // channels by nh (32 each) and position tiles by mh.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <utility>
 
 namespace heist {
 
@@ -49,18 +52,26 @@ template <int R, int C>
 struct ConvGeom {
   static constexpr int PC = C + 2, PR = R + 2, NP = PR * PC, RC = R * C, MT = (RC + 31) / 32;
   static constexpr int S0 = 8, S1 = 80, S2 = 144;  // bytes per padded position
+  // Row pitch of act1 / act2 in bytes: PB = C*S + 256 j (the smallest such >= PC*S), so
+  // stepping from the last position of a row to the first of the next moves the LDS bank
+  // group exactly as a step within a row does; 16 consecutive output positions then hit
+  // 16 distinct 16-byte bank groups in every ds_read_b128, row breaks included.
+  static constexpr int PB1 = C * S1 + 256 * ((2 * S1 + 255) / 256);
+  static constexpr int PB2 = C * S2 + 256 * ((2 * S2 + 255) / 256);
   static constexpr int IN = 0;
   static constexpr int A1 = align16c(IN + NP * S0);
-  static constexpr int A2 = align16c(A1 + NP * S1);
-  static constexpr int ZERO_END = align16c(A2 + NP * S2);  // zeroed once (padding borders)
+  static constexpr int A2 = align16c(A1 + PR * PB1);
+  static constexpr int ZERO_END = align16c(A2 + PR * PB2);  // zeroed once (padding borders)
   static constexpr int POOL = ZERO_END;                    // [64][16] f32
   static constexpr int BIAS = POOL + 64 * 16 * 4;          // b1[32] b2[64] b3[64]
   static constexpr int INVA = BIAS + 160 * 4;              // [16] f32 1/area
   static constexpr int PM = INVA + 16 * 4;                 // [2*NT2][2][64] pool-membership bytes
   static constexpr int NT2 = (MT + 1) / 2;                 // position tiles per wave (conv2/conv3)
   static constexpr int W2 = align16c(PM + 2 * NT2 * 128);  // conv2 fragments [2][18][64] x 16 B
-  static constexpr int LDS = W2 + 2 * 18 * 64 * 16;
+  static constexpr int SINK = W2 + 2 * 18 * 64 * 16;       // [64] x 8 B: stores of positions >= RC
+  static constexpr int LDS = SINK + 64 * 8;
   static constexpr int QI = (RC + 255) / 256;              // obs cells per thread
+  static_assert(LDS <= 160 * 1024, "one env's planes + conv2 fragments must fit the CU's 160 KiB LDS");
 };
 
 // torch adaptive_avg_pool2d window of output index i over n inputs into 4.
@@ -69,12 +80,102 @@ __host__ __device__ constexpr int pool_hi(int i, int n) { return ((i + 1) * n + 
 
 __device__ __forceinline__ float relu(float x) { return x > 0.f ? x : 0.f; }
 
+// Pin a weight fragment in the accumulator register file: MFMA reads A/B operands from
+// AGPRs as well (gfx90a+), and with the 144 conv3 + 12 conv1 weight VGPRs moved there the
+// VGPR file keeps room for deep LDS read rings.  The empty asm emits nothing; "+a" makes
+// the allocator keep the value in an AGPR at every use.
+__device__ __forceinline__ bf16x8 in_agpr(bf16x8& w) {
+  asm("" : "+a"(w));
+  return w;
+}
+
+// Byte offset of output position m's padded cell (row pitch PB, S bytes per position).
+template <int R, int C, int S, int PB>
+__device__ __forceinline__ int pos_off(int m) {
+  using G = ConvGeom<R, C>;
+  const int mc = m < G::RC ? m : G::RC - 1;
+  const int oy = mc / C;
+  return (oy + 1) * PB + (mc - oy * C + 1) * S;
+}
+
 template <int R, int C>
 __device__ __forceinline__ int padded_pos(int m) {  // output position m -> padded index
   using G = ConvGeom<R, C>;
   const int mc = m < G::RC ? m : G::RC - 1;
   const int oy = mc / C;
   return (oy + 1) * G::PC + (mc - oy * C) + 1;
+}
+
+// Scheduling pipelines: one MFMA then DS_READS LDS reads, NQ times, after an initial group
+// of PRE reads -- keeps the read rings PRE deep (the scheduler otherwise folds them to one
+// or two reads in flight).  W = 1 adds the next weight fragment's read at the last tile of
+// every k-step (conv2's k-outer stream over NT tiles).
+template <int NT, int W, int... Qs>
+__device__ __forceinline__ void sched_ring(std::integer_sequence<int, Qs...>) {
+  ((__builtin_amdgcn_sched_group_barrier(0x008, 1, 0),
+    __builtin_amdgcn_sched_group_barrier(0x100, (W && Qs % NT == NT - 1) ? 2 : 1, 0)),
+   ...);
+}
+
+// One k-outer pass of conv2 over the wave's position tiles [T0, T1) (tile i = position
+// tile mh + 2 i): one LDS weight fragment per k-step feeds every tile of the pass, the
+// (k-step, tile) act1 reads run through a ring of kPre2 reads in flight, and the epilogue
+// of the previous pass's tiles [P0, P1) (bias, ReLU, bf16, 8-byte stores into act2) is
+// spread over this pass's MFMA gaps.  Tiles past MT compute on clamped addresses and store
+// to the sink.
+template <int R, int C, int T0, int T1, int P0, int P1, int NA, int NP>
+__device__ __forceinline__ void conv2_pass(unsigned char* smem, const bf16x8* wl, const float4 (&b2v)[4], int mh,
+                                           int nh, int lr, int h, int l, f32x16 (&cur)[NA],
+                                           const f32x16 (&prv)[NP]) {
+  using G = ConvGeom<R, C>;
+  constexpr int NTP = T1 - T0, NQ = kW2Steps * NTP, kPre2 = 6;
+  constexpr int NPIECE = (P1 - P0) * 16;
+  constexpr int PER_Q = NQ > 0 ? (NPIECE + NQ - 1) / (NQ > 0 ? NQ : 1) : NPIECE;
+  bf16x4 o;
+  auto piece = [&](int k) {  // value k of the previous pass's epilogue
+    const int ti = k >> 4, kk = k & 15, g = kk >> 2, jj = kk & 3;
+    const float bv = jj == 0 ? b2v[g].x : (jj == 1 ? b2v[g].y : (jj == 2 ? b2v[g].z : b2v[g].w));
+    o[jj] = (__bf16)relu(prv[ti][kk] + bv);
+    if (jj == 3) {
+      const int m = 32 * (mh + 2 * (P0 + ti)) + lr;
+      const int off = m < G::RC ? G::A2 + pos_off<R, C, G::S2, G::PB2>(m) + (32 * nh + 8 * g + 4 * h) * 2
+                                : G::SINK + 8 * l;
+      *reinterpret_cast<bf16x4*>(smem + off) = o;
+    }
+  };
+  if constexpr (NQ > 0) {
+    const unsigned char* base[NTP];
+#pragma unroll
+    for (int i = 0; i < NTP; ++i) {
+      base[i] = smem + G::A1 + pos_off<R, C, G::S1, G::PB1>(32 * (mh + 2 * (T0 + i)) + lr) - G::PB1 - G::S1 + 16 * h;
+      cur[i] = f32x16{};
+    }
+    auto rd = [&](int q) {
+      const int s = q / NTP, tap = s >> 1;
+      return *reinterpret_cast<const bf16x8*>(base[q % NTP] + (tap / 3) * G::PB1 + (tap % 3) * G::S1 + (s & 1) * 32);
+    };
+    bf16x8 ring[kPre2];
+#pragma unroll
+    for (int q = 0; q < kPre2; ++q) ring[q] = rd(q < NQ ? q : NQ - 1);
+    bf16x8 wcur = wl[0], wnext = wcur;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int s = q / NTP, i = q % NTP;
+      if (i == 0 && s + 1 < kW2Steps) wnext = wl[(s + 1) * 64];
+      const bf16x8 f = ring[q % kPre2];
+      if (q + kPre2 < NQ) ring[q % kPre2] = rd(q + kPre2);
+      cur[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wcur, f, cur[i], 0, 0, 0);
+      if (i == NTP - 1) wcur = wnext;
+#pragma unroll
+      for (int r = 0; r < PER_Q; ++r)
+        if (q * PER_Q + r < NPIECE) piece(q * PER_Q + r);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, kPre2 + 1, 0);
+    sched_ring<NTP, 1>(std::make_integer_sequence<int, NQ>{});
+  } else {
+#pragma unroll
+    for (int k = 0; k < NPIECE; ++k) piece(k);
+  }
 }
 
 template <int R, int C>
@@ -113,12 +214,12 @@ __device__ __forceinline__ void stage_obs(unsigned char* smem, const float (&v)[
 
 // Epilogue of a D[channel][position] tile: lane holds position m = 32t + (l & 31) and, in
 // register 4g + i, channel n0 + i with n0 = 8g + 4h; relu(acc + bias) -> 4 bf16 -> 8 bytes.
-template <int R, int C, int S>
+template <int R, int C, int S, int PB>
 __device__ __forceinline__ void store_chan_major(unsigned char* dst, const float* bias, int nbase, const f32x16& acc,
                                                  int m, int h) {
   using G = ConvGeom<R, C>;
   if (m >= G::RC) return;
-  const int p = padded_pos<R, C>(m);
+  const int po = pos_off<R, C, S, PB>(m);
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int n0 = nbase + 8 * g + 4 * h;
@@ -128,14 +229,24 @@ __device__ __forceinline__ void store_chan_major(unsigned char* dst, const float
     o[1] = (__bf16)relu(acc[4 * g + 1] + b.y);
     o[2] = (__bf16)relu(acc[4 * g + 2] + b.z);
     o[3] = (__bf16)relu(acc[4 * g + 3] + b.w);
-    *reinterpret_cast<bf16x4*>(dst + p * S + n0 * 2) = o;
+    *reinterpret_cast<bf16x4*>(dst + po + n0 * 2) = o;
   }
 }
+
+// In-kernel phase stamps (instrumentation, heist_solver_stamps): lane 0 of every wave
+// records s_memtime at kStamps points of its workgroup's second env.
+constexpr int kStamps = 10;
+#define HEIST_STAMP(k)                                                            \
+  do {                                                                            \
+    if (stamps && e == (int)blockIdx.x + (int)gridDim.x && l == 0)                \
+      stamps[((size_t)blockIdx.x * 4 + w) * kStamps + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 
 template <int R, int C>
 __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __restrict__ obs, int n,
                                                              const uint4* __restrict__ packed,
-                                                             float* __restrict__ feat) {
+                                                             float* __restrict__ feat,
+                                                             unsigned long long* __restrict__ stamps) {
   using G = ConvGeom<R, C>;
   constexpr int PC = G::PC;
   extern __shared__ __align__(16) unsigned char smem[];
@@ -148,7 +259,10 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
 #pragma unroll
   for (int s = 0; s < kW1Steps; ++s) w1[s] = __builtin_bit_cast(bf16x8, packed[kOffW1 + s * 64 + l]);
 #pragma unroll
-  for (int s = 0; s < kW3Steps; ++s) w3[s] = __builtin_bit_cast(bf16x8, packed[kOffW3 + (nh * kW3Steps + s) * 64 + l]);
+  for (int s = 0; s < kW3Steps; ++s) {
+    w3[s] = __builtin_bit_cast(bf16x8, packed[kOffW3 + (nh * kW3Steps + s) * 64 + l]);
+    in_agpr(w3[s]);
+  }
   for (int i = tid; i < 2 * kW2Steps * 64; i += 256)  // conv2 fragments: LDS, read once per k-step
     reinterpret_cast<uint4*>(smem + G::W2)[i] = packed[kOffW2 + i];
   const float* gbias = reinterpret_cast<const float*>(packed + kOffBias);
@@ -197,76 +311,66 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
   __builtin_amdgcn_s_waitcnt(0);  // weights landed: no conservative vmcnt waits inside the loop
   __syncthreads();
 
-  for (; e < n; e += gridDim.x) {
+  // conv1: D[32 ch][pos] = W1 . im2col(in); wave w owns position tiles w + 4 i (a wave with
+  // fewer tiles repeats its last one, result not stored).  Inside the loop it runs for the
+  // NEXT env, interleaved with this env's conv3 (see there); the first env's runs here.
+  constexpr int NT1 = (G::MT + 3) / 4;
+  auto conv1_reads = [&](int i, bf16x8 (&f)[kW1Steps]) {
+    const unsigned char* base = smem + G::IN + (padded_pos<R, C>(32 * (w + 4 * i) + lr) - PC - 1) * G::S0;
+#pragma unroll
+    for (int s = 0; s < kW1Steps; ++s) {
+      const uint2 a = *reinterpret_cast<const uint2*>(base + off1a[s]);
+      const uint2 b = *reinterpret_cast<const uint2*>(base + off1b[s]);
+      f[s] = __builtin_bit_cast(bf16x8, make_uint4(a.x, a.y, b.x, b.y));
+    }
+  };
+  if (e < n) {
     stage_obs<R, C>(smem, pre);
-    __syncthreads();  // B1: input plane ready (and last env's pool reads done)
-
-    // ---- conv1: D[32 ch][pos] = W1 . im2col(in), position tiles split 4 ways; every
-    // read of the wave's tiles is issued before the first MFMA (a wave with fewer tiles
-    // repeats its last one, result not stored)
-    {
-      constexpr int NT1 = (G::MT + 3) / 4;
-      bf16x8 f1[NT1][kW1Steps];
+    __syncthreads();
+    bf16x8 f1[NT1][kW1Steps];
 #pragma unroll
-      for (int i = 0; i < NT1; ++i) {
-        const unsigned char* base = smem + G::IN + (padded_pos<R, C>(32 * (w + 4 * i) + lr) - PC - 1) * G::S0;
+    for (int i = 0; i < NT1; ++i) conv1_reads(i, f1[i]);
 #pragma unroll
-        for (int s = 0; s < kW1Steps; ++s) {
-          const uint2 a = *reinterpret_cast<const uint2*>(base + off1a[s]);
-          const uint2 b = *reinterpret_cast<const uint2*>(base + off1b[s]);
-          f1[i][s] = __builtin_bit_cast(bf16x8, make_uint4(a.x, a.y, b.x, b.y));
-        }
-      }
+    for (int i = 0; i < NT1; ++i) {
+      f32x16 acc = {};
 #pragma unroll
-      for (int i = 0; i < NT1; ++i) {
-        f32x16 acc = {};
-#pragma unroll
-        for (int s = 0; s < kW1Steps; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1[s], f1[i][s], acc, 0, 0, 0);
-        store_chan_major<R, C, G::S1>(smem + G::A1, bias, 0, acc, 32 * (w + 4 * i) + lr, h);
-      }
+      for (int s = 0; s < kW1Steps; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1[s], f1[i][s], acc, 0, 0, 0);
+      store_chan_major<R, C, G::S1, G::PB1>(smem + G::A1, bias, 0, acc, 32 * (w + 4 * i) + lr, h);
     }
-    __syncthreads();  // B2: act1 ready
+  }
+  __syncthreads();  // act1 of the first env ready
 
+  for (; e < n; e += gridDim.x) {
+    HEIST_STAMP(0);
     const int en = e + gridDim.x;
-    if (en < n) load_obs<R, C>(obs, en, pre);  // next env's observation in flight during conv2/3
+    const bool has_next = en < n;  // workgroup-uniform
+    if (has_next) load_obs<R, C>(obs, en, pre);  // next env's observation in flight during conv2
+    HEIST_STAMP(1);
+    HEIST_STAMP(2);
+    HEIST_STAMP(3);
 
-    // ---- conv2: D[32 ch of nh][pos] = W2 . im2col(act1), k-outer: one LDS weight
-    // fragment per k-step feeds all of the wave's position tiles (accumulators in AGPRs);
-    // the (k-step, tile) reads run through a ring of kPre2 LDS reads in flight.  A wave with
-    // fewer tiles repeats its last one (clamped address, result not stored) instead of
-    // branching: its partner wave has the extra tile anyway.
+    // ---- conv2: D[32 ch of nh][pos] = W2 . im2col(act1) in three k-outer passes over the
+    // wave's position tiles; each pass hides the previous pass's epilogue under its MFMAs
+    // (conv2_pass), so only the last pass's epilogue is exposed.
     {
-      constexpr int NT2 = G::NT2, NQ = kW2Steps * NT2, kPre2 = 6;
-      const unsigned char* base[NT2];
-      f32x16 acc[NT2];
-#pragma unroll
-      for (int i = 0; i < NT2; ++i) {
-        base[i] = smem + G::A1 + (padded_pos<R, C>(32 * (mh + 2 * i) + lr) - PC - 1) * G::S1 + 16 * h;
-        acc[i] = f32x16{};
-      }
-      auto rd = [&](int q) {
-        const int s = q / NT2, tap = s >> 1;
-        return *reinterpret_cast<const bf16x8*>(base[q % NT2] + ((tap / 3) * PC + (tap % 3)) * G::S1 + (s & 1) * 32);
-      };
+      constexpr int NT2 = G::NT2;
+      constexpr int SA = (NT2 * 3 + 6) / 7, SB = SA + (NT2 - SA + 1) / 2;
+      constexpr int NA = SA, NB = SB - SA > 0 ? SB - SA : 1, NC = NT2 - SB > 0 ? NT2 - SB : 1;
       const bf16x8* wl = reinterpret_cast<const bf16x8*>(smem + G::W2) + nh * kW2Steps * 64 + l;
-      bf16x8 ring[kPre2];
+      float4 b2v[4];
 #pragma unroll
-      for (int q = 0; q < kPre2; ++q) ring[q] = rd(q);
-      bf16x8 wcur = wl[0], wnext = wcur;
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        const int s = q / NT2, i = q % NT2;
-        if (i == 0 && s + 1 < kW2Steps) wnext = wl[(s + 1) * 64];
-        const bf16x8 f = ring[q % kPre2];
-        if (q + kPre2 < NQ) ring[q % kPre2] = rd(q + kPre2);
-        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wcur, f, acc[i], 0, 0, 0);
-        if (i == NT2 - 1) wcur = wnext;
-      }
-#pragma unroll
-      for (int i = 0; i < NT2; ++i)
-        store_chan_major<R, C, G::S2>(smem + G::A2, bias + 32, 32 * nh, acc[i], 32 * (mh + 2 * i) + lr, h);
+      for (int g = 0; g < 4; ++g) b2v[g] = *reinterpret_cast<const float4*>(bias + 32 + 32 * nh + 8 * g + 4 * h);
+      f32x16 accA[NA], accB[NB], accC[NC];
+      conv2_pass<R, C, 0, SA, 0, 0, NA, NA>(smem, wl, b2v, mh, nh, lr, h, l, accA, accA);
+      conv2_pass<R, C, SA, SB, 0, SA, NB, NA>(smem, wl, b2v, mh, nh, lr, h, l, accB, accA);
+      conv2_pass<R, C, SB, NT2, SA, SB, NC, NB>(smem, wl, b2v, mh, nh, lr, h, l, accC, accB);
+      HEIST_STAMP(4);
+      conv2_pass<R, C, NT2, NT2, SB, NT2, NC, NC>(smem, wl, b2v, mh, nh, lr, h, l, accC, accC);  // last epilogue
     }
-    __syncthreads();  // B3: act2 ready
+    HEIST_STAMP(5);
+    if (has_next) stage_obs<R, C>(smem, pre);  // in0 is free: this env's conv1 ran an iteration ago
+    __syncthreads();  // B3: act2 of env e and the input plane of env en ready; act1 reads done
+    HEIST_STAMP(6);
 
     // ---- conv3: D[pos][32 ch of nh] = im2col(act2) . W3, then Y[cell][ch] += P . relu(D).
     // The wave's (tile, k-step) sequence is one unrolled stream: A fragments run through a
@@ -279,15 +383,30 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
       const unsigned char* base[NT2];
 #pragma unroll
       for (int i = 0; i < NT2; ++i)
-        base[i] = smem + G::A2 + (padded_pos<R, C>(32 * (mh + 2 * i) + lr) - PC - 1) * G::S2 + 16 * h;
+        base[i] = smem + G::A2 + pos_off<R, C, G::S2, G::PB2>(32 * (mh + 2 * i) + lr) - G::PB2 - G::S2 + 16 * h;
       auto rd = [&](int q) {
         const int s = q % kW3Steps, tap = s >> 2;
-        return *reinterpret_cast<const bf16x8*>(base[q / kW3Steps] + ((tap / 3) * PC + (tap % 3)) * G::S2 +
+        return *reinterpret_cast<const bf16x8*>(base[q / kW3Steps] + (tap / 3) * G::PB2 + (tap % 3) * G::S2 +
                                                 (s & 3) * 32);
       };
       bf16x8 ring[kPre];
 #pragma unroll
       for (int q = 0; q < kPre; ++q) ring[q] = rd(q);
+      // software pipeline: tile i's pooling epilogue (ReLU + bias, bf16 packing, the two
+      // pooling MFMAs) is spread over the first k-steps of tile i + 1's MFMA chain, one
+      // element per MFMA gap, so it issues under the matrix core instead of stalling it
+      f32x16 prev = {};
+      bf16x8 x[2], pf[2];
+      auto pool_piece = [&](int tp, int s) {  // piece s of tile tp's epilogue (prev holds its sums)
+        if (s < 16) x[s >> 3][s & 7] = (__bf16)relu(prev[s] + b3v);
+        if (s == 0 || s == 1) {
+          const unsigned bits = smem[G::PM + (tp * 2 + s) * 64 + l];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) pf[s][j] = ((bits >> j) & 1u) ? (__bf16)1.0f : (__bf16)0.0f;
+        }
+        if (s == 16) Y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf[0], x[0], Y, 0, 0, 0);
+        if (s == 17) Y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf[1], x[1], Y, 0, 0, 0);
+      };
 #pragma unroll
       for (int i = 0; i < NT2; ++i) {
         f32x16 acc = {};
@@ -296,31 +415,39 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
           const int q = i * kW3Steps + s;
           const bf16x8 f = ring[q % kPre];
           if (q + kPre < NQ) ring[q % kPre] = rd(q + kPre);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, w3[s], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, in_agpr(w3[s]), acc, 0, 0, 0);
+          if (i > 0 && s < 18) pool_piece(mh + 2 * (i - 1), s);
         }
-        {
-          const int t = mh + 2 * i;
+        prev = acc;
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, kPre, 0);
+      sched_ring<kW3Steps, 0>(std::make_integer_sequence<int, NQ>{});
 #pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            bf16x8 x, pf;
-            const unsigned bits = smem[G::PM + (t * 2 + k) * 64 + l];
+      for (int s = 0; s < 18; ++s) pool_piece(mh + 2 * (NT2 - 1), s);  // the last tile's epilogue
+      // conv1 of the next env (its input plane was staged before B3): all reads first,
+      // then tile by tile (also after the last env: harmless)
+      {
+        bf16x8 g1[NT1][kW1Steps];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              x[j] = (__bf16)relu(acc[8 * k + j] + b3v);
-              pf[j] = ((bits >> j) & 1u) ? (__bf16)1.0f : (__bf16)0.0f;
-            }
-            Y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf, x, Y, 0, 0, 0);
-          }
+        for (int j = 0; j < NT1; ++j) conv1_reads(j, g1[j]);
+#pragma unroll
+        for (int j = 0; j < NT1; ++j) {
+          f32x16 a1 = {};
+#pragma unroll
+          for (int k = 0; k < kW1Steps; ++k) a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1[k], g1[j][k], a1, 0, 0, 0);
+          store_chan_major<R, C, G::S1, G::PB1>(smem + G::A1, bias, 0, a1, 32 * (w + 4 * j) + lr, h);
         }
       }
     }
+    HEIST_STAMP(7);
     // Y: lane = channel 32nh + lr, register r < 8 = cell (r & 3) + 8 (r >> 2) + 4h
     float* pool = reinterpret_cast<float*>(smem + G::POOL) + (32 * nh + lr) * 16 + 4 * h;
     if (mh == 1) {
       *reinterpret_cast<float4*>(pool) = make_float4(Y[0], Y[1], Y[2], Y[3]);
       *reinterpret_cast<float4*>(pool + 8) = make_float4(Y[4], Y[5], Y[6], Y[7]);
     }
-    __syncthreads();  // B4: partner half of the pool sums in LDS
+    __syncthreads();  // B4: partner half of the pool sums in LDS; act1 of env en written
+    HEIST_STAMP(8);
     if (mh == 0) {
       const float4 p0 = *reinterpret_cast<const float4*>(pool);
       const float4 p1 = *reinterpret_cast<const float4*>(pool + 8);
@@ -333,6 +460,7 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
       *reinterpret_cast<float4*>(out + 8) =
           make_float4((Y[4] + p1.x) * i1.x, (Y[5] + p1.y) * i1.y, (Y[6] + p1.z) * i1.z, (Y[7] + p1.w) * i1.w);
     }
+    HEIST_STAMP(9);
   }
 }
 
@@ -382,6 +510,9 @@ hipError_t launch_solver_pack(const float* w1, const float* b1, const float* w2,
   return hipGetLastError();
 }
 
+static unsigned long long* g_conv_stamps = nullptr;
+void set_solver_stamps(unsigned long long* p) { g_conv_stamps = p; }
+
 template <int R, int C>
 static hipError_t launch_conv_rc(const float* obs, int n, const void* packed, float* feat, int n_cu, hipStream_t st) {
   using G = ConvGeom<R, C>;
@@ -394,7 +525,7 @@ static hipError_t launch_conv_rc(const float* obs, int n, const void* packed, fl
   }
   const int grid = n < n_cu ? n : n_cu;
   hipLaunchKernelGGL((solver_conv_kernel<R, C>), dim3(grid), dim3(256), G::LDS, st, obs, n,
-                     reinterpret_cast<const uint4*>(packed), feat);
+                     reinterpret_cast<const uint4*>(packed), feat, g_conv_stamps);
   return hipGetLastError();
 }
 

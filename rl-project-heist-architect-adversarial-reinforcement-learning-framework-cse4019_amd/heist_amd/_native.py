@@ -45,6 +45,7 @@ SIGNATURES = {
     "heist_solver_packed_bytes": (_i, []),
     "heist_solver_pack": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "heist_solver_features": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp]),
+    "heist_solver_stamps": (_i, [_vp]),
     "heist_solver_head_packed_bytes": (_i, []),
     "heist_solver_head_pack": (_i, [_vp] * 14 + [_i, _vp, _vp]),
     "heist_solver_head": (_i, [_vp, _vp, _vp, _i, _vp, _i, ctypes.c_uint64, ctypes.c_uint64] + [_vp] * 7),

@@ -50,5 +50,34 @@ def main():
                           "act_fused_ms": round(ms_af, 3), "act_fp32_ms": round(ms_ar, 3)}), flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and not os.environ.get("PROBE_STAMPS"):
     main()
+
+
+def phase_stamps(n=4096):
+    """Median cycles per phase of solver_conv_kernel (s_memtime stamps, second env of
+    every workgroup): 0 start, 1 after B1, 2 conv1 done, 3 after B2, 4 conv2 MFMAs done,
+    5 conv2 epilogue done, 6 after B3, 7 conv3 done, 8 after B4, 9 end."""
+    from heist_amd import _native
+    from heist_amd.networks import SolverNetwork
+    dev = torch.device("cuda:0")
+    net = SolverNetwork().to(dev)
+    obs = torch.rand(n, 3, 20, 20, device=dev)
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    buf = torch.zeros(min(n, ncu) * 4 * 10, dtype=torch.int64, device=dev)
+    net.features_fused(obs)
+    _native.check(_native.lib().heist_solver_stamps(_native.ptr(buf)), "stamps")
+    net.features_fused(obs)
+    torch.cuda.synchronize()
+    _native.check(_native.lib().heist_solver_stamps(None), "stamps")
+    st = buf.reshape(-1, 4, 10).double()
+    d = (st[:, :, 1:] - st[:, :, :-1]).reshape(-1, 9)
+    ok = (st[:, :, 0] > 0).reshape(-1)
+    med = d[ok].median(0).values.tolist()
+    names = ["stage+B1", "conv1", "B2", "conv2_mfma", "conv2_epi", "B3", "conv3", "pool_xchg+B4", "feat_out"]
+    tot = (st[:, :, 9] - st[:, :, 0]).reshape(-1)[ok].median().item()
+    print(json.dumps({"phase_median_cycles": dict(zip(names, [round(x) for x in med])), "env_cycles_median": tot}))
+
+
+if __name__ == "__main__" and os.environ.get("PROBE_STAMPS"):
+    phase_stamps()

@@ -26,6 +26,11 @@ METRIC = "Solver env-steps/sec at 20×20, 4096 envs/GPU, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
+def log(msg):
+    """Progress on stderr (stdout carries only the one JSON result line)."""
+    print("[bench %s] %s" % (time.strftime("%H:%M:%S"), msg), file=sys.stderr, flush=True)
+
+
 def algorithmic_bytes_per_env_step(R, C, ncam, nguard):
     """obs f32 write + grid u8 read + action i64 + reward f32 + done + status
     + read and write of the dynamic per-env state (24 + 8*ncam + 12*nguard bytes)."""
@@ -126,6 +131,7 @@ def measure_train(cfg, dev, n_envs, rollout_len=32, minibatch=16384, update_prec
                             n_envs=n_envs, rollout_len=rollout_len, minibatch=minibatch, device=dev, seed=0,
                             update_precision=update_precision)
     tr._assign_layouts(np.arange(n_envs))
+    log("  warm-up iteration")
     tr.train_iteration()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -202,12 +208,16 @@ def main():
     # ALU work figure: ray samples evaluated per env-step, counted by the
     # kernel on extra steps after the timed region
     cnt = torch.zeros(N, dtype=torch.int64, device=dev)
+    cnt_x = torch.zeros(N, dtype=torch.int64, device=dev)
     env.count_samples(cnt)
+    env.count_exact_rays(cnt_x)
     n_count = 8
     for k in range(n_count):
         env.step(actions[k])
     env.count_samples(None)
+    env.count_exact_rays(None)
     samples_per_step = float(cnt.sum().item()) / (n_count * N)
+    exact_rays_per_step = float(cnt_x.sum().item()) / (n_count * N)
 
     ncam = float(np.mean([len(c) for _, c, _ in layouts]))
     ngu = float(np.mean([len(g) for _, _, g in layouts]))
@@ -235,15 +245,24 @@ def main():
                          "kernel": "heist::step_kernel", "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_env_step": b_step,
                          "ray_samples_per_env_step": samples_per_step,
+                         "exact_path_rays_per_env_step": exact_rays_per_step,
                          "host_issue_us_per_step": issue_s / args.steps * 1e6},
             "cpu_baseline": None,
         }
+        log("env-only: %.1f M env-steps/s, step kernel %.1f us" % (value / 1e6, kern_ms * 1e3))
         if not args.no_secondary:
-            line["secondary"] = {"rollout": measure_rollout(env, dev),
-                                 "policy_inference": measure_policy(dev, N),
-                                 "full_train": measure_train(cfg, dev, N),
-                                 "full_train_bf16_update": measure_train(cfg, dev, N, update_precision="bf16")}
+            sec = {}
+            log("rollout")
+            sec["rollout"] = measure_rollout(env, dev)
+            log("policy inference")
+            sec["policy_inference"] = measure_policy(dev, N)
+            log("full train (fp32 update)")
+            sec["full_train"] = measure_train(cfg, dev, N)
+            log("full train (bf16 update)")
+            sec["full_train_bf16_update"] = measure_train(cfg, dev, N, update_precision="bf16")
+            line["secondary"] = sec
         if not args.no_cpu_baseline:
+            log("cpu baseline")
             line["cpu_baseline"] = cpu_baseline(layouts, cfg, args.budget, target_s=args.cpu_seconds, threads=1)
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -96,6 +96,18 @@ int heist_export(heist_t h, int32_t* scalars, int8_t* grid, double* cam_heading,
  * env e evaluated (the ALU work figure of SURVEY 8(d)); NULL switches counting off (default). */
 int heist_count_samples(heist_t h, uint64_t* counter);
 
+/* Instrumentation, no reference counterpart: like heist_count_samples, counter[e] += the
+ * number of env e's rays whose fp32 fast path met a near .5 tie and were re-cast on the
+ * exact fp64 path. */
+int heist_count_redo(heist_t h, uint64_t* counter);
+
+/* Raycast arithmetic of later heist_step / heist_reset calls on h: 0 (default) = fp32 fast
+ * path with exact fp64 re-cast of every ray that comes within a bounded error of a .5 tie,
+ * 1 = exact fp64 path for every ray.  Both give bit-identical visibility; 1 exists for
+ * parity tests and A/B timing.  The environment variable HEIST_EXACT_RAYS=1 sets 1 at
+ * heist_create. */
+int heist_set_ray_mode(heist_t h, int ray_mode);
+
 /* Replaces bfs_path_exists (utils.py:52-85) on a batch of grids [N][R][C] int32. */
 int heist_bfs_valid(const int32_t* grid, int n, int rows, int cols, int start_r, int start_c, int goal_r,
                     int goal_c, uint8_t* valid_out, heist_stream_t stream);
@@ -106,6 +118,16 @@ int heist_bfs_valid(const int32_t* grid, int n, int rows, int cols, int start_r,
  *   params [n][2] f64 = fov_angle, heading;  tiles_out [n][R][C] uint8 (1 = visible). */
 int heist_cones(int n, int rows, int cols, const uint8_t* walls, const int32_t* meta, const double* params,
                 uint8_t* tiles_out, heist_stream_t stream);
+
+/* heist_cones with an explicit ray_mode (0 fast + exact re-cast, 1 exact only; see
+ * heist_set_ray_mode).  heist_cones is ray_mode 0. */
+int heist_cones_mode(int n, int rows, int cols, const uint8_t* walls, const int32_t* meta, const double* params,
+                     int ray_mode, uint8_t* tiles_out, heist_stream_t stream);
+
+/* The fast path's fp32 ray direction for angles in degrees (parity tooling: its error
+ * against the exact glibc direction bounds the near-tie tolerance).  [n] f64 in,
+ * cos_out, sin_out [n] f32. */
+int heist_fast_dir(const double* angle_deg, int64_t n, float* cos_out, float* sin_out, heist_stream_t stream);
 
 /* Replaces the decode half of ArchitectNetwork.generate_layout (networks.py:283-335) and
  * the curriculum filter of training.py:464-467 for n sampled layouts:

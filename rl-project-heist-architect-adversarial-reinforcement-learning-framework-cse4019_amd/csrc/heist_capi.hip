@@ -27,7 +27,8 @@ hipError_t launch_bfs(const int32_t* grid, int n, int R, int C, int sr, int sc, 
 int vis_gap_for(int R, int C, int U);
 bool env_variant_exists(int W, int U, int O, int D);
 hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
-                        uint8_t* out, hipStream_t st);
+                        uint8_t* out, int ray_mode, hipStream_t st);
+hipError_t launch_fast_dir(const double* deg, int64_t n, float* co, float* so, hipStream_t st);
 hipError_t launch_arch_decode(const int64_t* amap, int n, int R, int C, const float* cam, int cam_stride,
                               const int32_t* budget, int allow_cams, int allow_guards, int max_walls, int max_cams,
                               int max_guards, int max_path, int32_t* wall_rc, int32_t* n_walls, double* cam_out,
@@ -178,6 +179,10 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   if (const char* w = getenv("HEIST_STEP_WAVES")) p.step_waves = atoi(w);
   p.probe_mode = 0;
   if (const char* m = getenv("HEIST_PROBE_MODE")) p.probe_mode = atoi(m);
+  p.ray_mode = 0;
+  if (const char* m = getenv("HEIST_EXACT_RAYS")) p.ray_mode = atoi(m) ? 1 : 0;
+  p.sample_counter = nullptr;
+  p.redo_counter = nullptr;
   p.vis_gap = heist::vis_gap_for(R, C, p.ray_chunk == 2 ? 2 : 4);
   if (!heist::env_variant_exists(p.step_waves, p.ray_chunk, p.step_occ, p.vis_gap)) {
     p.step_waves = 4;
@@ -282,6 +287,19 @@ int heist_count_samples(heist_t h, uint64_t* counter) {
   return 0;
 }
 
+int heist_count_redo(heist_t h, uint64_t* counter) {
+  if (int rc = check_handle(h)) return rc;
+  h->p.redo_counter = reinterpret_cast<unsigned long long*>(counter);
+  return 0;
+}
+
+int heist_set_ray_mode(heist_t h, int ray_mode) {
+  if (int rc = check_handle(h)) return rc;
+  HEIST_REQUIRE(ray_mode == 0 || ray_mode == 1, "heist_set_ray_mode: ray_mode must be 0 or 1");
+  h->p.ray_mode = ray_mode;
+  return 0;
+}
+
 int heist_bfs_valid(const int32_t* grid, int n, int rows, int cols, int sr, int sc, int gr, int gc, uint8_t* valid_out,
                     heist_stream_t stream) {
   HEIST_REQUIRE(grid && valid_out, "heist_bfs_valid: null pointer");
@@ -300,8 +318,25 @@ int heist_cones(int n, int rows, int cols, const uint8_t* walls, const int32_t* 
   HEIST_REQUIRE(rows >= 1 && cols >= 1 && rows <= heist::kMaxDim && cols <= heist::kMaxDim,
                 "heist_cones: need 1 <= rows, cols <= 64");
   if (n <= 0) return 0;
-  return check_hip(heist::launch_cones(n, rows, cols, walls, meta, params, tiles_out, (hipStream_t)stream),
+  return check_hip(heist::launch_cones(n, rows, cols, walls, meta, params, tiles_out, 0, (hipStream_t)stream),
                    "heist_cones");
+}
+
+int heist_cones_mode(int n, int rows, int cols, const uint8_t* walls, const int32_t* meta, const double* params,
+                     int ray_mode, uint8_t* tiles_out, heist_stream_t stream) {
+  HEIST_REQUIRE(walls && meta && params && tiles_out, "heist_cones_mode: null pointer");
+  HEIST_REQUIRE(rows >= 1 && cols >= 1 && rows <= heist::kMaxDim && cols <= heist::kMaxDim,
+                "heist_cones_mode: need 1 <= rows, cols <= 64");
+  HEIST_REQUIRE(ray_mode == 0 || ray_mode == 1, "heist_cones_mode: ray_mode must be 0 or 1");
+  if (n <= 0) return 0;
+  return check_hip(heist::launch_cones(n, rows, cols, walls, meta, params, tiles_out, ray_mode, (hipStream_t)stream),
+                   "heist_cones_mode");
+}
+
+int heist_fast_dir(const double* angle_deg, int64_t n, float* cos_out, float* sin_out, heist_stream_t stream) {
+  HEIST_REQUIRE(angle_deg && cos_out && sin_out, "heist_fast_dir: null pointer");
+  if (n <= 0) return 0;
+  return check_hip(heist::launch_fast_dir(angle_deg, n, cos_out, sin_out, (hipStream_t)stream), "heist_fast_dir");
 }
 
 int heist_architect_decode(const int64_t* asset_map, int n, int rows, int cols, const float* cam_params,

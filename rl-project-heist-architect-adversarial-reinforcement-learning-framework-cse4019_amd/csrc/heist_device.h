@@ -51,10 +51,12 @@ __host__ __device__ inline int pack_rc(int r, int c) { return r | (c << 8); }
 struct Emit {
   double hmh;     // heading - fov / 2.0  (security.py:64, :70)
   double fov;
+  double step;    // fov / num_rays: the fast path's ray spacing (approximate angle)
   int32_t row, col, range, num_rays;
   int32_t first;  // index of this emitter's ray 0 in the env's flattened ray list
   int32_t kind;   // 0 camera (half-tile sub-steps), 1 guard (whole-tile steps)
 };
+static_assert(sizeof(Emit) == 48, "Emit layout");
 
 struct EnvParams {
   int R, C, RC, max_steps;
@@ -77,6 +79,8 @@ struct EnvParams {
   int step_occ;               // min waves per SIMD the step kernel is compiled for (1, 8)
   int vis_gap;                // LDS distance stop map -> vis plane (1024 or 5376), see heist_env.hip
   unsigned long long* sample_counter;  // optional [n_envs]: ray samples evaluated per env, else null
+  unsigned long long* redo_counter;    // optional [n_envs]: rays re-cast on the exact fp64 path, else null
+  int ray_mode;               // 0: fp32 fast path with exact fp64 re-cast of near-tie rays; 1: exact fp64 only
   int probe_mode;             // profiling only (HEIST_PROBE_MODE): 0 normal, 1 no rays, 2 angles+sin/cos only,
                               // 3 marches with a fixed direction (no sin/cos), 4 no observation write,
                               // 5 neither rays nor observation; results are wrong for 1-5

@@ -1,7 +1,7 @@
 // heist_env.hip -- CDNA4 kernels for the batched Heist environment.
 //
 // step/reset: one workgroup of W wavefronts (W = 1, 2, 4) owns one environment.
-//   * Prefetch first: the env's tile grid, guard paths and the glibc sin/cos table
+//   * Prefetch first: the env's tile grid and guard paths
 //     go to LDS, cameras/guards and the observation's static position plane to
 //     registers -- all issued together, so the env costs one HBM round trip.
 //   * Cameras and guards are updated in registers (no store -> reload) and flattened
@@ -46,7 +46,6 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(
 struct EnvLds {
   uint8_t* wall;   // LDS offset 0: [(R+2U)(C+2U)] ray stop map, 1 = wall or outside the grid
   uint8_t* vis;    // LDS offset D: visibility with the same padded geometry (ring bytes unused)
-  double* tab;     // [440] glibc sin/cos table
   uint8_t* grid;   // [RC]
   Emit* em;        // [n_emit]
   uint16_t* path;  // [max_guards][max_path]
@@ -64,9 +63,8 @@ __host__ __device__ inline int padded_bytes(int R, int C, int U) { return (R + 2
 
 __host__ __device__ inline size_t env_lds_bytes(int R, int C, int n_emit, int path_words, int D) {
   const int RC = R * C;
-  return 2 * (size_t)D + align16(sizeof(double) * kTabDoubles) + align16(RC) +
-         align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) +
-         align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1)) + align16(sizeof(float) * RC) + 16;
+  return 2 * (size_t)D + align16(RC) + align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) +
+         align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1)) + align16(sizeof(float) * RC) + 32;
 }
 
 template <int U, int D>
@@ -76,7 +74,6 @@ __device__ __forceinline__ EnvLds carve(unsigned char* smem, int R, int C, int n
   L.wall = smem;
   L.vis = smem + D;
   size_t o = 2 * (size_t)D;
-  L.tab = reinterpret_cast<double*>(smem + o); o += align16(sizeof(double) * kTabDoubles);
   L.grid = smem + o; o += align16(RC);
   L.em = reinterpret_cast<Emit*>(smem + o); o += align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1));
   L.path = reinterpret_cast<uint16_t*>(smem + o); o += align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1));
@@ -158,6 +155,137 @@ __device__ __forceinline__ int march(unsigned char* smem, int PC, int own, doubl
   return s0 + U - 1;
 }
 
+// ---- fp32 fast path -------------------------------------------------------------------
+//
+// A sample's tile is rint(col + dx*dist) (fp64, glibc dx).  Camera samples are
+// dist = k/2 (k = 1 .. 2*range) and guard samples dist = k = (2k)/2 (k = 1 .. range), so
+// with K = 2*range every sample is x = (dx/2) * k' for some k' <= K.  x_k sits on a .5 tie iff dx = j/k' with j odd: the
+// TIE POINTS of the ray are the fractions j/k', j odd, k' <= K.  Between two tie points
+// every rint(x_k) is constant, so for any approximation d of dx with |d - dx| <= E,
+// rint(col + k*d/2) equals the exact fp64 result whenever no tie point lies within E of
+// d (and the fp64 path itself cannot round differently: that needs dx within ~1e-14 of a
+// tie point).  The same holds for dy.
+//
+// The fast path therefore computes the direction in fp32 (angle reduced to an octant in
+// fp64, then the Cephes sinf/cosf polynomials; within ~2e-7 of the true direction, E =
+// kDirErr = 1e-6 bounds it with margin, tests/test_gpu_env.py::test_fast_direction_error),
+// screens |dx| and |dy| against the tie points once per ray, and marches with one fp32
+// fma per sample (magic-constant rounding, exact product, single rounding).  With
+// L = lcm(1..12) = 27720 the tie points for K <= 12 are integers of t = |d|*L, flagged in
+// a 27721-bit table; a ray is re-cast on the exact path (glibc sin/cos restatement + fp64
+// march) when |t - rint(t)| < kTieRad = E*L + (fp32 error of t) and rint(t) is a tie
+// point.  Emitters with range > 6 (K > 12) always take the exact path.
+constexpr float kDirErr = 1e-6f;
+constexpr int kTieMaxRange = 6;
+constexpr int kTieL = 27720;                                  // lcm(1, ..., 12)
+constexpr float kTieRad = kDirErr * (float)kTieL + 4e-3f;     // 0.0317 in units of t
+
+struct TieBits {
+  uint32_t w[kTieL / 32 + 1];
+};
+constexpr TieBits make_tie_bits() {
+  TieBits t{};
+  for (int k = 1; k <= 2 * kTieMaxRange; ++k)
+    for (int j = 1; j <= k; j += 2) {
+      const int n = j * (kTieL / k);
+      t.w[n >> 5] |= 1u << (n & 31);
+    }
+  return t;
+}
+__constant__ TieBits kTieBits = make_tie_bits();
+
+// 1.5 * 2^23: for |v| < 2^22, fl32(v + kMagic32) = kMagic32 + rint(v), and the low 22 bits
+// of its bit pattern hold the integer (plus any offset folded into the constant).
+constexpr float kMagic32 = 12582912.0f;
+
+// cos and sin of a (degrees) in fp32: q = rint(a / 90) in fp64, the octant remainder
+// (|r| <= 45 deg) to fp32 radians, Cephes sinf/cosf minimax polynomials on [-pi/4, pi/4],
+// then the quadrant rotation.
+__device__ __forceinline__ void fast_dir(double a, float* cs, float* sn) {
+  const double q = __builtin_rint(a * (1.0 / 90.0));
+  const float x = (float)(__builtin_fma(-90.0, q, a) * kDegToRad);
+  const float z = x * x;
+  const float ps = __builtin_fmaf(__builtin_fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
+  const float pc = __builtin_fmaf(__builtin_fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z,
+                                  4.166664568298827e-2f);
+  const float s = __builtin_fmaf(ps * z, x, x);
+  const float c = __builtin_fmaf(pc * z, z, __builtin_fmaf(-0.5f, z, 1.0f));
+  const int n = (int)q;
+  const float s0 = (n & 1) ? c : s;  // sin(a) up to sign
+  const float c0 = (n & 1) ? s : c;  // cos(a) up to sign
+  *sn = (n & 2) ? -s0 : s0;
+  *cs = ((n + 1) & 2) ? -c0 : c0;
+}
+
+// true if |c| or |s| lies within kTieRad / L of a tie point (the ray needs the exact path).
+// Scalar code on purpose: the float2 form of this function is miscompiled by the ROCm 7.2
+// clang (the two table lookups are merged into one).
+__device__ __forceinline__ bool near_tie(float c, float s) {
+  const float tx = __builtin_fabsf(c) * (float)kTieL, ty = __builtin_fabsf(s) * (float)kTieL;
+  const float mx = tx + kMagic32, my = ty + kMagic32;
+  const uint32_t nx = __builtin_bit_cast(uint32_t, mx) - 0x4B400000u;
+  const uint32_t ny = __builtin_bit_cast(uint32_t, my) - 0x4B400000u;
+  const uint32_t wx = kTieBits.w[nx >> 5], wy = kTieBits.w[ny >> 5];
+  const bool cx = __builtin_fabsf(tx - (mx - kMagic32)) < kTieRad;
+  const bool cy = __builtin_fabsf(ty - (my - kMagic32)) < kTieRad;
+  return (((wx >> (nx & 31)) & (uint32_t)cx) | ((wy >> (ny & 31)) & (uint32_t)cy)) & 1u;
+}
+
+// LDS byte at an absolute LDS address (the dynamic LDS base is folded into the address
+// once per ray instead of once per access).
+__device__ __forceinline__ uint8_t lds_ld(uint32_t a) {
+  return *reinterpret_cast<__attribute__((address_space(3))) uint8_t*>(a);
+}
+__device__ __forceinline__ void lds_st(uint32_t a, uint8_t v) {
+  *reinterpret_cast<__attribute__((address_space(3))) uint8_t*>(a) = v;
+}
+
+// U samples k0 .. k0+U-1 of a fast ray.  (dxs, dys) = (dx, dy) * stride, (mx, my) =
+// kMagic32 + the padded (col, row) of the emitter; kofs turns the two rounded bit patterns
+// into the absolute LDS address of the stop byte.  Returns true if the ray stopped.
+// Scalar fp32 on purpose (and this file builds with -fno-slp-vectorize): ROCm 7.2 clang
+// miscompiles the float2 / v_pk_fma_f32 form of this loop (a lane's negation is lost).
+template <int U, int D, bool TAIL, int OWN>
+__device__ __forceinline__ bool fast_chunk(uint32_t PC, uint32_t own, uint32_t dummy, float dxs, float dys, float mx,
+                                           float my, uint32_t kofs, float k0, int left) {
+  uint32_t a[U];
+  int w[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const float k = k0 + (float)u;  // exact small integer
+    const float yx = __builtin_fmaf(k, dxs, mx), yy = __builtin_fmaf(k, dys, my);  // rint(k*d) + magic + origin
+    a[u] = __umul24(__builtin_bit_cast(uint32_t, yy), PC) + __builtin_bit_cast(uint32_t, yx) - kofs;
+    w[u] = lds_ld(a[u]);
+  }
+  bool stop = false;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    stop |= w[u] != 0 || (TAIL && u >= left);
+    const bool skip = stop || (u < OWN && a[u] == own);
+    lds_st((skip ? dummy : a[u]) + D, 1);
+  }
+  return stop;
+}
+
+// All samples k = 1 .. n_samp of a fast ray (chunk structure of march() below).  Returns
+// the samples evaluated.
+template <int U, int D, int OWN>
+__device__ __forceinline__ int march_fast(uint32_t PC, uint32_t own, uint32_t dummy, float dxs, float dys, float mx,
+                                          float my, uint32_t kofs, int n_samp) {
+  float kf = 1.0f;
+  int s0 = 1;
+  if (n_samp < U) {
+    fast_chunk<U, D, true, OWN>(PC, own, dummy, dxs, dys, mx, my, kofs, kf, n_samp);
+    return U;
+  }
+  if (fast_chunk<U, D, false, OWN>(PC, own, dummy, dxs, dys, mx, my, kofs, kf, U)) return U;
+  for (s0 += U, kf += (float)U; s0 + U - 1 <= n_samp; s0 += U, kf += (float)U)
+    if (fast_chunk<U, D, false, 0>(PC, own, dummy, dxs, dys, mx, my, kofs, kf, U)) return s0 + U - 1;
+  if (s0 > n_samp) return s0 - 1;
+  fast_chunk<U, D, true, 0>(PC, own, dummy, dxs, dys, mx, my, kofs, kf, n_samp - s0 + 1);
+  return s0 + U - 1;
+}
+
 // Cast every ray of the env's emitters and mark visible tiles (visibility.py:48-57).
 // Camera rays sample dist = 0.5, 1.0, ..., range (np.linspace(0,1,3) sub-steps; the
 // duplicated integer samples of security.py:78-82 are idempotent and skipped); guard
@@ -172,45 +300,77 @@ __device__ __forceinline__ int march(unsigned char* smem, int PC, int own, doubl
 // dx^2 + dy^2 = 1), and a guard's rays never reach it at dist >= 1 (its tile is marked
 // afterwards anyway), so the own-tile test is confined to the first chunk of cameras.
 //
-// counter (optional): samples evaluated are summed in LDS meta[2] (the ALU work figure of
-// SURVEY 8(d)); raycast_pass adds the env's total to its slot.
+// mode 0 casts each ray on the fp32 fast path unless the tie screen sends it to the exact
+// path; mode 1 casts every ray exactly.  counting: samples evaluated are summed in LDS
+// meta[2] and exact casts in meta[4] (the ALU work figures of SURVEY 8(d)); raycast_pass
+// adds the env's totals to its counters.
 template <int NT, int U, int D>
-__device__ void cast_rays(unsigned char* smem, const EnvLds& L, const unsigned long long* counter, int probe = 0) {
+__device__ void cast_rays(unsigned char* smem, const EnvLds& L, bool counting, int mode, int probe = 0) {
   static_assert(U == 2 || U == 4, "ring offset assumes an even chunk");
   const int n_em = L.meta[0];
   const int total = L.meta[1];
   const int PC = L.PC;
+  const uint32_t base = (uint32_t)(uintptr_t)smem;  // LDS address of the stop map
+  // bits(kMagic32 + v) = 0x4B400000 + v: the row's low 24 bits carry 0x400000 into the
+  // product, which kofs removes together with the column's exponent bits.
+  const uint32_t kofs = 0x400000u * (uint32_t)PC + 0x4B400000u - base;
   int k = 0;
-  unsigned int n_eval = 0;
+  unsigned int n_eval = 0, n_exact = 0;
   for (int j = threadIdx.x; j < total; j += NT) {
     while (k + 1 < n_em && L.em[k + 1].first <= j) ++k;
     const Emit E = L.em[k];
     const int i = j - E.first;
-    const double angle = E.hmh + (E.fov * (double)i) / (double)E.num_rays;  // security.py:70
-    const double rad = angle * kDegToRad;                                   // math.radians
-    double sn, cs;
-    if (probe == 3) {  // profiling: fixed direction, no sin/cos
-      sn = 0.3 + 1e-3 * (double)i;
-      cs = 0.7;
-    } else {
-      heist_trig::sincos(rad, L.tab, &sn, &cs);
-    }
-    if (probe == 2) {  // profiling: angles and sin/cos only
-      if (sn == 12345.0 && cs == 0.0) L.meta[3] = 1;  // keeps the sin/cos live
-      continue;
-    }
-    // dist = stride * s with stride a power of two, so dx * dist == (dx * stride) * s
-    // bit for bit; dy = -sin (security.py:72-75).
-    const double col = (double)E.col, row = (double)E.row;
     const int own = (E.row + U) * PC + (E.col + U);
-    int done;
-    if (E.kind == 0)
-      done = march<U, D, 2>(smem, PC, own, col, row, cs * 0.5, -sn * 0.5, 2 * E.range);
-    else
-      done = march<U, D, 0>(smem, PC, own, col, row, cs, -sn, E.range);
+    const int n_samp = E.kind == 0 ? 2 * E.range : E.range;
+    int done = -1;
+    if (mode == 0 && E.range <= kTieMaxRange) {
+      float cf, sf;
+      fast_dir(__builtin_fma((double)i, E.step, E.hmh), &cf, &sf);
+      if (probe == 2) {  // profiling: angles and sin/cos only
+        if (sf == 12345.0f && cf == 0.0f) L.meta[3] = 1;  // keeps the sin/cos live
+        continue;
+      }
+      if (probe == 3) {  // profiling: fixed direction, no sin/cos
+        sf = 0.3f + 1e-3f * (float)i;
+        cf = 0.7f;
+      }
+      if (probe == 3 || !near_tie(cf, sf)) {
+        const float mx = kMagic32 + (float)(E.col + U), my = kMagic32 + (float)(E.row + U);
+        if (E.kind == 0)
+          done = march_fast<U, D, 2>(PC, own + base, base, cf * 0.5f, -sf * 0.5f, mx, my, kofs, n_samp);
+        else
+          done = march_fast<U, D, 0>(PC, own + base, base, cf, -sf, mx, my, kofs, n_samp);
+      }
+    }
+    if (done < 0) {  // exact path (mode 1, range > 6, or a ray near a tie point)
+      ++n_exact;
+      const double angle = E.hmh + (E.fov * (double)i) / (double)E.num_rays;  // security.py:70
+      const double rad = angle * kDegToRad;                                   // math.radians
+      double sn, cs;
+      if (probe == 3) {
+        sn = 0.3 + 1e-3 * (double)i;
+        cs = 0.7;
+      } else {
+        heist_trig::sincos(rad, kSinCosTab, &sn, &cs);
+      }
+      if (probe == 2) {
+        if (sn == 12345.0 && cs == 0.0) L.meta[3] = 1;
+        continue;
+      }
+      // dist = stride * s with stride a power of two, so dx * dist == (dx * stride) * s
+      // bit for bit; dy = -sin (security.py:72-75).
+      const double col = (double)E.col, row = (double)E.row;
+      if (E.kind == 0)
+        done = march<U, D, 2>(smem, PC, own, col, row, cs * 0.5, -sn * 0.5, n_samp);
+      else
+        done = march<U, D, 0>(smem, PC, own, col, row, cs, -sn, n_samp);
+    }
     n_eval += (unsigned int)done;
   }
-  if (counter) atomicAdd(reinterpret_cast<unsigned int*>(&L.meta[2]), (unsigned int)n_eval);
+  if (counting) {
+    atomicAdd(reinterpret_cast<unsigned int*>(&L.meta[2]), n_eval);
+    atomicAdd(reinterpret_cast<unsigned int*>(&L.meta[4]), n_exact);
+  }
 }
 
 // Publish this tick's emitter table: thread t < n_em holds emitter t in E.  Every
@@ -235,6 +395,7 @@ __device__ __forceinline__ void publish_emitters(const EnvLds& L, Emit E, int n_
       L.meta[0] = n_em;
       L.meta[1] = incl;
       L.meta[2] = 0;
+      L.meta[4] = 0;
     }
   }
 }
@@ -244,6 +405,7 @@ __device__ __forceinline__ Emit cam_emit(const Cam& cm) {
   E.hmh = cm.heading - cm.fov / 2.0;  // security.py:64, :70
   E.fov = cm.fov;
   E.row = cm.row; E.col = cm.col; E.range = cm.range; E.num_rays = cm.num_rays;
+  E.step = cm.fov / (double)cm.num_rays;
   E.first = 0; E.kind = 0;
   return E;
 }
@@ -253,6 +415,7 @@ __device__ __forceinline__ Emit guard_emit(const Guard& gd) {
   E.hmh = gd.heading - gd.fov / 2.0;
   E.fov = gd.fov;
   E.row = unpack_r(gd.pos); E.col = unpack_c(gd.pos); E.range = gd.range; E.num_rays = gd.num_rays;
+  E.step = gd.fov / (double)gd.num_rays;
   E.first = 0; E.kind = 1;
   return E;
 }
@@ -267,9 +430,11 @@ __device__ __forceinline__ void raycast_pass(const EnvParams& p, unsigned char* 
     const Emit E = L.em[t];
     L.vis[L.at(E.row, E.col)] = 1;
   }
-  if (p.probe_mode != 1 && p.probe_mode != 5) cast_rays<NT, U, D>(smem, L, p.sample_counter, p.probe_mode);
+  const bool counting = p.sample_counter || p.redo_counter;
+  if (p.probe_mode != 1 && p.probe_mode != 5) cast_rays<NT, U, D>(smem, L, counting, p.ray_mode, p.probe_mode);
   __syncthreads();
   if (p.sample_counter && t == 0) p.sample_counter[blockIdx.x] += (unsigned int)L.meta[2];
+  if (p.redo_counter && t == 0) p.redo_counter[blockIdx.x] += (unsigned int)L.meta[4];
 }
 
 template <int NT, int U>
@@ -293,7 +458,7 @@ static_assert(sizeof(EmitterRaw) == sizeof(Cam) && sizeof(EmitterRaw) == sizeof(
 __device__ __forceinline__ Cam as_cam(const EmitterRaw& r) { return __builtin_bit_cast(Cam, r); }
 __device__ __forceinline__ Guard as_guard(const EmitterRaw& r) { return __builtin_bit_cast(Guard, r); }
 
-// Issue every per-env HBM read before the first barrier: sin/cos table, grid, guard
+// Issue every per-env HBM read before the first barrier: grid, guard
 // paths and the static position plane (for LDS), this thread's camera/guard record (for
 // registers).  Each thread's first element of every array is loaded before anything is
 // stored, so the whole prefetch is one memory round trip; the loops only cover what one
@@ -304,9 +469,6 @@ __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds
                                          EmitterRaw& raw) {
   const int t = threadIdx.x;
   const int RC = p.RC;
-  constexpr int kTab2 = kTabDoubles / 2;
-  const double2* tab2 = reinterpret_cast<const double2*>(kSinCosTab);
-  double2* ltab2 = reinterpret_cast<double2*>(L.tab);
   const uint8_t* src = p.grid + (size_t)e * RC;
   const int pw = p.max_guards * p.max_path;
   const uint16_t* ps = p.paths + (size_t)e * pw;
@@ -317,11 +479,9 @@ __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds
   uint32_t* d4 = reinterpret_cast<uint32_t*>(L.grid);
   float4* lp = reinterpret_cast<float4*>(L.plane);
 
-  double2 tv = make_double2(0.0, 0.0);
   uint32_t gv = 0u;
   float4 pv = make_float4(0.f, 0.f, 0.f, 0.f);
   uint16_t wv = 0;
-  if (t < kTab2) tv = tab2[t];
   if (t < n4) {
     gv = s4[t];
     pv = pl0[t];
@@ -335,13 +495,11 @@ __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds
     raw.a = rs[0];
     raw.b = rs[1];
   }
-  if (t < kTab2) ltab2[t] = tv;
   if (t < n4) {
     d4[t] = gv;
     lp[t] = pv;
   }
   if (t < pw) L.path[t] = wv;
-  for (int i = t + NT; i < kTab2; i += NT) ltab2[i] = tab2[i];
   for (int i = t + NT; i < n4; i += NT) {
     d4[i] = s4[i];
     lp[i] = pl0[i];
@@ -454,7 +612,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   const int a_raw = (int)actions[e];
   clear_vis<NT, U>(p, L);
   const bool act = !s.done;
-  __syncthreads();  // grid, paths, table in LDS
+  __syncthreads();  // grid, paths in LDS
   build_wall_map<NT, U>(L.grid, L, p.R, p.C);  // read by the raycast after its first barrier
 
   double reward = 0.0;
@@ -739,15 +897,13 @@ __global__ __launch_bounds__(64) void bfs_kernel(const int32_t* __restrict__ gri
 template <int D>
 __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* __restrict__ walls,
                                                     const int32_t* __restrict__ meta, const double* __restrict__ params,
-                                                    uint8_t* __restrict__ out) {
+                                                    uint8_t* __restrict__ out, int ray_mode) {
   constexpr int U = 4;
   extern __shared__ __align__(16) unsigned char smem[];
   const int e = blockIdx.x;
   const int lane = threadIdx.x;
   const int RC = R * C;
   const EnvLds L = carve<U, D>(smem, R, C, 1, 0);
-  const double2* tab2 = reinterpret_cast<const double2*>(kSinCosTab);
-  for (int i = lane; i < kTabDoubles / 2; i += 64) reinterpret_cast<double2*>(L.tab)[i] = tab2[i];
   for (int i = lane; i < RC; i += 64) L.grid[i] = walls[(size_t)e * RC + i] ? kWall : kEmpty;
   for (int i = lane; i < padded_bytes(R, C, U); i += 64) L.vis[i] = 0;
   if (lane == 0) {
@@ -757,6 +913,7 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
     E.hmh = heading - fov / 2.0;
     E.fov = fov;
     E.row = row; E.col = col; E.range = range; E.num_rays = num_rays_for(fov);
+    E.step = fov / (double)E.num_rays;
     E.first = 0; E.kind = kind;
     L.em[0] = E;
     L.meta[0] = 1;
@@ -765,7 +922,7 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
   __syncthreads();
   build_wall_map<64, U>(L.grid, L, R, C);
   __syncthreads();
-  cast_rays<64, U, D>(smem, L, nullptr);
+  cast_rays<64, U, D>(smem, L, false, ray_mode);
   __syncthreads();
   for (int i = lane; i < RC; i += 64) {
     const int r = i / C;
@@ -899,13 +1056,25 @@ hipError_t launch_bfs(const int32_t* grid, int n, int R, int C, int sr, int sc, 
 }
 
 hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
-                        uint8_t* out, hipStream_t st) {
+                        uint8_t* out, int ray_mode, hipStream_t st) {
   const int D = vis_gap_for(R, C, 4);
   const size_t lds = env_lds_bytes(R, C, 1, 0, D);
   if (D == 1024)
-    hipLaunchKernelGGL(cones_kernel<1024>, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, out);
+    hipLaunchKernelGGL(cones_kernel<1024>, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, out, ray_mode);
   else
-    hipLaunchKernelGGL(cones_kernel<5376>, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, out);
+    hipLaunchKernelGGL(cones_kernel<5376>, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, out, ray_mode);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void fast_dir_kernel(const double* __restrict__ deg, int64_t n,
+                                                       float* __restrict__ co, float* __restrict__ so) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    fast_dir(deg[i], co + i, so + i);
+}
+
+hipError_t launch_fast_dir(const double* deg, int64_t n, float* co, float* so, hipStream_t st) {
+  int64_t b = (n + 255) / 256;
+  hipLaunchKernelGGL(fast_dir_kernel, dim3((unsigned)(b > 4096 ? 4096 : (b < 1 ? 1 : b))), dim3(256), 0, st, deg, n, co, so);
   return hipGetLastError();
 }
 

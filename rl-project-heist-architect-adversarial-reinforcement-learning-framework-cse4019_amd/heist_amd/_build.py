@@ -19,6 +19,9 @@ ARCH = os.environ.get("HEIST_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["heist_env.hip", "heist_arch.hip", "heist_ppo.hip", "heist_policy.hip", "heist_capi.hip"]
 HEADERS = ["heist_device.h", "heist_trig.h", "heist_sincos_table.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# heist_env.hip: no SLP vectorization -- ROCm 7.2 clang miscompiles the packed-fp32
+# (v_pk_*_f32) forms of the fast raycast (see the fast path notes in heist_env.hip).
+FILE_FLAGS = {"heist_env.hip": ["-fno-slp-vectorize"]}
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
           "--offload-arch=" + ARCH, "-I", INCLUDE, "-I", CSRC]
 
@@ -50,7 +53,7 @@ def build(force=False, verbose=False, jobs=4):
     procs, objs = [], []
     for src in SOURCES:
         obj = os.path.join(BUILD_DIR, src.replace(".hip", ".o"))
-        cmd = [HIPCC] + CFLAGS + ["-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [HIPCC] + CFLAGS + FILE_FLAGS.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))

@@ -32,8 +32,12 @@ SIGNATURES = {
     "heist_step": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
     "heist_export": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "heist_count_samples": (_i, [_vp, _vp]),
+    "heist_count_redo": (_i, [_vp, _vp]),
+    "heist_set_ray_mode": (_i, [_vp, _i]),
     "heist_bfs_valid": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "heist_cones": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
+    "heist_cones_mode": (_i, [_i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp]),
+    "heist_fast_dir": (_i, [_vp, _i64, _vp, _vp, _vp]),
     "heist_architect_decode": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp]),
     "heist_sincos": (_i, [_vp, _i64, _vp, _vp, _vp]),

@@ -268,6 +268,22 @@ class HeistEnv:
         nat.check(nat.lib().heist_count_samples(self._h, nat.ptr(counter)), "heist_count_samples")
         self._counter = counter  # keep the buffer alive while the library holds its pointer
 
+    def count_exact_rays(self, counter: Optional[torch.Tensor]) -> None:
+        """Instrumentation: later step/reset calls add to ``counter[e]`` the number of env e's
+        rays cast on the exact fp64 path (near-tie re-casts of the fp32 fast path, or every
+        ray with ``set_ray_mode(1)``).  ``None`` switches counting off."""
+        if counter is not None and (counter.dtype != torch.int64 or counter.numel() != self.n_envs
+                                    or counter.device != self.device or not counter.is_contiguous()):
+            raise ValueError("count_exact_rays: need a contiguous int64 [%d] tensor on %s" % (self.n_envs, self.device))
+        nat.check(nat.lib().heist_count_redo(self._h, nat.ptr(counter)), "heist_count_redo")
+        self._redo_counter = counter
+
+    def set_ray_mode(self, mode: int) -> None:
+        """0 (default): fp32 fast raycast with exact fp64 re-cast of near-tie rays; 1: exact
+        fp64 raycast for every ray.  Results are bit-identical; 1 is for parity tests and A/B
+        timing."""
+        nat.check(nat.lib().heist_set_ray_mode(self._h, int(mode)), "heist_set_ray_mode")
+
     @property
     def visibility(self) -> torch.Tensor:
         """Current visibility plane [N, R, C] (obs channel 1)."""

@@ -202,3 +202,121 @@ def test_sample_counter_work_figure(gpu_device):
     envs[0].count_samples(None)
     envs[0].step(torch.tensor([0, 0]))
     assert cnt.tolist() == [4 * per_pass] * 2
+
+
+# --- fp32 fast raycast vs exact fp64 raycast ------------------------------------------
+
+def _fast_dir(deg, dev):
+    from heist_amd import _native as nat
+    x = torch.as_tensor(deg, dtype=torch.float64, device=dev).contiguous()
+    co = torch.empty(x.numel(), dtype=torch.float32, device=dev)
+    so = torch.empty_like(co)
+    nat.check(nat.lib().heist_fast_dir(nat.ptr(x), x.numel(), nat.ptr(co), nat.ptr(so), nat.stream(dev)),
+              "heist_fast_dir")
+    return co, so
+
+
+def _exact_dir(deg, dev):
+    from heist_amd import _native as nat
+    rad = torch.as_tensor(deg, dtype=torch.float64, device=dev) * (np.pi / 180.0)  # math.radians
+    rad = rad.contiguous()
+    so = torch.empty_like(rad)
+    co = torch.empty_like(rad)
+    nat.check(nat.lib().heist_sincos(nat.ptr(rad), rad.numel(), nat.ptr(so), nat.ptr(co), nat.stream(dev)),
+              "heist_sincos")
+    return co, so
+
+
+def test_fast_direction_error(gpu_device):
+    """The fast path's fp32 direction is within 3e-7 of the exact (glibc) one; the near-tie
+    screen assumes kDirErr = 1e-6, so this keeps a >3x margin."""
+    rng = np.random.default_rng(0)
+    deg = np.concatenate([
+        rng.uniform(-200.0, 560.0, 4_000_000),
+        np.arange(-180.0, 540.0, 0.25),                                   # integer / quarter headings
+        (np.arange(-8, 13)[:, None] * 45.0 + rng.uniform(-1e-3, 1e-3, (21, 2000))).ravel(),  # octant edges
+        rng.uniform(0, 360, 200_000).astype(np.float32).astype(np.float64),  # f32 Architect params
+    ])
+    cf, sf = _fast_dir(deg, gpu_device)
+    ce, se = _exact_dir(deg, gpu_device)
+    err = max(float((cf.double() - ce).abs().max()), float((sf.double() - se).abs().max()))
+    assert err < 3e-7, err
+
+
+def _cones(n, R, C, walls, meta, par, mode, dev):
+    from heist_amd import _native as nat
+    out = torch.empty((n, R, C), dtype=torch.uint8, device=dev)
+    nat.check(nat.lib().heist_cones_mode(n, R, C, nat.ptr(walls), nat.ptr(meta), nat.ptr(par), mode, nat.ptr(out),
+                                         nat.stream(dev)), "heist_cones_mode")
+    return out
+
+
+@pytest.mark.parametrize("R,C", [(20, 20), (32, 32), (64, 64), (9, 23)])
+def test_cones_fast_equals_exact(R, C, gpu_device):
+    """heist_cones_mode 0 (fp32 fast + exact re-cast) == mode 1 (exact fp64) bit for bit on
+    random emitters, including exact-tie headings (integer and half degrees, the reference's
+    defaults), ranges above the fast path's limit, and random wall maps."""
+    rng = np.random.default_rng(R * 100 + C)
+    n = 20000
+    walls = (rng.random((n, R, C)) < rng.uniform(0.0, 0.35, (n, 1, 1))).astype(np.uint8)
+    kind = rng.integers(0, 2, n)
+    row = rng.integers(0, R, n)
+    col = rng.integers(0, C, n)
+    rng_ = np.where(rng.random(n) < 0.9, np.where(kind == 0, 6, 4), rng.integers(1, 12, n))
+    fov = np.where(rng.random(n) < 0.3, rng.choice([30.0, 45.0, 60.0, 90.0, 120.0], n),
+                   rng.uniform(30.0, 120.0, n).astype(np.float32).astype(np.float64))
+    head = np.select([rng.random(n) < 0.3, rng.random(n) < 0.5],
+                     [rng.integers(0, 72, n) * 5.0, rng.integers(0, 720, n) * 0.5],
+                     rng.uniform(0.0, 360.0, n).astype(np.float32).astype(np.float64))
+    walls[np.arange(n), row, col] = 0
+    dev = gpu_device
+    wt = torch.tensor(walls, device=dev)
+    meta = torch.tensor(np.stack([kind, row, col, rng_], 1).astype(np.int32), device=dev)
+    par = torch.tensor(np.stack([fov, head], 1), dtype=torch.float64, device=dev)
+    fast = _cones(n, R, C, wt, meta, par, 0, dev)
+    exact = _cones(n, R, C, wt, meta, par, 1, dev)
+    bad = (fast != exact).flatten(1).any(1).nonzero().flatten().tolist()
+    assert not bad, [(int(kind[i]), int(row[i]), int(col[i]), int(rng_[i]), fov[i], head[i]) for i in bad[:5]]
+
+
+def test_step_fast_equals_exact_and_redo_rate(gpu_device):
+    """Two handles on the same layouts, one fast (mode 0) and one exact (mode 1): every
+    observation, reward and status is identical over 150 ticks with auto-reset.  Synthetic
+    (f32-random) headings re-cast only a small fraction of rays exactly; the reference's
+    default cameras (heading 0, fov 60, speed 15: half-degree ray angles) re-cast many."""
+    n = 1024
+    cfg = EnvironmentConfig()
+    lays = synthetic_layouts(n - 64, 20, 20, 15, seed=77)
+    cam = {"row": 10, "col": 10, "fov_angle": 60.0, "heading": 0.0, "rotation_speed": 15.0, "vision_range": 6}
+    for k in range(64):
+        c = dict(cam, row=3 + k % 14, col=2 + (k * 7) % 15)
+        lays.append(([(5, 5 + k % 10)], [c], [{"patrol_path": [(15, 3), (15, 4), (14, 4)], "speed": 1,
+                                                 "vision_range": 4, "fov_angle": 90.0}]))
+    envs = [HeistEnv(n, cfg, device=gpu_device) for _ in range(2)]
+    envs[1].set_ray_mode(1)
+    cnt = [torch.zeros(n, dtype=torch.int64, device=gpu_device) for _ in range(2)]
+    for e, c in zip(envs, cnt):
+        e.set_layouts(lays, budget=15)
+        e.count_exact_rays(c)
+    o0, o1 = envs[0].reset(), envs[1].reset()
+    assert torch.equal(o0, o1)
+    cnt_s = [torch.zeros(n, dtype=torch.int64, device=gpu_device) for _ in range(2)]
+    envs[0].count_samples(cnt_s[0])
+    envs[1].count_samples(cnt_s[1])
+    g = torch.Generator(device="cpu").manual_seed(5)
+    for t in range(150):
+        a = torch.randint(0, 5, (n,), generator=g)
+        r0 = envs[0].step(a)
+        r1 = envs[1].step(a)
+        for x, y in zip(r0, r1):
+            assert torch.equal(x, y), t
+        assert torch.equal(envs[0].reward64, envs[1].reward64), t
+    assert torch.equal(cnt_s[0], cnt_s[1])
+    exact_all = cnt[1].double()
+    frac_syn = float(cnt[0][: n - 64].sum()) / float(exact_all[: n - 64].sum())
+    frac_def = float(cnt[0][n - 64:].sum()) / float(exact_all[n - 64:].sum())
+    assert frac_syn < 0.01, frac_syn
+    assert frac_def > frac_syn, (frac_def, frac_syn)
+    for e in envs:
+        e.count_exact_rays(None)
+        e.count_samples(None)

@@ -14,6 +14,7 @@ from heist_amd.layouts import valid_synthetic_layouts  # noqa: E402
 
 VARIANTS = {
     "w4_u4_o1": {},
+    "w4_u4_o1_exact": {"HEIST_EXACT_RAYS": "1"},
     "w4_u4_o8": {"HEIST_STEP_OCC": "8"},
     "w2_u4_o1": {"HEIST_STEP_WAVES": "2"},
     "w4_u2_o1": {"HEIST_RAY_CHUNK": "2"},
@@ -24,7 +25,7 @@ def main():
     n = int(os.environ.get("PROBE_N", "4096"))
     envs = {}
     for name, ev in VARIANTS.items():
-        for k in ("HEIST_STEP_WAVES", "HEIST_RAY_CHUNK", "HEIST_STEP_OCC"):
+        for k in ("HEIST_STEP_WAVES", "HEIST_RAY_CHUNK", "HEIST_STEP_OCC", "HEIST_EXACT_RAYS"):
             os.environ.pop(k, None)
         os.environ.update(ev)
         env = HeistEnv(n, EnvironmentConfig(), max_cams=8, max_guards=4, max_path=16, device="cuda", auto_reset=True)

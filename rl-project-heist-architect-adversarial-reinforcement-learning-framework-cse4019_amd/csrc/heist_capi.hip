@@ -24,7 +24,7 @@ hipError_t launch_export(const EnvParams& p, int32_t* scalars, int8_t* grid, dou
                          double* guard_heading, hipStream_t st);
 hipError_t launch_bfs(const int32_t* grid, int n, int R, int C, int sr, int sc, int gr, int gc, uint8_t* out,
                       hipStream_t st);
-int vis_gap_for(int R, int C, int U);
+int vis_gap_for(int R, int C);
 bool env_variant_exists(int W, int U, int O, int D);
 hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
                         uint8_t* out, int ray_mode, hipStream_t st);
@@ -172,8 +172,10 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
     p.axis_heading[3] = htab[(size_t)(R - 1) * W2 + (1 + C - 1)];
   }
   p.step_waves = 4;
-  p.ray_chunk = 4;  // tuning knobs; a combination without a compiled variant falls back to (4, 4, 1)
-  p.step_occ = 1;
+  p.ray_chunk = 4;  // tuning knobs; a combination without a compiled variant falls back to (4, 4, 8)
+  // 8 waves per SIMD (64 VGPRs): 4096 envs are two full rounds of 8 workgroups per CU
+  // (41.4 us per step vs 46.6 at the unbounded 85 VGPRs / 5 waves, profiles/r01m_*)
+  p.step_occ = 8;
   if (const char* u = getenv("HEIST_RAY_CHUNK")) p.ray_chunk = atoi(u);
   if (const char* o = getenv("HEIST_STEP_OCC")) p.step_occ = atoi(o);
   if (const char* w = getenv("HEIST_STEP_WAVES")) p.step_waves = atoi(w);
@@ -183,12 +185,12 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   if (const char* m = getenv("HEIST_EXACT_RAYS")) p.ray_mode = atoi(m) ? 1 : 0;
   p.sample_counter = nullptr;
   p.redo_counter = nullptr;
-  p.vis_gap = heist::vis_gap_for(R, C, p.ray_chunk == 2 ? 2 : 4);
+  p.vis_gap = heist::vis_gap_for(R, C);
   if (!heist::env_variant_exists(p.step_waves, p.ray_chunk, p.step_occ, p.vis_gap)) {
     p.step_waves = 4;
     p.ray_chunk = 4;
-    p.step_occ = 1;
-    p.vis_gap = heist::vis_gap_for(R, C, 4);
+    p.step_occ = 8;
+    p.vis_gap = heist::vis_gap_for(R, C);
   }
   for (int k = 0; k < 8; ++k) p.tile_lut[k] = k <= 5 ? (float)k / 5.0f : 0.0f;  // environment.py:319
 

@@ -44,31 +44,39 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(
 // ---------------------------------------------------------------------------
 
 struct EnvLds {
-  uint8_t* wall;   // LDS offset 0: [(R+2U)(C+2U)] ray stop map, 1 = wall or outside the grid
+  uint8_t* wall;   // LDS offset 0: [(R+2G)(C+2G)] ray stop map, 1 = wall or outside the grid (G = kRing)
   uint8_t* vis;    // LDS offset D: visibility with the same padded geometry (ring bytes unused)
   uint8_t* grid;   // [RC]
   Emit* em;        // [n_emit]
   uint16_t* path;  // [max_guards][max_path]
   float* plane;    // [RC] static position channel (plane0)
+  int* queue;      // [W][64] per-wave exact-path ray queues (cast_rays)
   int* meta;       // [0] emitters, [1] total rays
-  int PC;          // padded row stride C + 2U
-  int off0;        // padded index of tile (0, 0): U * PC + U
+  int PC;          // padded row stride C + 2G
+  int off0;        // padded index of tile (0, 0): G * PC + G
   __device__ __forceinline__ int at(int r, int c) const { return off0 + r * PC + c; }
 };
 
-// The padded planes hold (R + 2U) x (C + 2U) bytes; D is the compile-time distance from
-// the stop map to the visibility plane (so one address serves both), 1024 for grids up to
-// 24 x 24 at U = 4 and 5376 for the 64 x 64 maximum.
-__host__ __device__ inline int padded_bytes(int R, int C, int U) { return (R + 2 * U) * (C + 2 * U); }
+// Width G of the stop ring around the grid: the longest fp32 fast-path ray (range
+// kTieMaxRange = 6) ends at most G tiles from its emitter, so every one of its sample
+// addresses lies inside the padded map, stopped or not (march_fast); the exact path's
+// U-sample chunks need G >= U.  Even, so the half-to-even rounding can carry the offset.
+constexpr int kRing = 6;
 
-__host__ __device__ inline size_t env_lds_bytes(int R, int C, int n_emit, int path_words, int D) {
+// The padded planes hold (R + 2G) x (C + 2G) bytes; D is the compile-time distance from
+// the stop map to the visibility plane (so one address serves both), 1024 for grids up to
+// 20 x 20 and 6144 for the 64 x 64 maximum.
+__host__ __device__ inline int padded_bytes(int R, int C) { return (R + 2 * kRing) * (C + 2 * kRing); }
+
+__host__ __device__ inline size_t env_lds_bytes(int R, int C, int n_emit, int path_words, int D, int waves) {
   const int RC = R * C;
   return 2 * (size_t)D + align16(RC) + align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) +
-         align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1)) + align16(sizeof(float) * RC) + 32;
+         align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1)) + align16(sizeof(float) * RC) +
+         sizeof(int) * 64 * (size_t)waves + 32;
 }
 
-template <int U, int D>
-__device__ __forceinline__ EnvLds carve(unsigned char* smem, int R, int C, int n_emit, int path_words) {
+template <int D>
+__device__ __forceinline__ EnvLds carve(unsigned char* smem, int R, int C, int n_emit, int path_words, int waves) {
   const int RC = R * C;
   EnvLds L;
   L.wall = smem;
@@ -78,19 +86,20 @@ __device__ __forceinline__ EnvLds carve(unsigned char* smem, int R, int C, int n
   L.em = reinterpret_cast<Emit*>(smem + o); o += align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1));
   L.path = reinterpret_cast<uint16_t*>(smem + o); o += align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1));
   L.plane = reinterpret_cast<float*>(smem + o); o += align16(sizeof(float) * RC);
+  L.queue = reinterpret_cast<int*>(smem + o); o += sizeof(int) * 64 * (size_t)waves;
   L.meta = reinterpret_cast<int*>(smem + o);
-  L.PC = C + 2 * U;
-  L.off0 = U * L.PC + U;
+  L.PC = C + 2 * kRing;
+  L.off0 = kRing * L.PC + kRing;
   return L;
 }
 
 // The padded stop map for tile grid g (stride C bytes in LDS).
-template <int NT, int U>
+template <int NT>
 __device__ __forceinline__ void build_wall_map(const uint8_t* g, const EnvLds& L, int R, int C) {
   const int PC = L.PC;
-  for (int i = threadIdx.x; i < (R + 2 * U) * PC; i += NT) {
+  for (int i = threadIdx.x; i < (R + 2 * kRing) * PC; i += NT) {
     const int pr = i / PC;
-    const int r = pr - U, c = i - pr * PC - U;
+    const int r = pr - kRing, c = i - pr * PC - kRing;
     const bool out = (unsigned)r >= (unsigned)R || (unsigned)c >= (unsigned)C;
     L.wall[i] = out ? 1 : (g[r * C + c] == kWall ? 1 : 0);
   }
@@ -114,45 +123,56 @@ __device__ __forceinline__ int round_plus(double x) {
 // branch-free visibility stores (a masked sample writes byte 0 of the vis plane, a ring
 // byte nobody reads).  TAIL masks samples past the ray's last one (u >= left).  OWN is the
 // number of leading samples that may land on the emitter's own tile (see cast_rays).
+// Returns the index of the chunk's first sample that ends the ray (a wall or the grid
+// edge; with TAIL also sample `left`), U if none does.
 template <int U, int D, bool TAIL, int OWN>
-__device__ __forceinline__ bool sample_chunk(unsigned char* smem, int PC, int own, double col, double row,
-                                             double dxs, double dys, double kd, int left) {
+__device__ __forceinline__ int sample_chunk(unsigned char* smem, int PC, int own, double col, double row,
+                                            double dxs, double dys, double kd, int left) {
   int a[U], w[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const double ku = kd + (double)u;  // exact small integer
-    const int c = round_plus<U>(col + dxs * ku);  // padded column c + U
-    const int r = round_plus<U>(row + dys * ku);
+    const int c = round_plus<kRing>(col + dxs * ku);  // padded column c + G
+    const int r = round_plus<kRing>(row + dys * ku);
     a[u] = __mul24(r, PC) + c;
     w[u] = smem[a[u]];
   }
   bool stop = false;
+  int first = U;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    stop |= w[u] != 0 || (TAIL && u >= left);
+    const bool st = w[u] != 0 || (TAIL && u >= left);
+    first = (!stop && st) ? u : first;
+    stop |= st;
     const bool skip = stop || (u < OWN && a[u] == own);
     smem[D + (skip ? 0 : a[u])] = 1;
   }
-  return stop;
+  return first;
 }
 
 // All samples of one ray from sample s0 = 1 on; the first chunk is peeled so that only it
-// carries the own-tile test.  Returns the number of samples evaluated (whole chunks).
+// carries the own-tile test.  Returns the ray's sample count up to and including the
+// sample that ends it (n_samp if none does): the raycast's work figure, the same on the
+// fast path.
 template <int U, int D, int OWN>
 __device__ __forceinline__ int march(unsigned char* smem, int PC, int own, double col, double row, double dxs,
                                      double dys, int n_samp) {
-  double kd = 1.0;
-  int s0 = 1;
   if (n_samp < U) {
-    sample_chunk<U, D, true, OWN>(smem, PC, own, col, row, dxs, dys, kd, n_samp);
-    return U;
+    const int f = sample_chunk<U, D, true, OWN>(smem, PC, own, col, row, dxs, dys, 1.0, n_samp);
+    return f + 1 < n_samp ? f + 1 : n_samp;
   }
-  if (sample_chunk<U, D, false, OWN>(smem, PC, own, col, row, dxs, dys, kd, U)) return U;
-  for (s0 += U, kd += (double)U; s0 + U - 1 <= n_samp; s0 += U, kd += (double)U)
-    if (sample_chunk<U, D, false, 0>(smem, PC, own, col, row, dxs, dys, kd, U)) return s0 + U - 1;
-  if (s0 > n_samp) return s0 - 1;
-  sample_chunk<U, D, true, 0>(smem, PC, own, col, row, dxs, dys, kd, n_samp - s0 + 1);
-  return s0 + U - 1;
+  int f = sample_chunk<U, D, false, OWN>(smem, PC, own, col, row, dxs, dys, 1.0, U);
+  if (f < U) return f + 1;
+  double kd = 1.0 + U;
+  int s0 = 1 + U;
+  for (; s0 + U - 1 <= n_samp; s0 += U, kd += (double)U) {
+    f = sample_chunk<U, D, false, 0>(smem, PC, own, col, row, dxs, dys, kd, U);
+    if (f < U) return s0 + f;
+  }
+  if (s0 > n_samp) return n_samp;
+  const int left = n_samp - s0 + 1;
+  f = sample_chunk<U, D, true, 0>(smem, PC, own, col, row, dxs, dys, kd, left);
+  return s0 - 1 + (f + 1 < left ? f + 1 : left);
 }
 
 // ---- fp32 fast path -------------------------------------------------------------------
@@ -177,6 +197,7 @@ __device__ __forceinline__ int march(unsigned char* smem, int PC, int own, doubl
 // point.  Emitters with range > 6 (K > 12) always take the exact path.
 constexpr float kDirErr = 1e-6f;
 constexpr int kTieMaxRange = 6;
+static_assert(kRing >= kTieMaxRange, "march_fast reads every sample of a ray unconditionally");
 constexpr int kTieL = 27720;                                  // lcm(1, ..., 12)
 constexpr float kTieRad = kDirErr * (float)kTieL + 4e-3f;     // 0.0317 in units of t
 
@@ -240,50 +261,88 @@ __device__ __forceinline__ void lds_st(uint32_t a, uint8_t v) {
   *reinterpret_cast<__attribute__((address_space(3))) uint8_t*>(a) = v;
 }
 
-// U samples k0 .. k0+U-1 of a fast ray.  (dxs, dys) = (dx, dy) * stride, (mx, my) =
-// kMagic32 + the padded (col, row) of the emitter; kofs turns the two rounded bit patterns
-// into the absolute LDS address of the stop byte.  Returns true if the ray stopped.
-// Scalar fp32 on purpose (and this file builds with -fno-slp-vectorize): ROCm 7.2 clang
-// miscompiles the float2 / v_pk_fma_f32 form of this loop (a lane's negation is lost).
-template <int U, int D, bool TAIL, int OWN>
-__device__ __forceinline__ bool fast_chunk(uint32_t PC, uint32_t own, uint32_t dummy, float dxs, float dys, float mx,
-                                           float my, uint32_t kofs, float k0, int left) {
-  uint32_t a[U];
-  int w[U];
+// Every sample k = 1 .. n_samp of a fast ray in one LDS round trip.  (dxs, dys) = (dx, dy)
+// * stride, (mx, my) = kMagic32 + the padded (col, row) of the emitter; kofs turns the two
+// rounded bit patterns into the absolute LDS address of the stop byte.  The ring is as
+// wide as the longest fast ray (kRing >= kTieMaxRange), so each sample address lies inside
+// the padded stop map whether or not the ray has already stopped: all NS wall reads are
+// issued before any is used, and a running stop flag masks the visibility stores (a masked
+// store goes to a ring byte of the vis plane that nobody reads).  NS = n_samp, or with
+// CLAMP NS >= n_samp and the samples past n_samp repeat sample n_samp (k clamped), which
+// changes nothing.  Only the first two samples can land on the emitter's own tile (see
+// cast_rays).  Returns the ray's sample count up to and including the sample that ends it
+// (n_samp if none does), when COUNT.  Scalar fp32 on purpose (and this file builds with
+// -fno-slp-vectorize): ROCm 7.2 clang miscompiles the float2 / v_pk_fma_f32 form of this
+// loop (a lane's negation is lost).
+template <int D, int NS, bool CLAMP, bool COUNT>
+__device__ __forceinline__ int march_fast(uint32_t PC, uint32_t own, uint32_t dummy, float dxs, float dys, float mx,
+                                          float my, uint32_t kofs, int n_samp) {
+  uint32_t a[NS], w[NS];
+  const float kmax = (float)n_samp;
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const float k = k0 + (float)u;  // exact small integer
+  for (int u = 0; u < NS; ++u) {
+    const float k = (CLAMP && u > 0) ? __builtin_fminf((float)(u + 1), kmax) : (float)(u + 1);  // n_samp >= 1
     const float yx = __builtin_fmaf(k, dxs, mx), yy = __builtin_fmaf(k, dys, my);  // rint(k*d) + magic + origin
     a[u] = __umul24(__builtin_bit_cast(uint32_t, yy), PC) + __builtin_bit_cast(uint32_t, yx) - kofs;
     w[u] = lds_ld(a[u]);
   }
-  bool stop = false;
+  uint32_t stop = 0;
+  int cnt = n_samp;
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    stop |= w[u] != 0 || (TAIL && u >= left);
-    const bool skip = stop || (u < OWN && a[u] == own);
+  for (int u = 0; u < NS; ++u) {
+    if (COUNT) cnt = (stop == 0 && w[u] != 0 && u < n_samp) ? u + 1 : cnt;
+    stop |= w[u];
+    const bool skip = stop != 0 || (u < 2 && a[u] == own);
     lds_st((skip ? dummy : a[u]) + D, 1);
   }
-  return stop;
+  return cnt;
 }
 
-// All samples k = 1 .. n_samp of a fast ray (chunk structure of march() below).  Returns
-// the samples evaluated.
-template <int U, int D, int OWN>
-__device__ __forceinline__ int march_fast(uint32_t PC, uint32_t own, uint32_t dummy, float dxs, float dys, float mx,
-                                          float my, uint32_t kofs, int n_samp) {
-  float kf = 1.0f;
-  int s0 = 1;
-  if (n_samp < U) {
-    fast_chunk<U, D, true, OWN>(PC, own, dummy, dxs, dys, mx, my, kofs, kf, n_samp);
-    return U;
+// One ray on the exact path: security.py:70 angle, glibc-exact sin/cos, fp64 march.
+// Returns the ray's sample count (march).
+template <int U, int D>
+__device__ __forceinline__ int exact_ray(unsigned char* smem, const Emit& E, int i, int PC, int probe) {
+  const double angle = E.hmh + (E.fov * (double)i) / (double)E.num_rays;  // security.py:70
+  const double rad = angle * kDegToRad;                                   // math.radians
+  double sn, cs;
+  if (probe == 3) {  // profiling: fixed direction, no sin/cos
+    sn = 0.3 + 1e-3 * (double)i;
+    cs = 0.7;
+  } else {
+    heist_trig::sincos(rad, kSinCosTab, &sn, &cs);
   }
-  if (fast_chunk<U, D, false, OWN>(PC, own, dummy, dxs, dys, mx, my, kofs, kf, U)) return U;
-  for (s0 += U, kf += (float)U; s0 + U - 1 <= n_samp; s0 += U, kf += (float)U)
-    if (fast_chunk<U, D, false, 0>(PC, own, dummy, dxs, dys, mx, my, kofs, kf, U)) return s0 + U - 1;
-  if (s0 > n_samp) return s0 - 1;
-  fast_chunk<U, D, true, 0>(PC, own, dummy, dxs, dys, mx, my, kofs, kf, n_samp - s0 + 1);
-  return s0 + U - 1;
+  const int own = (E.row + kRing) * PC + (E.col + kRing);
+  const int n_samp = E.kind == 0 ? 2 * E.range : E.range;
+  // dist = stride * s with stride a power of two, so dx * dist == (dx * stride) * s
+  // bit for bit; dy = -sin (security.py:72-75).
+  const double col = (double)E.col, row = (double)E.row;
+  if (E.kind == 0) return march<U, D, 2>(smem, PC, own, col, row, cs * 0.5, -sn * 0.5, n_samp);
+  return march<U, D, 0>(smem, PC, own, col, row, cs, -sn, n_samp);
+}
+
+// Wave-uniform values into scalar registers (every lane holds the same copy).
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ double uni(double x) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, x);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ Emit uni(const Emit& e) {
+  Emit u;
+  u.hmh = uni(e.hmh); u.fov = uni(e.fov); u.step = uni(e.step);
+  u.row = uni(e.row); u.col = uni(e.col); u.range = uni(e.range); u.num_rays = uni(e.num_rays);
+  u.first = uni(e.first); u.kind = uni(e.kind);
+  return u;
+}
+
+// An emitter's rays go to the fp32 fast path unless it is exact-only (mode 1, range > 6).
+__device__ __forceinline__ bool fast_emitter(const Emit& E, int mode) { return mode == 0 && E.range <= kTieMaxRange; }
+
+// The emitter of ray chunk c (wave-uniform), searching forward from emitter k.
+__device__ __forceinline__ int emitter_of_chunk(const EnvLds& L, int n_em, int k, int c) {
+  while (k + 1 < n_em && uni(L.em[k + 1].first) <= c) ++k;
+  return k;
 }
 
 // Cast every ray of the env's emitters and mark visible tiles (visibility.py:48-57).
@@ -292,95 +351,147 @@ __device__ __forceinline__ int march_fast(uint32_t PC, uint32_t own, uint32_t du
 // rays sample dist = 1..range.  A wall or the grid edge ends the ray; the emitter's own
 // tile is never marked by its rays.
 //
-// A sample moves at most one tile per axis from the previous one, and a chunk of U
-// samples only starts while the ray is still inside the grid, so every sample lands
-// within U tiles of the grid: a U-wide ring of stop bytes makes every lookup
-// unconditional, with no clamping.  Only a camera's first two samples (dist 0.5, 1) can
-// round back to its own tile (|dx|, |dy| < 0.5 cannot both hold beyond dist 1 since
-// dx^2 + dy^2 = 1), and a guard's rays never reach it at dist >= 1 (its tile is marked
-// afterwards anyway), so the own-tile test is confined to the first chunk of cameras.
+// On the exact path a sample moves at most one tile per axis from the previous one, and a
+// chunk of U samples only starts while the ray is still inside the grid, so every sample
+// lands within U <= G tiles of the grid; a fast ray stays within its range <= G of its
+// emitter (march_fast).  The G-wide ring of stop bytes makes every lookup unconditional,
+// with no clamping.  Only a camera's first two samples (dist 0.5, 1) can round back to its
+// own tile (|dx|, |dy| < 0.5 cannot both hold beyond dist 1 since dx^2 + dy^2 = 1), and a
+// guard's rays never reach it at dist >= 1 (its tile is marked afterwards anyway), so the
+// own-tile test is confined to the first two samples.
 //
-// mode 0 casts each ray on the fp32 fast path unless the tie screen sends it to the exact
-// path; mode 1 casts every ray exactly.  counting: samples evaluated are summed in LDS
-// meta[2] and exact casts in meta[4] (the ALU work figures of SURVEY 8(d)); raycast_pass
-// adds the env's totals to its counters.
-template <int NT, int U, int D>
-__device__ void cast_rays(unsigned char* smem, const EnvLds& L, bool counting, int mode, int probe = 0) {
-  static_assert(U == 2 || U == 4, "ring offset assumes an even chunk");
-  const int n_em = L.meta[0];
-  const int total = L.meta[1];
+// Work unit: a CHUNK of 64 consecutive rays of one emitter (publish_emitters numbers them),
+// one ray per lane; wave w takes chunks w, w + W, ...  Within a chunk the emitter, and so
+// its pose, sample count and stride, is wave-uniform and lives in scalar registers; only
+// the ray angle differs per lane.  Two passes per wave, so that the exact path's fp64
+// registers are not live during the fast one.  Pass 1 casts the fast emitters' rays on the
+// fp32 fast path; a ray the tie screen rejects goes to the wave's 64-entry LDS queue
+// (ballot + mbcnt, no atomics).  Pass 2 casts the queued rays exactly, one per lane (a wave
+// whose queue overflowed re-walks its fast chunks and re-casts every ray the same
+// deterministic screen rejects), then every ray of the wave's exact-only chunks.
+// Visibility stores are idempotent, so the pass order does not matter.  COUNT: samples (up
+// to the one that ends each ray) are summed in LDS meta[2] and exact casts in meta[4] (the
+// ALU work figures of SURVEY 8(d)); raycast_pass adds the env's totals to its counters.
+template <int NT, int U, int D, bool COUNT>
+__device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int probe) {
+  static_assert(U == 2 || U == 4, "exact-path chunk");
+  static_assert(kRing >= U, "the exact path's chunks stay inside the ring");
+  constexpr int W = NT / 64;
+  const int n_em = uni(L.meta[0]);
+  const int n_chunk = uni(L.meta[1]);
   const int PC = L.PC;
+  const int lane = threadIdx.x & 63;
+  const int wave = uni((int)(threadIdx.x >> 6));
+  int* queue = L.queue + wave * 64;
   const uint32_t base = (uint32_t)(uintptr_t)smem;  // LDS address of the stop map
   // bits(kMagic32 + v) = 0x4B400000 + v: the row's low 24 bits carry 0x400000 into the
   // product, which kofs removes together with the column's exponent bits.
   const uint32_t kofs = 0x400000u * (uint32_t)PC + 0x4B400000u - base;
-  int k = 0;
+  // masked fast-path stores: one dword per lane of a 32-lane LDS group, in the vis plane's
+  // top ring rows (G * PC >= 78 bytes; wrapped below that)
+  const uint32_t dummy = base + (uint32_t)((4 * (threadIdx.x & 31)) % (kRing * PC));
   unsigned int n_eval = 0, n_exact = 0;
-  for (int j = threadIdx.x; j < total; j += NT) {
-    while (k + 1 < n_em && L.em[k + 1].first <= j) ++k;
-    const Emit E = L.em[k];
-    const int i = j - E.first;
-    const int own = (E.row + U) * PC + (E.col + U);
-    const int n_samp = E.kind == 0 ? 2 * E.range : E.range;
-    int done = -1;
-    if (mode == 0 && E.range <= kTieMaxRange) {
+  int qn = 0;               // near-tie rays met by this wave (queued while <= 64)
+  bool exact_em = false;    // this wave owns chunks of an exact-only emitter
+  int k = 0;
+  // pass 1: fp32 fast path
+  for (int c = wave; c < n_chunk; c += W) {
+    k = emitter_of_chunk(L, n_em, k, c);
+    const Emit E = uni(L.em[k]);
+    if (!fast_emitter(E, mode)) {
+      exact_em = true;
+      continue;
+    }
+    const int i = (c - E.first) * 64 + lane;
+    const bool active = i <= E.num_rays;  // rays 0 .. num_rays (security.py:68)
+    float cf, sf;
+    fast_dir(__builtin_fma((double)i, E.step, E.hmh), &cf, &sf);
+    if (probe == 2) {  // profiling: angles and sin/cos only
+      if (sf == 12345.0f && cf == 0.0f) L.meta[3] = 1;  // keeps the sin/cos live
+      continue;
+    }
+    if (probe == 3) {  // profiling: fixed direction, no sin/cos
+      sf = 0.3f + 1e-3f * (float)i;
+      cf = 0.7f;
+    }
+    const bool tie = active && probe != 3 && near_tie(cf, sf);
+    const unsigned long long b = __ballot(tie);
+    if (tie) {
+      const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+      if (pos < 64) queue[pos] = (k << 16) | i;
+    }
+    qn += __popcll(b);
+    if (active && !tie) {
+      const uint32_t own = base + (uint32_t)((E.row + kRing) * PC + (E.col + kRing));
+      const int n_samp = E.kind == 0 ? 2 * E.range : E.range;
+      const float mx = kMagic32 + (float)(E.col + kRing), my = kMagic32 + (float)(E.row + kRing);
+      const float h = E.kind == 0 ? 0.5f : 1.0f;  // sample stride: camera half tiles, guard whole tiles
+      const float dxs = cf * h, dys = -sf * h;     // exact scalings; dy = -sin (security.py:72-75)
+      int done;
+      if (n_samp == 2 * kTieMaxRange)  // the reference cameras (range 6)
+        done = march_fast<D, 2 * kTieMaxRange, false, COUNT>(PC, own, dummy, dxs, dys, mx, my, kofs, n_samp);
+      else if (n_samp == 4)  // the reference guards (range 4)
+        done = march_fast<D, 4, false, COUNT>(PC, own, dummy, dxs, dys, mx, my, kofs, n_samp);
+      else if (n_samp < 4)
+        done = march_fast<D, 4, true, COUNT>(PC, own, dummy, dxs, dys, mx, my, kofs, n_samp);
+      else
+        done = march_fast<D, 2 * kTieMaxRange, true, COUNT>(PC, own, dummy, dxs, dys, mx, my, kofs, n_samp);
+      n_eval += (unsigned int)done;
+    }
+  }
+  if (probe == 2) return;
+  // pass 2: exact path (the wave's own LDS writes to its queue are ordered before its reads)
+  __builtin_amdgcn_wave_barrier();
+  if (qn <= 64) {
+    if (lane < qn) {
+      const int v = queue[lane];
+      const Emit E = L.em[v >> 16];
+      ++n_exact;
+      n_eval += (unsigned int)exact_ray<U, D>(smem, E, v & 0xffff, PC, probe);
+    }
+  } else {
+    k = 0;
+    for (int c = wave; c < n_chunk; c += W) {
+      k = emitter_of_chunk(L, n_em, k, c);
+      const Emit E = uni(L.em[k]);
+      if (!fast_emitter(E, mode)) continue;
+      const int i = (c - E.first) * 64 + lane;
       float cf, sf;
       fast_dir(__builtin_fma((double)i, E.step, E.hmh), &cf, &sf);
-      if (probe == 2) {  // profiling: angles and sin/cos only
-        if (sf == 12345.0f && cf == 0.0f) L.meta[3] = 1;  // keeps the sin/cos live
-        continue;
-      }
-      if (probe == 3) {  // profiling: fixed direction, no sin/cos
-        sf = 0.3f + 1e-3f * (float)i;
-        cf = 0.7f;
-      }
-      if (probe == 3 || !near_tie(cf, sf)) {
-        const float mx = kMagic32 + (float)(E.col + U), my = kMagic32 + (float)(E.row + U);
-        if (E.kind == 0)
-          done = march_fast<U, D, 2>(PC, own + base, base, cf * 0.5f, -sf * 0.5f, mx, my, kofs, n_samp);
-        else
-          done = march_fast<U, D, 0>(PC, own + base, base, cf, -sf, mx, my, kofs, n_samp);
+      if (i <= E.num_rays && near_tie(cf, sf)) {
+        ++n_exact;
+        n_eval += (unsigned int)exact_ray<U, D>(smem, E, i, PC, probe);
       }
     }
-    if (done < 0) {  // exact path (mode 1, range > 6, or a ray near a tie point)
-      ++n_exact;
-      const double angle = E.hmh + (E.fov * (double)i) / (double)E.num_rays;  // security.py:70
-      const double rad = angle * kDegToRad;                                   // math.radians
-      double sn, cs;
-      if (probe == 3) {
-        sn = 0.3 + 1e-3 * (double)i;
-        cs = 0.7;
-      } else {
-        heist_trig::sincos(rad, kSinCosTab, &sn, &cs);
-      }
-      if (probe == 2) {
-        if (sn == 12345.0 && cs == 0.0) L.meta[3] = 1;
-        continue;
-      }
-      // dist = stride * s with stride a power of two, so dx * dist == (dx * stride) * s
-      // bit for bit; dy = -sin (security.py:72-75).
-      const double col = (double)E.col, row = (double)E.row;
-      if (E.kind == 0)
-        done = march<U, D, 2>(smem, PC, own, col, row, cs * 0.5, -sn * 0.5, n_samp);
-      else
-        done = march<U, D, 0>(smem, PC, own, col, row, cs, -sn, n_samp);
-    }
-    n_eval += (unsigned int)done;
   }
-  if (counting) {
+  if (exact_em) {
+    k = 0;
+    for (int c = wave; c < n_chunk; c += W) {
+      k = emitter_of_chunk(L, n_em, k, c);
+      const Emit E = uni(L.em[k]);
+      if (fast_emitter(E, mode)) continue;
+      const int i = (c - E.first) * 64 + lane;
+      if (i <= E.num_rays) {
+        ++n_exact;
+        n_eval += (unsigned int)exact_ray<U, D>(smem, E, i, PC, probe);
+      }
+    }
+  }
+  if (COUNT) {
     atomicAdd(reinterpret_cast<unsigned int*>(&L.meta[2]), n_eval);
     atomicAdd(reinterpret_cast<unsigned int*>(&L.meta[4]), n_exact);
   }
 }
 
 // Publish this tick's emitter table: thread t < n_em holds emitter t in E.  Every
-// emitter lives in wave 0 (at most 64 of them), where an exclusive lane scan of the ray
-// counts gives each emitter its first flattened ray index.
+// emitter lives in wave 0 (at most 64 of them), where an exclusive lane scan of the
+// emitters' chunk counts (ceil((num_rays + 1) / 64) chunks of 64 rays) gives each emitter
+// its first chunk index.
 static_assert(kMaxEmitters <= 64, "publish_emitters keeps every emitter in wave 0");
 __device__ __forceinline__ void publish_emitters(const EnvLds& L, Emit E, int n_em) {
   const int t = threadIdx.x;
   if (t < 64) {
-    const int cnt = t < n_em ? E.num_rays + 1 : 0;
+    const int cnt = t < n_em ? (E.num_rays + 1 + 63) / 64 : 0;
     int incl = cnt;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -430,17 +541,21 @@ __device__ __forceinline__ void raycast_pass(const EnvParams& p, unsigned char* 
     const Emit E = L.em[t];
     L.vis[L.at(E.row, E.col)] = 1;
   }
-  const bool counting = p.sample_counter || p.redo_counter;
-  if (p.probe_mode != 1 && p.probe_mode != 5) cast_rays<NT, U, D>(smem, L, counting, p.ray_mode, p.probe_mode);
+  if (p.probe_mode != 1 && p.probe_mode != 5) {
+    if (p.sample_counter || p.redo_counter)
+      cast_rays<NT, U, D, true>(smem, L, p.ray_mode, p.probe_mode);
+    else
+      cast_rays<NT, U, D, false>(smem, L, p.ray_mode, p.probe_mode);
+  }
   __syncthreads();
   if (p.sample_counter && t == 0) p.sample_counter[blockIdx.x] += (unsigned int)L.meta[2];
   if (p.redo_counter && t == 0) p.redo_counter[blockIdx.x] += (unsigned int)L.meta[4];
 }
 
-template <int NT, int U>
+template <int NT>
 __device__ __forceinline__ void clear_vis(const EnvParams& p, const EnvLds& L) {
   uint32_t* v4 = reinterpret_cast<uint32_t*>(L.vis);
-  for (int i = threadIdx.x; i < (padded_bytes(p.R, p.C, U) + 3) / 4; i += NT) v4[i] = 0u;
+  for (int i = threadIdx.x; i < (padded_bytes(p.R, p.C) + 3) / 4; i += NT) v4[i] = 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -525,7 +640,7 @@ __device__ __forceinline__ void patch4(float4& v, int m, float val) {
 // Observation row [3][R][C] (environment.py:347-374): occupancy / 5, visibility, and the
 // position channel (static plane with the solver and vault cells patched; the vault
 // wins if the solver stands on it).
-template <int NT, int U>
+template <int NT>
 __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvScalars& s, const EnvLds& L,
                                           float* __restrict__ obs) {
   const int t = threadIdx.x;
@@ -534,7 +649,8 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
   const int solver = s.pos_r * C + s.pos_c;
   const int vault = p.vr * C + p.vc;
   const float sv = 1.0f + L.plane[solver];  // == plane1[solver]: fl32(1 + g) (see heist_create)
-  if ((C & 3) == 0) {  // a float4 never crosses a row; padded vis rows are 4-byte aligned for U = 4
+  static_assert((kRing & 1) == 0, "padded vis rows of a C % 4 == 0 grid are 2-byte aligned");
+  if ((C & 3) == 0) {  // a float4 never crosses a row; 4 vis bytes in two aligned u16 reads
     const int n4 = RC / 4, c4 = C / 4;
     float4* o0 = reinterpret_cast<float4*>(o);
     float4* o1 = o0 + n4;
@@ -546,10 +662,11 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
       const int r = q / c4;
       const uint8_t* vp = L.vis + L.at(r, 4 * (q - r * c4));
       uint32_t v;
-      if ((U & 3) == 0) {
+      if ((kRing & 3) == 0) {
         v = *reinterpret_cast<const uint32_t*>(vp);
       } else {
-        v = (uint32_t)vp[0] | ((uint32_t)vp[1] << 8) | ((uint32_t)vp[2] << 16) | ((uint32_t)vp[3] << 24);
+        const uint16_t* vp2 = reinterpret_cast<const uint16_t*>(vp);
+        v = (uint32_t)vp2[0] | ((uint32_t)vp2[1] << 16);
       }
       o1[q] = make_float4((v & 0xff) ? 1.0f : 0.0f, (v & 0xff00) ? 1.0f : 0.0f, (v & 0xff0000) ? 1.0f : 0.0f,
                           (v & 0xff000000u) ? 1.0f : 0.0f);
@@ -604,16 +721,16 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   extern __shared__ __align__(16) unsigned char smem[];
   const int e = blockIdx.x;
   const int t = threadIdx.x;
-  const EnvLds L = carve<U, D>(smem, p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path);
+  const EnvLds L = carve<D>(smem, p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path, W);
   EnvScalars s = p.scal[e];
   const int n_cams = s.n_cams, n_em = s.n_cams + s.n_guards;
   EmitterRaw raw;
   prefetch<NT>(p, e, L, n_cams, n_em, raw);
   const int a_raw = (int)actions[e];
-  clear_vis<NT, U>(p, L);
+  clear_vis<NT>(p, L);
   const bool act = !s.done;
   __syncthreads();  // grid, paths in LDS
-  build_wall_map<NT, U>(L.grid, L, p.R, p.C);  // read by the raycast after its first barrier
+  build_wall_map<NT>(L.grid, L, p.R, p.C);  // read by the raycast after its first barrier
 
   double reward = 0.0;
   int status = kAlreadyDone;
@@ -703,10 +820,10 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
       E2.col = unpack_c(pos0);
     }
     publish_emitters(L, E2, n_em);
-    clear_vis<NT, U>(p, L);
+    clear_vis<NT>(p, L);
     raycast_pass<NT, U, D>(p, smem, L, n_em, n_cams);
   }
-  if (p.probe_mode < 4) write_obs<NT, U>(p, e, s, L, obs);
+  if (p.probe_mode < 4) write_obs<NT>(p, e, s, L, obs);
   if (t == 0) {
     rew[e] = (float)reward;
     if (rew64) rew64[e] = reward;
@@ -724,14 +841,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   const int e = blockIdx.x;
   const int t = threadIdx.x;
   if (mask && !mask[e]) return;
-  const EnvLds L = carve<U, D>(smem, p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path);
+  const EnvLds L = carve<D>(smem, p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path, W);
   EnvScalars s = p.scal[e];
   const int n_cams = s.n_cams, n_em = s.n_cams + s.n_guards;
   EmitterRaw raw;
   prefetch<NT>(p, e, L, n_cams, n_em, raw);
-  clear_vis<NT, U>(p, L);
+  clear_vis<NT>(p, L);
   __syncthreads();  // grid in LDS
-  build_wall_map<NT, U>(L.grid, L, p.R, p.C);
+  build_wall_map<NT>(L.grid, L, p.R, p.C);
   reset_solver(p, s);
   Emit E;
   if (t < n_cams) {
@@ -747,7 +864,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   }
   publish_emitters(L, E, n_em);
   raycast_pass<NT, U, D>(p, smem, L, n_em, n_cams);
-  write_obs<NT, U>(p, e, s, L, obs);
+  write_obs<NT>(p, e, s, L, obs);
   if (t == 0) p.scal[e] = s;
 }
 
@@ -903,9 +1020,9 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
   const int e = blockIdx.x;
   const int lane = threadIdx.x;
   const int RC = R * C;
-  const EnvLds L = carve<U, D>(smem, R, C, 1, 0);
+  const EnvLds L = carve<D>(smem, R, C, 1, 0, 1);
   for (int i = lane; i < RC; i += 64) L.grid[i] = walls[(size_t)e * RC + i] ? kWall : kEmpty;
-  for (int i = lane; i < padded_bytes(R, C, U); i += 64) L.vis[i] = 0;
+  for (int i = lane; i < padded_bytes(R, C); i += 64) L.vis[i] = 0;
   if (lane == 0) {
     const int kind = meta[e * 4], row = meta[e * 4 + 1], col = meta[e * 4 + 2], range = meta[e * 4 + 3];
     const double fov = params[e * 2], heading = params[e * 2 + 1];
@@ -920,9 +1037,9 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
     L.meta[1] = E.num_rays + 1;
   }
   __syncthreads();
-  build_wall_map<64, U>(L.grid, L, R, C);
+  build_wall_map<64>(L.grid, L, R, C);
   __syncthreads();
-  cast_rays<64, U, D>(smem, L, false, ray_mode);
+  cast_rays<64, U, D, false>(smem, L, ray_mode, 0);
   __syncthreads();
   for (int i = lane; i < RC; i += 64) {
     const int r = i / C;
@@ -984,7 +1101,7 @@ __global__ __launch_bounds__(256) void sincos_kernel(const double* __restrict__ 
 // ---------------------------------------------------------------------------
 
 static size_t env_lds(const EnvParams& p) {
-  return env_lds_bytes(p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path, p.vis_gap);
+  return env_lds_bytes(p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path, p.vis_gap, p.step_waves);
 }
 
 hipError_t launch_init(const EnvParams& p, hipStream_t st) {
@@ -1004,9 +1121,10 @@ hipError_t launch_set_layout(const EnvParams& p, int max_walls, const int32_t* w
 // (waves per env W, samples per ray chunk U, min waves per SIMD O, stop-map -> vis gap D)
 // variants; (4, 4, 1, D) is the default for either D.
 #define HEIST_ENV_VARIANTS(X) \
-  X(4, 4, 1, 1024) X(4, 4, 1, 5376) X(1, 4, 1, 1024) X(2, 4, 1, 1024) X(4, 2, 1, 1024) X(4, 4, 8, 1024)
+  X(4, 4, 1, 1024) X(4, 4, 1, 6144) X(1, 4, 1, 1024) X(2, 4, 1, 1024) X(4, 2, 1, 1024) X(4, 4, 8, 1024) \
+  X(4, 4, 8, 6144) X(2, 4, 8, 1024) X(1, 4, 8, 1024) X(2, 4, 8, 6144)
 
-int vis_gap_for(int R, int C, int U) { return padded_bytes(R, C, U) <= 1024 ? 1024 : 5376; }
+int vis_gap_for(int R, int C) { return padded_bytes(R, C) <= 1024 ? 1024 : 6144; }
 
 bool env_variant_exists(int W, int U, int O, int D) {
 #define HEIST_HAS_CASE(W_, U_, O_, D_) \
@@ -1057,12 +1175,12 @@ hipError_t launch_bfs(const int32_t* grid, int n, int R, int C, int sr, int sc, 
 
 hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
                         uint8_t* out, int ray_mode, hipStream_t st) {
-  const int D = vis_gap_for(R, C, 4);
-  const size_t lds = env_lds_bytes(R, C, 1, 0, D);
+  const int D = vis_gap_for(R, C);
+  const size_t lds = env_lds_bytes(R, C, 1, 0, D, 1);
   if (D == 1024)
     hipLaunchKernelGGL(cones_kernel<1024>, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, out, ray_mode);
   else
-    hipLaunchKernelGGL(cones_kernel<5376>, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, out, ray_mode);
+    hipLaunchKernelGGL(cones_kernel<6144>, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, out, ray_mode);
   return hipGetLastError();
 }
 

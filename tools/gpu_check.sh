@@ -25,6 +25,7 @@ for s in ${STEPS:-pytest smoke bench prof}; do
     pytestall) step pytest_gpu 900 python -m pytest tests -m gpu -q ;;
     pytestw) for w in 1 4; do HEIST_STEP_WAVES=$w step pytest_env_w$w 900 python -m pytest tests/test_gpu_env.py -x -q; done ;;
     pytestu) for o in 8; do HEIST_STEP_OCC=$o step pytest_env_o$o 900 python -m pytest tests/test_gpu_env.py -x -q; done ;;
+    pytesto8) for w in 1 2 4; do HEIST_STEP_OCC=8 HEIST_STEP_WAVES=$w step pytest_env_w${w}_o8 900 python -m pytest tests/test_gpu_env.py -x -q; done ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o heist --output-format csv -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-secondary ;;

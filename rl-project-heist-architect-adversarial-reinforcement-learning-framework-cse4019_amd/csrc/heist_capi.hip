@@ -13,6 +13,7 @@
 
 namespace heist {
 hipError_t launch_init(const EnvParams& p, hipStream_t st);
+hipError_t launch_order(const EnvParams& p, hipStream_t st);
 hipError_t launch_set_layout(const EnvParams& p, int max_walls, const int32_t* wall_rc, const int32_t* n_walls,
                              const double* cam_params, const int32_t* n_cams, const int32_t* guard_paths,
                              const int32_t* guard_meta, const double* guard_fov, const int32_t* n_guards,
@@ -185,6 +186,7 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   if (const char* m = getenv("HEIST_EXACT_RAYS")) p.ray_mode = atoi(m) ? 1 : 0;
   p.sample_counter = nullptr;
   p.redo_counter = nullptr;
+  p.stamps = nullptr;
   p.vis_gap = heist::vis_gap_for(R, C);
   if (!heist::env_variant_exists(p.step_waves, p.ray_chunk, p.step_occ, p.vis_gap)) {
     p.step_waves = 4;
@@ -202,6 +204,7 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
       sizeof(uint16_t) * n * (max_guards > 0 ? max_guards : 1) * max_path,
       sizeof(double) * htab.size(),
       sizeof(float) * planes.size(),
+      sizeof(int32_t) * n,
   };
   h->n_allocs = 0;
   for (size_t k = 0; k < sizeof(sizes) / sizeof(sizes[0]); ++k) {
@@ -222,6 +225,7 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   p.heading_tab = (const double*)h->allocs[5];
   p.plane0 = (const float*)h->allocs[6];
   p.plane1 = p.plane0 + (size_t)R * C;
+  p.order = (int32_t*)h->allocs[7];
 
   int rc = check_hip(hipMemcpy(h->allocs[5], htab.data(), sizes[5], hipMemcpyHostToDevice), "heist_create: upload");
   if (!rc) rc = check_hip(hipMemcpy(h->allocs[6], planes.data(), sizes[6], hipMemcpyHostToDevice), "heist_create: upload");
@@ -255,10 +259,12 @@ int heist_set_layout(heist_t h, int max_walls, const int32_t* wall_rc, const int
   HEIST_REQUIRE(max_walls == 0 || wall_rc, "heist_set_layout: wall_rc is null");
   HEIST_REQUIRE(h->p.max_cams == 0 || cam_params, "heist_set_layout: cam_params is null");
   HEIST_REQUIRE(h->p.max_guards == 0 || (guard_paths && guard_meta && guard_fov), "heist_set_layout: guard arrays null");
-  return check_hip(heist::launch_set_layout(h->p, max_walls, wall_rc, n_walls, cam_params, n_cams, guard_paths,
-                                            guard_meta, guard_fov, n_guards, budget, mask, valid_out,
-                                            (hipStream_t)stream),
-                   "heist_set_layout");
+  if (int rc = check_hip(heist::launch_set_layout(h->p, max_walls, wall_rc, n_walls, cam_params, n_cams, guard_paths,
+                                                   guard_meta, guard_fov, n_guards, budget, mask, valid_out,
+                                                   (hipStream_t)stream),
+                          "heist_set_layout"))
+    return rc;
+  return check_hip(heist::launch_order(h->p, (hipStream_t)stream), "heist_set_layout: order");
 }
 
 int heist_reset(heist_t h, const uint8_t* mask, float* obs_out, heist_stream_t stream) {
@@ -292,6 +298,12 @@ int heist_count_samples(heist_t h, uint64_t* counter) {
 int heist_count_redo(heist_t h, uint64_t* counter) {
   if (int rc = check_handle(h)) return rc;
   h->p.redo_counter = reinterpret_cast<unsigned long long*>(counter);
+  return 0;
+}
+
+int heist_step_stamps(heist_t h, uint64_t* buf) {
+  if (int rc = check_handle(h)) return rc;
+  h->p.stamps = reinterpret_cast<unsigned long long*>(buf);
   return 0;
 }
 

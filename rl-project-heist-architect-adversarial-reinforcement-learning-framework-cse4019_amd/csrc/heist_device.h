@@ -80,6 +80,8 @@ struct EnvParams {
   int vis_gap;                // LDS distance stop map -> vis plane (1024 or 6144), see heist_env.hip
   unsigned long long* sample_counter;  // optional [n_envs]: ray samples evaluated per env, else null
   unsigned long long* redo_counter;    // optional [n_envs]: rays re-cast on the exact fp64 path, else null
+  int32_t* order;              // [n_envs] env of step/reset block b: heaviest raycast first (order_kernel)
+  unsigned long long* stamps;          // optional [n_envs][waves][8]: step-kernel phase stamps (s_memtime), else null
   int ray_mode;               // 0: fp32 fast path with exact fp64 re-cast of near-tie rays; 1: exact fp64 only
   int probe_mode;             // profiling only (HEIST_PROBE_MODE): 0 normal, 1 no rays, 2 angles+sin/cos only,
                               // 3 marches with a fixed direction (no sin/cos), 4 no observation write,

@@ -27,7 +27,12 @@ __device__ __forceinline__ int unpack_r(uint16_t v) { return v & 0xff; }
 __device__ __forceinline__ int unpack_c(uint16_t v) { return v >> 8; }
 
 // Python float % 360.0 (floatobject.c float_rem: remainder takes the divisor's sign).
+// Headings advance by a positive speed below 360, so x lies in [0, 720) almost always:
+// there fmod is x or x - 360, and x - 360 is exact (Sterbenz: 360 <= x < 720), so the
+// shortcut returns fmod's value without the library's reduction loop; -0.0 -> +0.0 as
+// Python does.
 __device__ __forceinline__ double py_mod360(double x) {
+  if (x > 0.0 && x < 720.0) return x >= 360.0 ? x - 360.0 : x;
   double r = fmod(x, 360.0);
   if (r != 0.0) {
     if (r < 0.0) r += 360.0;
@@ -97,8 +102,11 @@ __device__ __forceinline__ EnvLds carve(unsigned char* smem, int R, int C, int n
 template <int NT>
 __device__ __forceinline__ void build_wall_map(const uint8_t* g, const EnvLds& L, int R, int C) {
   const int PC = L.PC;
+  // i / PC as a multiply-shift: with m = ceil(2^20 / PC) the quotient is exact for
+  // i < 2^20 / (m * PC - 2^20), i.e. every i < 2^20 / 75 > 76 * 76 (PC <= 76)
+  const uint32_t m = ((1u << 20) + (uint32_t)PC - 1u) / (uint32_t)PC;
   for (int i = threadIdx.x; i < (R + 2 * kRing) * PC; i += NT) {
-    const int pr = i / PC;
+    const int pr = (int)(((uint32_t)i * m) >> 20);
     const int r = pr - kRing, c = i - pr * PC - kRing;
     const bool out = (unsigned)r >= (unsigned)R || (unsigned)c >= (unsigned)C;
     L.wall[i] = out ? 1 : (g[r * C + c] == kWall ? 1 : 0);
@@ -533,7 +541,7 @@ __device__ __forceinline__ Emit guard_emit(const Guard& gd) {
 
 // Visibility (visibility.py:31-65) once the emitter table is in LDS and vis is zeroed.
 template <int NT, int U, int D>
-__device__ __forceinline__ void raycast_pass(const EnvParams& p, unsigned char* smem, const EnvLds& L, int n_em,
+__device__ __forceinline__ void raycast_pass(const EnvParams& p, int e, unsigned char* smem, const EnvLds& L, int n_em,
                                              int n_cams) {
   __syncthreads();  // emitter table, stop map and cleared vis in place
   const int t = threadIdx.x;
@@ -548,8 +556,8 @@ __device__ __forceinline__ void raycast_pass(const EnvParams& p, unsigned char* 
       cast_rays<NT, U, D, false>(smem, L, p.ray_mode, p.probe_mode);
   }
   __syncthreads();
-  if (p.sample_counter && t == 0) p.sample_counter[blockIdx.x] += (unsigned int)L.meta[2];
-  if (p.redo_counter && t == 0) p.redo_counter[blockIdx.x] += (unsigned int)L.meta[4];
+  if (p.sample_counter && t == 0) p.sample_counter[e] += (unsigned int)L.meta[2];
+  if (p.redo_counter && t == 0) p.redo_counter[e] += (unsigned int)L.meta[4];
 }
 
 template <int NT>
@@ -712,15 +720,31 @@ __device__ __forceinline__ double guard_heading_after(const EnvParams& p, int dr
 // step / reset
 // ---------------------------------------------------------------------------
 
-template <int W, int U, int O, int D>
+// Phase stamps (instrumentation, heist_step_stamps): lane 0 of every wave records the
+// shader clock at phase boundaries k = 0..7 into stamps[env][wave][k] (10 slots per wave).
+// Slot 8 holds HW_ID (CU / SIMD / SE of the wave) and slot 9 XCC_ID, so that clocks are
+// compared per CU (the counter is not synchronised across CUs).
+#define HEIST_STEP_STAMP(k)                                                                    \
+  do {                                                                                         \
+    if (STAMP && (threadIdx.x & 63) == 0)                                                      \
+      p.stamps[((size_t)e * W + (threadIdx.x >> 6)) * 10 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+
+template <int W, int U, int O, int D, bool STAMP>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) void step_kernel(EnvParams p, const int64_t* __restrict__ actions,
                                                        float* __restrict__ obs, float* __restrict__ rew,
                                                        double* __restrict__ rew64, uint8_t* __restrict__ done_out,
                                                        int8_t* __restrict__ status_out, int auto_reset) {
   constexpr int NT = 64 * W;
   extern __shared__ __align__(16) unsigned char smem[];
-  const int e = blockIdx.x;
+  const int e = p.order[blockIdx.x];
   const int t = threadIdx.x;
+  HEIST_STEP_STAMP(0);
+  if (STAMP && (t & 63) == 0) {
+    unsigned long long* q = p.stamps + ((size_t)e * W + (t >> 6)) * 10;
+    q[8] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+    q[9] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+  }
   const EnvLds L = carve<D>(smem, p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path, W);
   EnvScalars s = p.scal[e];
   const int n_cams = s.n_cams, n_em = s.n_cams + s.n_guards;
@@ -730,6 +754,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   clear_vis<NT>(p, L);
   const bool act = !s.done;
   __syncthreads();  // grid, paths in LDS
+  HEIST_STEP_STAMP(1);
   build_wall_map<NT>(L.grid, L, p.R, p.C);  // read by the raycast after its first barrier
 
   double reward = 0.0;
@@ -774,8 +799,10 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     E = guard_emit(gd);
   }
   publish_emitters(L, E, n_em);
+  HEIST_STEP_STAMP(2);
   // 3. visibility (environment.py:257-258); an already-done env recomputes the same plane
-  raycast_pass<NT, U, D>(p, smem, L, n_em, n_cams);
+  raycast_pass<NT, U, D>(p, e, smem, L, n_em, n_cams);
+  HEIST_STEP_STAMP(3);
 
   if (act) {
     // 4-5. shaping, detection, vault, timeout (environment.py:235, :261-297)
@@ -807,6 +834,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     }
   }
   const int done_now = s.done;
+  HEIST_STEP_STAMP(4);
   if (auto_reset && done_now) {  // block-uniform: the barriers inside are safe
     __syncthreads();  // every wave has read vis (detection) before it is cleared
     reset_solver(p, s);
@@ -821,9 +849,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     }
     publish_emitters(L, E2, n_em);
     clear_vis<NT>(p, L);
-    raycast_pass<NT, U, D>(p, smem, L, n_em, n_cams);
+    raycast_pass<NT, U, D>(p, e, smem, L, n_em, n_cams);
   }
+  HEIST_STEP_STAMP(5);
   if (p.probe_mode < 4) write_obs<NT>(p, e, s, L, obs);
+  HEIST_STEP_STAMP(6);
   if (t == 0) {
     rew[e] = (float)reward;
     if (rew64) rew64[e] = reward;
@@ -831,6 +861,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     status_out[e] = (int8_t)status;
     p.scal[e] = s;
   }
+  HEIST_STEP_STAMP(7);
 }
 
 template <int W, int U, int O, int D>
@@ -838,7 +869,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
                                                         float* __restrict__ obs) {
   constexpr int NT = 64 * W;
   extern __shared__ __align__(16) unsigned char smem[];
-  const int e = blockIdx.x;
+  const int e = p.order[blockIdx.x];
   const int t = threadIdx.x;
   if (mask && !mask[e]) return;
   const EnvLds L = carve<D>(smem, p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path, W);
@@ -863,7 +894,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     E = guard_emit(gd);
   }
   publish_emitters(L, E, n_em);
-  raycast_pass<NT, U, D>(p, smem, L, n_em, n_cams);
+  raycast_pass<NT, U, D>(p, e, smem, L, n_em, n_cams);
   write_obs<NT>(p, e, s, L, obs);
   if (t == 0) p.scal[e] = s;
 }
@@ -1050,6 +1081,7 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
 __global__ void init_kernel(EnvParams p) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= p.n_envs) return;
+  p.order[e] = e;
   EnvScalars s;
   s.pos_r = p.sr; s.pos_c = p.sc; s.tick = 0; s.done = 0; s.detected = 0; s.vault_reached = 0;
   s.prev_dist = s.initial_dist = iabs_(p.sr - p.vr) + iabs_(p.sc - p.vc);
@@ -1104,6 +1136,50 @@ static size_t env_lds(const EnvParams& p) {
   return env_lds_bytes(p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path, p.vis_gap, p.step_waves);
 }
 
+// Block -> env dispatch order for step/reset (longest-processing-time first): envs sorted
+// by a raycast cost estimate, sum over emitters of (num_rays + 1) * samples per ray, in
+// descending 1024-bucket counting-sort order.  The workgroup dispatcher hands out blocks
+// in index order, so the heaviest envs start in the first round and the light ones fill
+// the tail.  Results do not depend on the order (envs are independent); the order within
+// a bucket is whatever the LDS atomics produce.  One workgroup; runs once per set_layout.
+__global__ __launch_bounds__(1024) void order_kernel(EnvParams p) {
+  __shared__ int bucket[1024];
+  const int t = threadIdx.x;
+  bucket[t] = 0;
+  __syncthreads();
+  auto key = [&](int e) {
+    const EnvScalars& s = p.scal[e];
+    int cost = 0;
+    for (int c = 0; c < s.n_cams; ++c) {
+      const Cam& cm = p.cams[(size_t)e * p.max_cams + c];
+      cost += (cm.num_rays + 1) * 2 * cm.range;
+    }
+    for (int g = 0; g < s.n_guards; ++g) {
+      const Guard& gd = p.guards[(size_t)e * p.max_guards + g];
+      cost += (gd.num_rays + 1) * gd.range;
+    }
+    const int b = cost >> 5;
+    return 1023 - (b < 1023 ? b : 1023);  // descending cost
+  };
+  for (int e = t; e < p.n_envs; e += 1024) atomicAdd(&bucket[key(e)], 1);
+  __syncthreads();
+  if (t == 0) {
+    int run = 0;
+    for (int b = 0; b < 1024; ++b) {
+      const int c = bucket[b];
+      bucket[b] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (int e = t; e < p.n_envs; e += 1024) p.order[atomicAdd(&bucket[key(e)], 1)] = e;
+}
+
+hipError_t launch_order(const EnvParams& p, hipStream_t st) {
+  hipLaunchKernelGGL(order_kernel, dim3(1), dim3(1024), 0, st, p);
+  return hipGetLastError();
+}
+
 hipError_t launch_init(const EnvParams& p, hipStream_t st) {
   hipLaunchKernelGGL(init_kernel, dim3((p.n_envs + 255) / 256), dim3(256), 0, st, p);
   return hipGetLastError();
@@ -1151,8 +1227,12 @@ hipError_t launch_step(const EnvParams& p, const int64_t* actions, float* obs, f
   const size_t lds = env_lds(p);
 #define HEIST_STEP_CASE(W, U, O, D)                                                                       \
   if (p.step_waves == W && p.ray_chunk == U && p.step_occ == O && p.vis_gap == D) {                      \
-    hipLaunchKernelGGL((step_kernel<W, U, O, D>), dim3(p.n_envs), dim3(64 * W), lds, st, p, actions, obs, \
-                       rew, rew64, done_out, status_out, auto_reset);                                    \
+    if (p.stamps)                                                                                        \
+      hipLaunchKernelGGL((step_kernel<W, U, O, D, true>), dim3(p.n_envs), dim3(64 * W), lds, st, p, actions, \
+                         obs, rew, rew64, done_out, status_out, auto_reset);                             \
+    else                                                                                                 \
+      hipLaunchKernelGGL((step_kernel<W, U, O, D, false>), dim3(p.n_envs), dim3(64 * W), lds, st, p, actions, \
+                         obs, rew, rew64, done_out, status_out, auto_reset);                             \
     return hipGetLastError();                                                                            \
   }
   HEIST_ENV_VARIANTS(HEIST_STEP_CASE)

@@ -36,6 +36,7 @@ for s in ${STEPS:-pytest smoke bench prof}; do
     pprobe) step probe_policy 600 python tools/probe_policy.py ;;
     tprobe) step probe_train 600 python tools/probe_train.py ;;
     pstamp) PROBE_STAMPS=1 step policy_stamps 300 python tools/probe_policy.py ;;
+    sstamp) step step_stamps 300 python tools/probe_step_stamps.py ;;
     uprobe) step probe_update 600 python tools/probe_update.py ;;
     mprobe) step probe_modes 600 python tools/probe_step_modes.py ;;
     vprobe) step probe_variants 600 python tools/probe_step_variants.py ;;

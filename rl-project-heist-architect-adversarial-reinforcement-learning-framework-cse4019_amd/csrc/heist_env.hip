@@ -203,7 +203,20 @@ __device__ __forceinline__ int march(unsigned char* smem, int PC, int own, doubl
 // a 27721-bit table; a ray is re-cast on the exact path (glibc sin/cos restatement + fp64
 // march) when |t - rint(t)| < kTieRad = E*L + (fp32 error of t) and rint(t) is a tie
 // point.  Emitters with range > 6 (K > 12) always take the exact path.
+//
+// The tie point 1 (|d| = 1, an axis-aligned ray) is screened differently: there the
+// direction is flat in the angle, so |d| within E of 1 covers an angle window of +-1.5e-3
+// rad around every multiple of 90 degrees (most of all re-casts), yet only a far smaller
+// window matters.  With x the angle's remainder from the nearest multiple of 90 degrees,
+// the exact |d| is 1 - delta, delta ~ x^2/2.  For |x| >= kAxisRad = 1e-6 rad, delta >=
+// 5e-13 keeps every fp64 col + (d/2)*k (k <= 12, |col| < 64) strictly below its .5 tie,
+// i.e. fp64 rounds as the real numbers do, and so does the fast path once an fp32 |d|
+// that rounded to 1.0f is replaced by 1 - 2^-24 (the same side of the tie point; the next
+// one, 11/12, is far).  Rays with |x| < kAxisRad take the exact path.  Guard rays (whole
+// tiles) have no tie at |d| = 1, and the replacement leaves their samples unchanged.
 constexpr float kDirErr = 1e-6f;
+constexpr float kAxisRad = 1e-6f;
+constexpr float kBelowOne = 0.99999994f;  // 1 - 2^-24
 constexpr int kTieMaxRange = 6;
 static_assert(kRing >= kTieMaxRange, "march_fast reads every sample of a ray unconditionally");
 constexpr int kTieL = 27720;                                  // lcm(1, ..., 12)
@@ -219,6 +232,7 @@ constexpr TieBits make_tie_bits() {
       const int n = j * (kTieL / k);
       t.w[n >> 5] |= 1u << (n & 31);
     }
+  t.w[kTieL >> 5] &= ~(1u << (kTieL & 31));  // |d| = 1 is screened by kAxisRad instead
   return t;
 }
 __constant__ TieBits kTieBits = make_tie_bits();
@@ -229,8 +243,8 @@ constexpr float kMagic32 = 12582912.0f;
 
 // cos and sin of a (degrees) in fp32: q = rint(a / 90) in fp64, the octant remainder
 // (|r| <= 45 deg) to fp32 radians, Cephes sinf/cosf minimax polynomials on [-pi/4, pi/4],
-// then the quadrant rotation.
-__device__ __forceinline__ void fast_dir(double a, float* cs, float* sn) {
+// then the quadrant rotation.  *xr = the remainder in radians (for the axis screen).
+__device__ __forceinline__ void fast_dir(double a, float* cs, float* sn, float* xr) {
   const double q = __builtin_rint(a * (1.0 / 90.0));
   const float x = (float)(__builtin_fma(-90.0, q, a) * kDegToRad);
   const float z = x * x;
@@ -244,12 +258,19 @@ __device__ __forceinline__ void fast_dir(double a, float* cs, float* sn) {
   const float c0 = (n & 1) ? s : c;  // cos(a) up to sign
   *sn = (n & 2) ? -s0 : s0;
   *cs = ((n + 1) & 2) ? -c0 : c0;
+  *xr = x;
 }
 
-// true if |c| or |s| lies within kTieRad / L of a tie point (the ray needs the exact path).
+// |d| that rounded to 1.0f in fp32 -> 1 - 2^-24 with its sign (see kAxisRad).
+__device__ __forceinline__ float below_one(float d) {
+  return __builtin_fabsf(d) == 1.0f ? __builtin_copysignf(kBelowOne, d) : d;
+}
+
+// true if |c| or |s| lies within kTieRad / L of a tie point below 1, or a camera ray is
+// within kAxisRad of an axis (the ray needs the exact path).
 // Scalar code on purpose: the float2 form of this function is miscompiled by the ROCm 7.2
 // clang (the two table lookups are merged into one).
-__device__ __forceinline__ bool near_tie(float c, float s) {
+__device__ __forceinline__ bool near_tie(float c, float s, float x, bool camera) {
   const float tx = __builtin_fabsf(c) * (float)kTieL, ty = __builtin_fabsf(s) * (float)kTieL;
   const float mx = tx + kMagic32, my = ty + kMagic32;
   const uint32_t nx = __builtin_bit_cast(uint32_t, mx) - 0x4B400000u;
@@ -257,7 +278,8 @@ __device__ __forceinline__ bool near_tie(float c, float s) {
   const uint32_t wx = kTieBits.w[nx >> 5], wy = kTieBits.w[ny >> 5];
   const bool cx = __builtin_fabsf(tx - (mx - kMagic32)) < kTieRad;
   const bool cy = __builtin_fabsf(ty - (my - kMagic32)) < kTieRad;
-  return (((wx >> (nx & 31)) & (uint32_t)cx) | ((wy >> (ny & 31)) & (uint32_t)cy)) & 1u;
+  return ((((wx >> (nx & 31)) & (uint32_t)cx) | ((wy >> (ny & 31)) & (uint32_t)cy)) & 1u) ||
+         (camera && __builtin_fabsf(x) < kAxisRad);
 }
 
 // LDS byte at an absolute LDS address (the dynamic LDS base is folded into the address
@@ -412,8 +434,8 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
     }
     const int i = (c - E.first) * 64 + lane;
     const bool active = i <= E.num_rays;  // rays 0 .. num_rays (security.py:68)
-    float cf, sf;
-    fast_dir(__builtin_fma((double)i, E.step, E.hmh), &cf, &sf);
+    float cf, sf, xr;
+    fast_dir(__builtin_fma((double)i, E.step, E.hmh), &cf, &sf, &xr);
     if (probe == 2) {  // profiling: angles and sin/cos only
       if (sf == 12345.0f && cf == 0.0f) L.meta[3] = 1;  // keeps the sin/cos live
       continue;
@@ -422,7 +444,7 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
       sf = 0.3f + 1e-3f * (float)i;
       cf = 0.7f;
     }
-    const bool tie = active && probe != 3 && near_tie(cf, sf);
+    const bool tie = active && probe != 3 && near_tie(cf, sf, xr, E.kind == 0);
     const unsigned long long b = __ballot(tie);
     if (tie) {
       const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
@@ -434,7 +456,7 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
       const int n_samp = E.kind == 0 ? 2 * E.range : E.range;
       const float mx = kMagic32 + (float)(E.col + kRing), my = kMagic32 + (float)(E.row + kRing);
       const float h = E.kind == 0 ? 0.5f : 1.0f;  // sample stride: camera half tiles, guard whole tiles
-      const float dxs = cf * h, dys = -sf * h;     // exact scalings; dy = -sin (security.py:72-75)
+      const float dxs = below_one(cf) * h, dys = -below_one(sf) * h;  // exact scalings; dy = -sin (security.py:72-75)
       int done;
       if (n_samp == 2 * kTieMaxRange)  // the reference cameras (range 6)
         done = march_fast<D, 2 * kTieMaxRange, false, COUNT>(PC, own, dummy, dxs, dys, mx, my, kofs, n_samp);
@@ -464,9 +486,9 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
       const Emit E = uni(L.em[k]);
       if (!fast_emitter(E, mode)) continue;
       const int i = (c - E.first) * 64 + lane;
-      float cf, sf;
-      fast_dir(__builtin_fma((double)i, E.step, E.hmh), &cf, &sf);
-      if (i <= E.num_rays && near_tie(cf, sf)) {
+      float cf, sf, xr;
+      fast_dir(__builtin_fma((double)i, E.step, E.hmh), &cf, &sf, &xr);
+      if (i <= E.num_rays && near_tie(cf, sf, xr, E.kind == 0)) {
         ++n_exact;
         n_eval += (unsigned int)exact_ray<U, D>(smem, E, i, PC, probe);
       }
@@ -1267,7 +1289,10 @@ hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t
 __global__ __launch_bounds__(256) void fast_dir_kernel(const double* __restrict__ deg, int64_t n,
                                                        float* __restrict__ co, float* __restrict__ so) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    fast_dir(deg[i], co + i, so + i);
+  {
+    float xr;
+    fast_dir(deg[i], co + i, so + i, &xr);
+  }
 }
 
 hipError_t launch_fast_dir(const double* deg, int64_t n, float* co, float* so, hipStream_t st) {

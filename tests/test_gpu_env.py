@@ -268,6 +268,12 @@ def test_cones_fast_equals_exact(R, C, gpu_device):
     head = np.select([rng.random(n) < 0.3, rng.random(n) < 0.5],
                      [rng.integers(0, 72, n) * 5.0, rng.integers(0, 720, n) * 0.5],
                      rng.uniform(0.0, 360.0, n).astype(np.float32).astype(np.float64))
+    # axis-grazing rays: fov 60 puts ray 60 of 120 exactly on the heading, which sits within
+    # 1e-12 .. 1e-2 degrees of a multiple of 90 (cos or sin within ~1e-20 .. 1e-8 of +-1)
+    graze = rng.random(n) < 0.25
+    tiny = 10.0 ** rng.uniform(-12, -2, n) * rng.choice([-1.0, 1.0], n)
+    head = np.where(graze, rng.integers(0, 5, n) * 90.0 + tiny, head)
+    fov = np.where(graze, 60.0, fov)
     walls[np.arange(n), row, col] = 0
     dev = gpu_device
     wt = torch.tensor(walls, device=dev)

@@ -62,7 +62,7 @@ using heist::EnvParams;
 struct heist_env {
   int device;
   EnvParams p;
-  void* allocs[8];
+  void* allocs[12];
   int n_allocs;
 };
 
@@ -205,6 +205,7 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
       sizeof(double) * htab.size(),
       sizeof(float) * planes.size(),
       sizeof(int32_t) * n,
+      sizeof(double) * 3 * heist::kHalfDegN,  // [sin | cos | staging radians]
   };
   h->n_allocs = 0;
   for (size_t k = 0; k < sizeof(sizes) / sizeof(sizes[0]); ++k) {
@@ -226,12 +227,22 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   p.plane0 = (const float*)h->allocs[6];
   p.plane1 = p.plane0 + (size_t)R * C;
   p.order = (int32_t*)h->allocs[7];
+  p.half_deg = (const double*)h->allocs[8];
+  std::vector<double> hrad(heist::kHalfDegN);
+  for (int m = 0; m < heist::kHalfDegN; ++m) hrad[m] = (0.5 * (m - heist::kHalfDegN / 2)) * heist::kDegToRad;
 
   int rc = check_hip(hipMemcpy(h->allocs[5], htab.data(), sizes[5], hipMemcpyHostToDevice), "heist_create: upload");
   if (!rc) rc = check_hip(hipMemcpy(h->allocs[6], planes.data(), sizes[6], hipMemcpyHostToDevice), "heist_create: upload");
   if (!rc) rc = check_hip(hipMemset(h->allocs[2], 0, sizes[2]), "heist_create: memset");
   if (!rc) rc = check_hip(hipMemset(h->allocs[3], 0, sizes[3]), "heist_create: memset");
   if (!rc) rc = check_hip(hipMemset(h->allocs[4], 0, sizes[4]), "heist_create: memset");
+  if (!rc) rc = check_hip(hipMemcpy((double*)h->allocs[8] + 2 * heist::kHalfDegN, hrad.data(),
+                                    sizeof(double) * heist::kHalfDegN, hipMemcpyHostToDevice), "heist_create: upload");
+  if (!rc) {
+    double* hd = (double*)h->allocs[8];
+    rc = check_hip(heist::launch_sincos(hd + 2 * heist::kHalfDegN, heist::kHalfDegN, hd, hd + heist::kHalfDegN, nullptr),
+                   "heist_create: half-degree table");
+  }
   if (!rc) rc = check_hip(heist::launch_init(p, nullptr), "heist_create: init");
   if (!rc) rc = check_hip(hipDeviceSynchronize(), "heist_create: init");
   if (rc) {

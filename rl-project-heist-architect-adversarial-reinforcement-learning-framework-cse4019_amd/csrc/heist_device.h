@@ -20,6 +20,7 @@ enum : int { kRunning = 0, kDetected = 1, kVaultReached = 2, kTimeout = 3, kAlre
 constexpr int kMaxDim = 64;          // R, C <= 64
 constexpr int kMaxEmitters = 64;     // max_cams + max_guards per env
 constexpr double kDegToRad = 3.141592653589793 / 180.0;  // CPython math.radians factor
+constexpr int kHalfDegN = 2880;      // half-degree sin/cos table: angles -720 .. 719.5
 
 struct EnvScalars {
   int32_t pos_r, pos_c, tick, done;
@@ -80,6 +81,7 @@ struct EnvParams {
   int vis_gap;                // LDS distance stop map -> vis plane (1024 or 6144), see heist_env.hip
   unsigned long long* sample_counter;  // optional [n_envs]: ray samples evaluated per env, else null
   unsigned long long* redo_counter;    // optional [n_envs]: rays re-cast on the exact fp64 path, else null
+  const double* half_deg;      // [2][kHalfDegN] glibc-exact sin, cos of m/2 degrees (m = -1440 .. 1439)
   int32_t* order;              // [n_envs] env of step/reset block b: heaviest raycast first (order_kernel)
   unsigned long long* stamps;          // optional [n_envs][waves][8]: step-kernel phase stamps (s_memtime), else null
   int ray_mode;               // 0: fp32 fast path with exact fp64 re-cast of near-tie rays; 1: exact fp64 only

@@ -330,15 +330,24 @@ __device__ __forceinline__ int march_fast(uint32_t PC, uint32_t own, uint32_t du
 
 // One ray on the exact path: security.py:70 angle, glibc-exact sin/cos, fp64 march.
 // Returns the ray's sample count (march).
+// A ray angle that is a whole number of half degrees (guards after an axis move; the
+// reference's default cameras: heading 0, fov 60, speed 15) reads the same glibc-exact
+// sin/cos from hd (computed by heist_trig::sincos at heist_create) instead of evaluating it.
 template <int U, int D>
-__device__ __forceinline__ int exact_ray(unsigned char* smem, const Emit& E, int i, int PC, int probe) {
+__device__ __forceinline__ int exact_ray(unsigned char* smem, const Emit& E, int i, int PC, int probe,
+                                         const double* hd) {
   const double angle = E.hmh + (E.fov * (double)i) / (double)E.num_rays;  // security.py:70
-  const double rad = angle * kDegToRad;                                   // math.radians
   double sn, cs;
+  const double a2 = angle * 2.0;  // exact
   if (probe == 3) {  // profiling: fixed direction, no sin/cos
     sn = 0.3 + 1e-3 * (double)i;
     cs = 0.7;
+  } else if (hd && a2 == __builtin_rint(a2) && a2 >= -0.5 * kHalfDegN && a2 < 0.5 * kHalfDegN) {
+    const int m = (int)a2 + kHalfDegN / 2;
+    sn = hd[m];
+    cs = hd[kHalfDegN + m];
   } else {
+    const double rad = angle * kDegToRad;  // math.radians
     heist_trig::sincos(rad, kSinCosTab, &sn, &cs);
   }
   const int own = (E.row + kRing) * PC + (E.col + kRing);
@@ -403,7 +412,7 @@ __device__ __forceinline__ int emitter_of_chunk(const EnvLds& L, int n_em, int k
 // to the one that ends each ray) are summed in LDS meta[2] and exact casts in meta[4] (the
 // ALU work figures of SURVEY 8(d)); raycast_pass adds the env's totals to its counters.
 template <int NT, int U, int D, bool COUNT>
-__device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int probe) {
+__device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int probe, const double* hd) {
   static_assert(U == 2 || U == 4, "exact-path chunk");
   static_assert(kRing >= U, "the exact path's chunks stay inside the ring");
   constexpr int W = NT / 64;
@@ -477,7 +486,7 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
       const int v = queue[lane];
       const Emit E = L.em[v >> 16];
       ++n_exact;
-      n_eval += (unsigned int)exact_ray<U, D>(smem, E, v & 0xffff, PC, probe);
+      n_eval += (unsigned int)exact_ray<U, D>(smem, E, v & 0xffff, PC, probe, hd);
     }
   } else {
     k = 0;
@@ -490,7 +499,7 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
       fast_dir(__builtin_fma((double)i, E.step, E.hmh), &cf, &sf, &xr);
       if (i <= E.num_rays && near_tie(cf, sf, xr, E.kind == 0)) {
         ++n_exact;
-        n_eval += (unsigned int)exact_ray<U, D>(smem, E, i, PC, probe);
+        n_eval += (unsigned int)exact_ray<U, D>(smem, E, i, PC, probe, hd);
       }
     }
   }
@@ -503,7 +512,7 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
       const int i = (c - E.first) * 64 + lane;
       if (i <= E.num_rays) {
         ++n_exact;
-        n_eval += (unsigned int)exact_ray<U, D>(smem, E, i, PC, probe);
+        n_eval += (unsigned int)exact_ray<U, D>(smem, E, i, PC, probe, hd);
       }
     }
   }
@@ -573,9 +582,9 @@ __device__ __forceinline__ void raycast_pass(const EnvParams& p, int e, unsigned
   }
   if (p.probe_mode != 1 && p.probe_mode != 5) {
     if (p.sample_counter || p.redo_counter)
-      cast_rays<NT, U, D, true>(smem, L, p.ray_mode, p.probe_mode);
+      cast_rays<NT, U, D, true>(smem, L, p.ray_mode, p.probe_mode, p.half_deg);
     else
-      cast_rays<NT, U, D, false>(smem, L, p.ray_mode, p.probe_mode);
+      cast_rays<NT, U, D, false>(smem, L, p.ray_mode, p.probe_mode, p.half_deg);
   }
   __syncthreads();
   if (p.sample_counter && t == 0) p.sample_counter[e] += (unsigned int)L.meta[2];
@@ -1092,7 +1101,7 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
   __syncthreads();
   build_wall_map<64>(L.grid, L, R, C);
   __syncthreads();
-  cast_rays<64, U, D, false>(smem, L, ray_mode, 0);
+  cast_rays<64, U, D, false>(smem, L, ray_mode, 0, nullptr);
   __syncthreads();
   for (int i = lane; i < RC; i += 64) {
     const int r = i / C;

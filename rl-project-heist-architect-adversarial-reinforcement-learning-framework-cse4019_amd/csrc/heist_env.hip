@@ -555,7 +555,7 @@ __device__ __forceinline__ Emit cam_emit(const Cam& cm) {
   E.hmh = cm.heading - cm.fov / 2.0;  // security.py:64, :70
   E.fov = cm.fov;
   E.row = cm.row; E.col = cm.col; E.range = cm.range; E.num_rays = cm.num_rays;
-  E.step = cm.fov / (double)cm.num_rays;
+  E.step = cm.fov * __builtin_amdgcn_rcp((double)cm.num_rays);  // fast-path angles only: approximate
   E.first = 0; E.kind = 0;
   return E;
 }
@@ -565,7 +565,7 @@ __device__ __forceinline__ Emit guard_emit(const Guard& gd) {
   E.hmh = gd.heading - gd.fov / 2.0;
   E.fov = gd.fov;
   E.row = unpack_r(gd.pos); E.col = unpack_c(gd.pos); E.range = gd.range; E.num_rays = gd.num_rays;
-  E.step = gd.fov / (double)gd.num_rays;
+  E.step = gd.fov * __builtin_amdgcn_rcp((double)gd.num_rays);
   E.first = 0; E.kind = 1;
   return E;
 }
@@ -802,6 +802,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   }
   // 2. cameras rotate, guards patrol (security.py:49-51, :145-159) -- in registers
   uint16_t pos0 = 0;  // a guard thread's patrol start, for the auto-reset below
+  bool off_start = false;  // a guard thread's guard stands off its patrol start
   Emit E;
   if (t < n_cams) {
     Cam cm = as_cam(raw);
@@ -827,6 +828,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
       gp->idx = gd.idx;
       gp->pos = gd.pos;
     }
+    off_start = gd.pos != pos0;
     E = guard_emit(gd);
   }
   publish_emitters(L, E, n_em);
@@ -867,20 +869,28 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   const int done_now = s.done;
   HEIST_STEP_STAMP(4);
   if (auto_reset && done_now) {  // block-uniform: the barriers inside are safe
-    __syncthreads();  // every wave has read vis (detection) before it is cleared
+    // The reset keeps every heading (environment.py:204-208) and moves only the guards
+    // back to patrol point 0, so its visibility is this tick's unless a guard stands
+    // elsewhere.  The barrier also orders every wave's detection read before a clear.
+    const bool is_guard = t >= n_cams && t < n_em;
+    const int any_moved = __syncthreads_or(off_start);
     reset_solver(p, s);
-    Emit E2;
-    if (t < n_em) E2 = L.em[t];  // this tick's headings, fov and range stay
-    if (t >= n_cams && t < n_em) {  // guards back to patrol point 0, headings carry over (environment.py:204-208)
+    if (is_guard) {
       Guard* gp = p.guards + (size_t)e * p.max_guards + (t - n_cams);
       gp->idx = 0;
       gp->pos = pos0;
-      E2.row = unpack_r(pos0);
-      E2.col = unpack_c(pos0);
     }
-    publish_emitters(L, E2, n_em);
-    clear_vis<NT>(p, L);
-    raycast_pass<NT, U, D>(p, e, smem, L, n_em, n_cams);
+    if (any_moved) {
+      Emit E2;
+      if (t < n_em) E2 = L.em[t];  // this tick's headings, fov and range stay
+      if (is_guard) {
+        E2.row = unpack_r(pos0);
+        E2.col = unpack_c(pos0);
+      }
+      publish_emitters(L, E2, n_em);
+      clear_vis<NT>(p, L);
+      raycast_pass<NT, U, D>(p, e, smem, L, n_em, n_cams);
+    }
   }
   HEIST_STEP_STAMP(5);
   if (p.probe_mode < 4) write_obs<NT>(p, e, s, L, obs);
@@ -1096,7 +1106,7 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
     E.first = 0; E.kind = kind;
     L.em[0] = E;
     L.meta[0] = 1;
-    L.meta[1] = E.num_rays + 1;
+    L.meta[1] = (E.num_rays + 1 + 63) / 64;  // 64-ray chunks (publish_emitters)
   }
   __syncthreads();
   build_wall_map<64>(L.grid, L, R, C);

@@ -250,7 +250,9 @@ def main():
             "cpu_baseline": None,
         }
         log("env-only: %.1f M env-steps/s, step kernel %.1f us" % (value / 1e6, kern_ms * 1e3))
-        if not args.no_secondary:
+        # single-GPU figures: the secondary numbers and the CPU baseline run on rank 0 at N=1
+        # only (at N>1 the other ranks would idle at the closing barrier meanwhile)
+        if not args.no_secondary and world == 1:
             sec = {}
             log("rollout")
             sec["rollout"] = measure_rollout(env, dev)
@@ -261,7 +263,7 @@ def main():
             log("full train (bf16 update)")
             sec["full_train_bf16_update"] = measure_train(cfg, dev, N, update_precision="bf16")
             line["secondary"] = sec
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:
             log("cpu baseline")
             line["cpu_baseline"] = cpu_baseline(layouts, cfg, args.budget, target_s=args.cpu_seconds, threads=1)
         print(json.dumps(line), flush=True)

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Final round-1 GPU session: GPU parity suite, smoke, default bench, rocprof kernel stats, PMC traffic passes.
+cd "${GRAFT_REPO_ROOT:-.}" || exit 1
+OUT=gpurun_out/r01z
+mkdir -p $OUT
+export TMPDIR=/tmp
+fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+run() { local name=$1 secs=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 $secs "$@" > $OUT/$name.log 2>&1; local rc=$?; echo "== $name rc=$rc"; tail -n 3 $OUT/$name.log; if fatal $rc; then exit $rc; fi; }
+run pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
+run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o heist --output-format csv -- python3 bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary
+run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary
+run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary
+run sstamp 300 python tools/probe_step_stamps.py
+run bench 900 python bench.py
+echo "== all done"

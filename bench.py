@@ -85,6 +85,38 @@ def measure_rollout(env, dev, steps=20, warmup=3):
             "note": "heist_step + fused Solver select_action (backbone + head kernels), carried LSTM state"}
 
 
+def measure_env_config(dev, R, n, budget, steps=100, warmup=10, **kw):
+    """env-only heist_step at another BASELINE config (C4: 8192 envs/GPU at the top of the
+    budget schedule; C5: 2048 envs/GPU, 32x32, exactly 4 cameras + 3 guards), timed like
+    the headline number (HIP events around `steps` launches)."""
+    from heist_amd import EnvironmentConfig, HeistEnv
+    from heist_amd.layouts import valid_synthetic_layouts
+    cfg = EnvironmentConfig(grid_rows=R, grid_cols=R, max_steps=200, architect_budget=budget)
+    env = HeistEnv(n, cfg, max_cams=8, max_guards=4, max_path=16, device=dev, auto_reset=True)
+    lays = valid_synthetic_layouts(env, budget, seed=99, **kw)
+    env.reset()
+    acts = torch.randint(0, 5, (warmup + steps, n), device=dev, dtype=torch.int64)
+    for k in range(warmup):
+        env.step(acts[k])
+    st = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize(dev)
+    e0.record(st)
+    for k in range(steps):
+        env.step(acts[warmup + k])
+    e1.record(st)
+    torch.cuda.synchronize(dev)
+    ms = e0.elapsed_time(e1) / steps
+    ncam = float(np.mean([len(c) for _, c, _ in lays]))
+    ngu = float(np.mean([len(g) for _, _, g in lays]))
+    b = algorithmic_bytes_per_env_step(R, R, ncam, ngu)
+    gbs = b * n / (ms * 1e-3) / 1e9
+    return {"value": n / (ms * 1e-3), "unit": "env-steps/s", "kernel_ms": ms, "envs": n, "grid": "%dx%d" % (R, R),
+            "budget": budget, "mean_cameras": ncam, "mean_guards": ngu,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_env_step": b}}
+
+
 SOLVER_BACKBONE_FLOP = 2 * 400 * (32 * 27 + 64 * 288 + 64 * 576)  # conv1..3 MACs x 2 at 20x20, per env
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
 
@@ -254,6 +286,10 @@ def main():
         # only (at N>1 the other ranks would idle at the closing barrier meanwhile)
         if not args.no_secondary and world == 1:
             sec = {}
+            log("env-only at the other BASELINE configs")
+            sec["env_only_c4_8192envs_budget40"] = measure_env_config(dev, 20, 8192, 40)
+            sec["env_only_c5_32x32_2048envs_4cams_3guards"] = measure_env_config(dev, 32, 2048, 40, n_cams=4,
+                                                                                 n_guards=3)
             log("rollout")
             sec["rollout"] = measure_rollout(env, dev)
             log("policy inference")

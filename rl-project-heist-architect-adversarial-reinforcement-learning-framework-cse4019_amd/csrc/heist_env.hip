@@ -710,10 +710,11 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
       o1[q] = make_float4((v & 0xff) ? 1.0f : 0.0f, (v & 0xff00) ? 1.0f : 0.0f, (v & 0xff0000) ? 1.0f : 0.0f,
                           (v & 0xff000000u) ? 1.0f : 0.0f);
     }
+    const int qs = solver >> 2, qv = vault >> 2;
     for (int q = t; q < n4; q += NT) {
       float4 v = reinterpret_cast<const float4*>(L.plane)[q];
-      patch4(v, solver - 4 * q, sv);
-      patch4(v, vault - 4 * q, p.vault_val);
+      if (q == qs) patch4(v, solver & 3, sv);          // only the solver's and the vault's
+      if (q == qv) patch4(v, vault & 3, p.vault_val);  // float4 take these branches
       o2[q] = v;
     }
   } else {

@@ -173,6 +173,33 @@ def test_step_after_done_without_auto_reset(gpu_device):
     assert torch.equal(env.obs, obs_before)
 
 
+def test_step_stamps_instrumentation(gpu_device):
+    """heist_step_stamps: the stamped kernel variant gives the same results as the plain
+    one, every wave records 8 non-decreasing clock stamps, and HW_ID / XCC_ID are filled."""
+    from heist_amd import _native as nat
+    n = 256
+    cfg = EnvironmentConfig()
+    lays = synthetic_layouts(n, 20, 20, 15, seed=31)
+    envs = [HeistEnv(n, cfg, device=gpu_device) for _ in range(2)]
+    for e in envs:
+        e.set_layouts(lays, budget=15)
+        e.reset()
+    buf = torch.zeros((n, 4, 10), dtype=torch.int64, device=gpu_device)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    for t in range(20):
+        a = torch.randint(0, 5, (n,), generator=g)
+        nat.check(nat.lib().heist_step_stamps(envs[0]._h, nat.ptr(buf)), "heist_step_stamps")
+        r0 = envs[0].step(a)
+        nat.check(nat.lib().heist_step_stamps(envs[0]._h, None), "heist_step_stamps")
+        r1 = envs[1].step(a)
+        for x, y in zip(r0, r1):
+            assert torch.equal(x, y), t
+    s = buf.cpu().numpy()
+    assert (s[:, :, :8] > 0).all()
+    assert (np.diff(s[:, :, :8], axis=2) >= 0).all()
+    assert (s[:, :, 8] != 0).any()
+
+
 def test_sample_counter_work_figure(gpu_device):
     """heist_count_samples: an unobstructed camera ray evaluates all 2*range samples, a guard
     ray all range samples; counting leaves the results unchanged."""

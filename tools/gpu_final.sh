@@ -1,7 +1,7 @@
 #!/bin/bash
 # Final round-1 GPU session: GPU parity suite, smoke, default bench, rocprof kernel stats, PMC traffic passes.
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
-OUT=gpurun_out/r01z
+OUT=gpurun_out/${TAG:-r01z}
 mkdir -p $OUT
 export TMPDIR=/tmp
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }

@@ -92,7 +92,8 @@ def measure_env_config(dev, R, n, budget, steps=100, warmup=10, **kw):
     from heist_amd import EnvironmentConfig, HeistEnv
     from heist_amd.layouts import valid_synthetic_layouts
     cfg = EnvironmentConfig(grid_rows=R, grid_cols=R, max_steps=200, architect_budget=budget)
-    env = HeistEnv(n, cfg, max_cams=8, max_guards=4, max_path=16, device=dev, auto_reset=True)
+    # capacity for whatever the budget can buy (cameras cost 3, guards 5: budget.py:13-17)
+    env = HeistEnv(n, cfg, max_cams=budget // 3, max_guards=budget // 5, max_path=16, device=dev, auto_reset=True)
     lays = valid_synthetic_layouts(env, budget, seed=99, **kw)
     env.reset()
     acts = torch.randint(0, 5, (warmup + steps, n), device=dev, dtype=torch.int64)

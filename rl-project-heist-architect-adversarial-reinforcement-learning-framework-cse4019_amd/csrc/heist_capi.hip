@@ -26,6 +26,7 @@ hipError_t launch_export(const EnvParams& p, int32_t* scalars, int8_t* grid, dou
 hipError_t launch_bfs(const int32_t* grid, int n, int R, int C, int sr, int sc, int gr, int gc, uint8_t* out,
                       hipStream_t st);
 int vis_gap_for(int R, int C);
+int stop_map_bytes(int R, int C);
 bool env_variant_exists(int W, int U, int O, int D);
 hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
                         uint8_t* out, int ray_mode, hipStream_t st);
@@ -206,6 +207,7 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
       sizeof(float) * planes.size(),
       sizeof(int32_t) * n,
       sizeof(double) * 3 * heist::kHalfDegN,  // [sin | cos | staging radians]
+      (size_t)heist::stop_map_bytes(R, C) * n,
   };
   h->n_allocs = 0;
   for (size_t k = 0; k < sizeof(sizes) / sizeof(sizes[0]); ++k) {
@@ -228,6 +230,8 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   p.plane1 = p.plane0 + (size_t)R * C;
   p.order = (int32_t*)h->allocs[7];
   p.half_deg = (const double*)h->allocs[8];
+  p.stop = (uint8_t*)h->allocs[9];
+  p.stop_bytes = heist::stop_map_bytes(R, C);
   std::vector<double> hrad(heist::kHalfDegN);
   for (int m = 0; m < heist::kHalfDegN; ++m) hrad[m] = (0.5 * (m - heist::kHalfDegN / 2)) * heist::kDegToRad;
 

@@ -654,6 +654,11 @@ __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds
     lp[t] = pv;
   }
   if (t < pw) L.path[t] = wv;
+  {  // the layout's padded stop map, built once by set_layout_kernel
+    const float4* ss = reinterpret_cast<const float4*>(p.stop + (size_t)e * p.stop_bytes);
+    float4* sd = reinterpret_cast<float4*>(L.wall);
+    for (int i = t; i < p.stop_bytes / 16; i += NT) sd[i] = ss[i];
+  }
   for (int i = t + NT; i < n4; i += NT) {
     d4[i] = s4[i];
     lp[i] = pl0[i];
@@ -787,7 +792,6 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   const bool act = !s.done;
   __syncthreads();  // grid, paths in LDS
   HEIST_STEP_STAMP(1);
-  build_wall_map<NT>(L.grid, L, p.R, p.C);  // read by the raycast after its first barrier
 
   double reward = 0.0;
   int status = kAlreadyDone;
@@ -920,8 +924,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   EmitterRaw raw;
   prefetch<NT>(p, e, L, n_cams, n_em, raw);
   clear_vis<NT>(p, L);
-  __syncthreads();  // grid in LDS
-  build_wall_map<NT>(L.grid, L, p.R, p.C);
+  __syncthreads();  // grid, stop map in LDS
   reset_solver(p, s);
   Emit E;
   if (t < n_cams) {
@@ -944,6 +947,22 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
 // ---------------------------------------------------------------------------
 // layout placement + BFS
 // ---------------------------------------------------------------------------
+
+// The padded stop map of tile grid g (1 = wall or outside the grid; the layout of
+// EnvLds::wall) into p.stop for env e, by threads lane, lane + stride, ...  Built once per
+// layout; step and reset copy it into LDS with the rest of the prefetch.
+__device__ __forceinline__ void write_stop_map(const EnvParams& p, int e, const uint8_t* g, int lane, int stride) {
+  const int R = p.R, C = p.C, PC = C + 2 * kRing, nb = (R + 2 * kRing) * PC;
+  uint8_t* stp = p.stop + (size_t)e * p.stop_bytes;
+  for (int i = lane; i < p.stop_bytes; i += stride) {
+    const int pr = i / PC;
+    const int r = pr - kRing, c = i - pr * PC - kRing;
+    const bool out = i >= nb || (unsigned)r >= (unsigned)R || (unsigned)c >= (unsigned)C;
+    stp[i] = out ? 1 : (g[r * C + c] == kWall ? 1 : 0);
+  }
+}
+
+int stop_map_bytes(int R, int C) { return (int)align16((size_t)padded_bytes(R, C)); }
 
 // 4-neighbour reachability start -> goal over non-wall tiles (utils.py:52-85) as a
 // wave-level bitboard flood fill: lane r holds row r as a 64-bit mask.
@@ -1061,6 +1080,7 @@ __global__ __launch_bounds__(64) void set_layout_kernel(EnvParams p, int max_wal
   const bool ok = bfs_wave(m, p.sr, p.sc, p.vr, p.vc);
   uint8_t* dst = p.grid + (size_t)e * p.RC;
   for (int i = lane; i < p.RC; i += 64) dst[i] = g[i];
+  write_stop_map(p, e, g, lane, 64);
   if (lane == 0) {
     EnvScalars* s = p.scal + e;
     s->n_walls = cnt[0];
@@ -1120,7 +1140,7 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
   }
 }
 
-__global__ void init_kernel(EnvParams p) {
+__global__ void init_kernel(EnvParams p) {  // one thread per env
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= p.n_envs) return;
   p.order[e] = e;
@@ -1136,6 +1156,7 @@ __global__ void init_kernel(EnvParams p) {
   }
   g[p.sr * p.C + p.sc] = kStart;
   g[p.vr * p.C + p.vc] = kVault;
+  write_stop_map(p, e, g, 0, 1);
 }
 
 __global__ void export_kernel(EnvParams p, int32_t* scalars, int8_t* grid, double* cam_heading, int32_t* guard_idx,

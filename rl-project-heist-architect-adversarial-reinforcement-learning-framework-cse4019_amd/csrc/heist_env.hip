@@ -641,6 +641,12 @@ __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds
     pv = pl0[t];
   }
   if (t < pw) wv = ps[t];
+  // the layout's padded stop map, built once by set_layout_kernel
+  const float4* ss = reinterpret_cast<const float4*>(p.stop + (size_t)e * p.stop_bytes);
+  float4* sd = reinterpret_cast<float4*>(L.wall);
+  const int n_stop = p.stop_bytes / 16;
+  float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t < n_stop) sv = ss[t];
   raw.a = make_uint4(0u, 0u, 0u, 0u);
   raw.b = raw.a;
   if (t < n_em) {
@@ -654,11 +660,8 @@ __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds
     lp[t] = pv;
   }
   if (t < pw) L.path[t] = wv;
-  {  // the layout's padded stop map, built once by set_layout_kernel
-    const float4* ss = reinterpret_cast<const float4*>(p.stop + (size_t)e * p.stop_bytes);
-    float4* sd = reinterpret_cast<float4*>(L.wall);
-    for (int i = t; i < p.stop_bytes / 16; i += NT) sd[i] = ss[i];
-  }
+  if (t < n_stop) sd[t] = sv;
+  for (int i = t + NT; i < n_stop; i += NT) sd[i] = ss[i];
   for (int i = t + NT; i < n4; i += NT) {
     d4[i] = s4[i];
     lp[i] = pl0[i];

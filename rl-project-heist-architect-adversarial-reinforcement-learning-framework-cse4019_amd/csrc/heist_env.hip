@@ -702,7 +702,10 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
     float4* o0 = reinterpret_cast<float4*>(o);
     float4* o1 = o0 + n4;
     float4* o2 = o1 + n4;
-    for (int q = t; q < n4; q += NT) {
+    // the first half of the block writes channels 0 and 1, the second half channel 2
+    constexpr int H = NT / 2;
+    if (t < H) {
+    for (int q = t; q < n4; q += H) {
       const uint32_t b = *reinterpret_cast<const uint32_t*>(L.grid + 4 * q);
       o0[q] = make_float4(p.tile_lut[b & 7], p.tile_lut[(b >> 8) & 7], p.tile_lut[(b >> 16) & 7],
                           p.tile_lut[(b >> 24) & 7]);
@@ -718,12 +721,14 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
       o1[q] = make_float4((v & 0xff) ? 1.0f : 0.0f, (v & 0xff00) ? 1.0f : 0.0f, (v & 0xff0000) ? 1.0f : 0.0f,
                           (v & 0xff000000u) ? 1.0f : 0.0f);
     }
+    } else {
     const int qs = solver >> 2, qv = vault >> 2;
-    for (int q = t; q < n4; q += NT) {
+    for (int q = t - H; q < n4; q += H) {
       float4 v = reinterpret_cast<const float4*>(L.plane)[q];
       if (q == qs) patch4(v, solver & 3, sv);          // only the solver's and the vault's
       if (q == qv) patch4(v, vault & 3, p.vault_val);  // float4 take these branches
       o2[q] = v;
+    }
     }
   } else {
     for (int q = t; q < 3 * RC; q += NT) {

@@ -3,9 +3,14 @@
 One "step" = one heist_step launch over all envs of the rank: move, camera/guard
 update, raycast visibility, reward/termination, in-kernel auto-reset, and the
 [N,3,20,20] float32 observation write.  Inputs (layouts, per-step actions) are
-resident in HBM before the timed region.  Multi-GPU: one process per GPU (torchrun),
-envs sharded by rank with no data-path collective (weak scaling); the only RCCL
-calls are the barrier and the max-over-ranks of the elapsed time.
+resident in HBM before the timed region.  The headline layouts are BASELINE config 2's:
+sampled at temperature 1.0 and budget 15 from the fixed Architect checkpoint
+(checkpoints/architect_c2_fixed.pt, tools/mint_architect_checkpoint.py), resampled until
+BFS-valid; the round-1 synthetic mix (SURVEY 8d generator (ii)) is a secondary line.
+Multi-GPU: one process per GPU, envs sharded by rank with no data-path collective (weak
+scaling); the only RCCL calls are the barrier and the max-over-ranks of the elapsed time.
+`--gpus N` without torchrun's WORLD_SIZE spawns the N ranks itself (before any GPU call);
+under torchrun WORLD_SIZE must equal N.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 4096] [--no-cpu-baseline]
 """
@@ -37,11 +42,23 @@ def algorithmic_bytes_per_env_step(R, C, ncam, nguard):
     return 12 * R * C + R * C + 8 + 4 + 1 + 1 + 2 * (24 + 8 * ncam + 12 * nguard)
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(layouts, cfg, budget, target_s=10.0, threads=1):
     """The C oracle (restatement of the reference CPU path) on a bounded sample of the
-    same workload: env.step + get_state_tensor with random actions, auto-reset."""
+    same workload: env.step + get_state_tensor with random actions, auto-reset; one
+    pthread per core over disjoint envs when threads > 1."""
     from oracle import pyoracle as po
-    sample = layouts[:256]
+    sample = layouts[:max(256, 16 * threads)]
 
     def make():
         envs = []
@@ -61,16 +78,51 @@ def cpu_baseline(layouts, cfg, budget, target_s=10.0, threads=1):
     t0 = time.perf_counter()
     n = po.run_random(envs, steps, seed=2, n_threads=threads)
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "sample": "%d of the same synthetic 20x20 layouts x %d ticks (%d env-steps, %.1f s), random actions, "
-                      "auto-reset, state tensor each tick; C oracle (oracle/heist_oracle.c) with host libm"
-                      % (len(sample), steps, n, dt)}
+    return {"value": n / dt, "unit": "env-steps/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+            "host_cpus": os.cpu_count(),
+            "sample": "%d of the bench's layouts x %d ticks (%d env-steps, %.1f s wall), random actions, "
+                      "auto-reset, state tensor each tick; C oracle (oracle/heist_oracle.c, host libm), %d thread%s"
+                      % (len(sample), steps, n, dt, threads, "s" if threads > 1 else "")}
 
 
-def measure_rollout(env, dev, steps=20, warmup=3):
-    """env step + batched Solver select_action on the fused kernels (carried LSTM state)."""
+def architect_layouts(env, budget, seed, ckpt=None, max_rounds=20):
+    """BASELINE config 2's layouts: the fixed Architect checkpoint sampled at T = 1.0 with
+    the given budget (cameras and guards allowed), every env resampled until its layout is
+    BFS-valid.  Returns the accepted layouts as reference-format lists."""
+    from heist_amd.agents import ArchitectAgent
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import mint_architect_checkpoint as mint
+    path = ckpt or mint.DEFAULT
+    if not os.path.exists(path):
+        mint.mint(path)
+    ag = ArchitectAgent(grid_rows=env.rows, grid_cols=env.cols, budget=budget, device=env.device)
+    ag.load(path)
+    gen = torch.Generator(device=env.device)
+    gen.manual_seed(seed)
+    n = env.n_envs
+    from heist_amd.training import _lb_rows, _scatter_layout
+    lb, _, _ = ag.generate_layouts(n, 1.0, True, True, env=env, generator=gen, record=False)
+    valid = env.set_layout_batch(lb).clone()
+    for _ in range(max_rounds):
+        bad = (~valid).nonzero().reshape(-1).cpu().numpy()
+        if len(bad) == 0:
+            break
+        lbk, _, _ = ag.generate_layouts(len(bad), 1.0, True, True, env=env, generator=gen, record=False)
+        full = _scatter_layout(lbk, bad, env)
+        m = torch.zeros(n, dtype=torch.uint8, device=env.device)
+        m[torch.as_tensor(bad, device=env.device)] = 1
+        v = env.set_layout_batch(full, m)
+        for k in lb.__dataclass_fields__:
+            getattr(lb, k)[torch.as_tensor(bad, device=env.device)] = getattr(lbk, k)
+        valid[torch.as_tensor(bad, device=env.device)] = v[torch.as_tensor(bad, device=env.device)]
+    return lb, bool(valid.all())
+
+
+def measure_rollout(env, dev, steps=20, warmup=3, precision="bf16"):
+    """env step + batched Solver select_action (carried LSTM state): "bf16" on the fused
+    kernels (opt-in), "fp32" on the reference's fp32 forward (the parity default)."""
     from heist_amd.agents import SolverAgent
-    ag = SolverAgent(env.rows, env.cols, device=dev)
+    ag = SolverAgent(env.rows, env.cols, device=dev, rollout_precision=precision)
     h = c = torch.zeros(1, env.n_envs, 128, device=dev)
     for k in range(warmup + steps):
         if k == warmup:
@@ -81,8 +133,10 @@ def measure_rollout(env, dev, steps=20, warmup=3):
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     return {"value": steps * env.n_envs / dt, "unit": "env-steps/s", "ms_per_step": dt / steps * 1e3,
-            "dtype": "bf16 MFMA policy (fp32 accumulate)",
-            "note": "heist_step + fused Solver select_action (backbone + head kernels), carried LSTM state"}
+            "dtype": "bf16 MFMA policy (fp32 accumulate)" if precision == "bf16" else "fp32 policy (PyTorch-ROCm)",
+            "note": ("heist_step + fused Solver select_action (backbone + head kernels)" if precision == "bf16" else
+                     "heist_step + reference fp32 select_action (MIOpen convs, fused-gate LSTM)") +
+                    ", carried LSTM state"}
 
 
 def measure_env_config(dev, R, n, budget, steps=100, warmup=10, **kw):
@@ -93,8 +147,12 @@ def measure_env_config(dev, R, n, budget, steps=100, warmup=10, **kw):
     from heist_amd.layouts import valid_synthetic_layouts
     cfg = EnvironmentConfig(grid_rows=R, grid_cols=R, max_steps=200, architect_budget=budget)
     # capacity for whatever the budget can buy (cameras cost 3, guards 5: budget.py:13-17)
-    env = HeistEnv(n, cfg, max_cams=budget // 3, max_guards=budget // 5, max_path=16, device=dev, auto_reset=True)
-    lays = valid_synthetic_layouts(env, budget, seed=99, **kw)
+    env = HeistEnv(n, cfg, max_cams=max(1, budget // 3), max_guards=max(1, budget // 5), max_path=16, device=dev,
+                   auto_reset=True)
+    if kw.pop("architect", False):
+        architect_layouts(env, budget, seed=99)
+    else:
+        valid_synthetic_layouts(env, budget, seed=99, **kw)
     env.reset()
     acts = torch.randint(0, 5, (warmup + steps, n), device=dev, dtype=torch.int64)
     for k in range(warmup):
@@ -108,8 +166,8 @@ def measure_env_config(dev, R, n, budget, steps=100, warmup=10, **kw):
     e1.record(st)
     torch.cuda.synchronize(dev)
     ms = e0.elapsed_time(e1) / steps
-    ncam = float(np.mean([len(c) for _, c, _ in lays]))
-    ngu = float(np.mean([len(g) for _, _, g in lays]))
+    st = env.export()
+    ncam, ngu = float(st["n_cams"].double().mean()), float(st["n_guards"].double().mean())
     b = algorithmic_bytes_per_env_step(R, R, ncam, ngu)
     gbs = b * n / (ms * 1e-3) / 1e9
     return {"value": n / (ms * 1e-3), "unit": "env-steps/s", "kernel_ms": ms, "envs": n, "grid": "%dx%d" % (R, R),
@@ -154,15 +212,18 @@ def measure_policy(dev, n, iters=50, warmup=5):
                                   "flop_per_env": SOLVER_BACKBONE_FLOP}}
 
 
-def measure_train(cfg, dev, n_envs, rollout_len=32, minibatch=16384, update_precision="fp32"):
-    """Batched AdversarialTrainer iteration: rollout + heist_gae + adv-norm + 3 PPO epochs
-    (heist_ppo_loss, Adam) + Architect scoring/update/re-layout."""
+def measure_train(cfg, dev, n_envs, rollout_len=32, minibatch=16384, update_precision="fp32",
+                  rollout_precision="fp32"):
+    """Batched AdversarialTrainer iteration (C3-style self-play at the Full Security phase):
+    rollout + heist_gae (V(s_T) bootstrap) + adv-norm + 3 PPO epochs (heist_ppo_loss,
+    Adam) + Architect scoring/update/re-layout."""
     from heist_amd.training import AdversarialTrainer
     import tempfile
     d = tempfile.mkdtemp()
     tr = AdversarialTrainer(cfg, solver_episodes_per_layout=4, total_episodes=10 ** 9, save_dir=d, log_dir=d,
                             n_envs=n_envs, rollout_len=rollout_len, minibatch=minibatch, device=dev, seed=0,
-                            update_precision=update_precision)
+                            update_precision=update_precision, rollout_precision=rollout_precision)
+    tr.global_episode = 200
     tr._assign_layouts(np.arange(n_envs))
     log("  warm-up iteration")
     tr.train_iteration()
@@ -172,8 +233,19 @@ def measure_train(cfg, dev, n_envs, rollout_len=32, minibatch=16384, update_prec
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     return {"value": rollout_len * n_envs / dt, "unit": "env-steps/s", "s_per_iteration": dt,
-            "config": "T=%d x %d envs, 3 epochs, minibatch %d; rollout policy bf16 fused kernels, PPO update %s "
-                      "(NHWC MIOpen convs)" % (rollout_len, n_envs, minibatch, update_precision)}
+            "dtype": "rollout %s, update %s" % (rollout_precision, update_precision),
+            "config": "T=%d x %d envs, 3 epochs, minibatch %d; rollout policy %s, PPO update %s "
+                      "(NHWC MIOpen convs)" % (rollout_len, n_envs, minibatch,
+                                               "bf16 fused kernels" if rollout_precision == "bf16" else "fp32",
+                                               update_precision)}
+
+
+def _spawned_rank(rank, world, port, argv):
+    """Body of a rank started by `bench.py --gpus N` (torch.multiprocessing spawn)."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    sys.argv = [sys.argv[0]] + list(argv)
+    main()
 
 
 def main():
@@ -183,12 +255,29 @@ def main():
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--budget", type=int, default=15)
+    ap.add_argument("--layouts", choices=("architect", "synthetic"), default="architect",
+                    help="headline layout source: the fixed Architect checkpoint (C2) or the synthetic mix")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-secondary", action="store_true", help="skip the rollout / full-train numbers")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # launch the N ranks here (spawned interpreters; this process never touches the GPU)
+        import socket
+        import torch.multiprocessing as tmp
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        tmp.spawn(_spawned_rank, args=(args.gpus, port, sys.argv[1:]), nprocs=args.gpus, join=True)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d (launch N ranks with torchrun --nproc-per-node N, or run "
+              "without torchrun and let --gpus spawn them)" % (args.gpus, world), file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = torch.distributed
@@ -204,8 +293,15 @@ def main():
 
     cfg = EnvironmentConfig(grid_rows=20, grid_cols=20, max_steps=200, architect_budget=args.budget)
     N = args.envs
-    env = HeistEnv(N, cfg, max_cams=8, max_guards=4, max_path=16, device=dev, auto_reset=True)
-    layouts = valid_synthetic_layouts(env, args.budget, seed=1234 + rank)
+    env = HeistEnv(N, cfg, max_cams=max(1, args.budget // 3), max_guards=max(1, args.budget // 5), max_path=16,
+                   device=dev, auto_reset=True)
+    if args.layouts == "architect":
+        lb, all_valid = architect_layouts(env, args.budget, seed=1234 + rank)
+        layouts = None
+        if not all_valid:
+            log("warning: some Architect layouts stayed BFS-invalid after resampling")
+    else:
+        layouts = valid_synthetic_layouts(env, args.budget, seed=1234 + rank)
     env.reset()
     gen = torch.Generator(device=dev)
     gen.manual_seed(4321 + rank)
@@ -252,29 +348,35 @@ def main():
     samples_per_step = float(cnt.sum().item()) / (n_count * N)
     exact_rays_per_step = float(cnt_x.sum().item()) / (n_count * N)
 
-    ncam = float(np.mean([len(c) for _, c, _ in layouts]))
-    ngu = float(np.mean([len(g) for _, _, g in layouts]))
+    st = env.export()  # accepted placements (set_layout's rules), not the requested lists
+    ncam, ngu = float(st["n_cams"].double().mean()), float(st["n_guards"].double().mean())
     b_step = algorithmic_bytes_per_env_step(20, 20, ncam, ngu)
     achieved = b_step * N / (kern_ms * 1e-3) / 1e9  # GB/s, per launch / launch duration
     total_steps = args.steps * N * world
     value = total_steps / elapsed
 
     if rank == 0:
-        traffic = None
+        traffic, traffic_src = None, None
         tf = os.path.join(ROOT, "profiles", "heist_step_traffic.json")
         if os.path.exists(tf) and N == 4096:
             with open(tf) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                tj = json.load(f)
+            if tj.get("workload") == args.layouts:
+                traffic = tj.get("hbm_bytes_per_launch")
+                traffic_src = "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this command (%s), corrected per " \
+                              "MI355X_MICROARCH.md: profiles/heist_step_traffic.json" % tj.get("profile", "?")
         line = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "env-only heist_step, 20x20 grid, %d envs/GPU, synthetic budget-%d layouts "
-                                   "(mean %.2f cameras, %.2f guards/env), uniform random actions, auto-reset"
-                                   % (N, args.budget, ncam, ngu),
-                       "envs_per_gpu": N, "grid": "20x20", "parallelism": "env-sharded x%d" % world},
+            "config": {"workload": "env-only heist_step, 20x20 grid, %d envs/GPU, %s budget-%d layouts "
+                                   "(mean %.2f cameras, %.2f guards/env accepted), uniform random actions, auto-reset"
+                                   % (N, "BASELINE C2: fixed Architect checkpoint (T=1.0)" if args.layouts == "architect"
+                                      else "synthetic (SURVEY 8d generator ii)", args.budget, ncam, ngu),
+                       "envs_per_gpu": N, "grid": "20x20", "layouts": args.layouts,
+                       "parallelism": "env-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "heist::step_kernel", "kernel_ms": kern_ms,
                          "algorithmic_bytes_per_env_step": b_step,
                          "ray_samples_per_env_step": samples_per_step,
@@ -287,22 +389,32 @@ def main():
         # only (at N>1 the other ranks would idle at the closing barrier meanwhile)
         if not args.no_secondary and world == 1:
             sec = {}
-            log("env-only at the other BASELINE configs")
-            sec["env_only_c4_8192envs_budget40"] = measure_env_config(dev, 20, 8192, 40)
+            log("env-only at the other BASELINE configs / layout sources")
+            other = "synthetic" if args.layouts == "architect" else "architect"
+            sec["env_only_%s_layouts" % other] = measure_env_config(dev, 20, N, args.budget,
+                                                                    architect=other == "architect")
+            sec["env_only_c4_8192envs_budget40"] = measure_env_config(dev, 20, 8192, 40, architect=True)
             sec["env_only_c5_32x32_2048envs_4cams_3guards"] = measure_env_config(dev, 32, 2048, 40, n_cams=4,
                                                                                  n_guards=3)
             log("rollout")
-            sec["rollout"] = measure_rollout(env, dev)
+            sec["rollout_bf16"] = measure_rollout(env, dev, precision="bf16")
+            sec["rollout_fp32"] = measure_rollout(env, dev, steps=10, precision="fp32")
             log("policy inference")
             sec["policy_inference"] = measure_policy(dev, N)
-            log("full train (fp32 update)")
-            sec["full_train"] = measure_train(cfg, dev, N)
-            log("full train (bf16 update)")
-            sec["full_train_bf16_update"] = measure_train(cfg, dev, N, update_precision="bf16")
+            log("full train (fp32 rollout + fp32 update: the parity mode)")
+            sec["full_train_fp32"] = measure_train(cfg, dev, N)
+            log("full train (bf16 rollout + bf16 update)")
+            sec["full_train_bf16"] = measure_train(cfg, dev, N, update_precision="bf16", rollout_precision="bf16")
             line["secondary"] = sec
         if not args.no_cpu_baseline and world == 1:
             log("cpu baseline")
-            line["cpu_baseline"] = cpu_baseline(layouts, cfg, args.budget, target_s=args.cpu_seconds, threads=1)
+            if layouts is None:
+                from heist_amd.training import _lb_rows
+                layouts = _lb_rows(lb, np.arange(min(N, 512))).to_lists()
+            cores = max(1, min(os.cpu_count() or 1, 16))  # the GPU box's CPU share is 16 threads per GPU
+            line["cpu_baseline"] = cpu_baseline(layouts, cfg, args.budget, target_s=args.cpu_seconds, threads=cores)
+            line["cpu_baseline_1core"] = cpu_baseline(layouts, cfg, args.budget, target_s=args.cpu_seconds / 2,
+                                                      threads=1)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

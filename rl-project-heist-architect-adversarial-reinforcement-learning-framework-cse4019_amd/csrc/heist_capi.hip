@@ -407,15 +407,16 @@ int heist_gae(const float* rewards, const float* values, const uint8_t* dones, c
 }
 
 int heist_adv_moments(const float* x, int64_t n, int phase, double* acc, heist_stream_t stream) {
-  HEIST_REQUIRE(x && acc, "heist_adv_moments: null pointer");
   HEIST_REQUIRE(phase == 0 || phase == 1, "heist_adv_moments: phase must be 0 or 1");
   HEIST_REQUIRE(n >= 0, "heist_adv_moments: negative size");
+  if (n == 0) return 0;  // an empty shard adds nothing to the sums (its rank still joins the all-reduce)
+  HEIST_REQUIRE(x && acc, "heist_adv_moments: null pointer");
   return check_hip(heist::launch_adv_moments(x, n, phase, acc, (hipStream_t)stream), "heist_adv_moments");
 }
 
 int heist_adv_apply(float* x, int64_t n, const double* acc, float eps, heist_stream_t stream) {
-  HEIST_REQUIRE(x && acc, "heist_adv_apply: null pointer");
   if (n <= 0) return 0;
+  HEIST_REQUIRE(x && acc, "heist_adv_apply: null pointer");
   return check_hip(heist::launch_adv_apply(x, n, acc, eps, (hipStream_t)stream), "heist_adv_apply");
 }
 

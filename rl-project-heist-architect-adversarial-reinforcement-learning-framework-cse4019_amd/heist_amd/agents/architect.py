@@ -5,6 +5,12 @@ including its "simplified PPO": the log-probabilities are recorded under no_grad
 the policy term carries no gradient and only the encoder, fc_global and value head
 train (agents/architect.py:75-81, :105, :133).  generate_layouts() draws N layouts
 from one forward of the (constant-input) network and decodes them on the GPU.
+
+Batched training records each layout's (log_prob, value, reward) as one transition
+(store_transitions) when the layout is scored, so rewards can never pair with another
+layout's log-prob.  update() is the reference's formula over whatever the buffer holds;
+inside a process group it is global: the buffer statistics are all-reduced (one float64
+vector), every rank forms the same value target and takes the same step.
 """
 from typing import Dict, List, Optional
 
@@ -16,7 +22,7 @@ import torch.nn.functional as F
 from ..architect_decode import decode_layouts
 from ..networks import ArchitectNetwork
 from ..utils import DEVICE, TileType
-from .solver import allreduce_grads
+from .. import dist_utils
 
 
 class ArchitectAgent:  # agents/architect.py:16-170
@@ -72,7 +78,7 @@ class ArchitectAgent:  # agents/architect.py:16-170
             self.values.extend([value] * n)
         return lb, total_logp, value
 
-    def store_reward(self, reward: float):
+    def store_reward(self, reward: float):  # agents/architect.py:85-89
         self.rewards.append(reward)
         self.total_reward += reward
         self.episode_count += 1
@@ -81,11 +87,74 @@ class ArchitectAgent:  # agents/architect.py:16-170
         for r in (rewards.tolist() if torch.is_tensor(rewards) else list(rewards)):
             self.store_reward(float(r))
 
-    def update(self) -> Dict[str, float]:  # agents/architect.py:91-155
+    def store_transitions(self, log_probs: torch.Tensor, values: torch.Tensor, rewards):
+        """Batched training: k scored layouts as (log_prob [k], value [k], reward [k]) triples."""
+        rw = rewards.tolist() if torch.is_tensor(rewards) else list(rewards)
+        if len(rw) != len(log_probs) or len(rw) != len(values):
+            raise ValueError("store_transitions: %d log-probs, %d values, %d rewards"
+                             % (len(log_probs), len(values), len(rw)))
+        self.log_probs.extend(log_probs.detach().reshape(-1).unbind(0))
+        self.values.extend(values.detach().reshape(-1).unbind(0))
+        for r in rw:
+            self.store_reward(float(r))
+
+    def _step(self, loss: torch.Tensor, collective: bool):
+        self.optimizer.zero_grad()
+        loss.backward()
+        params = list(self.network.parameters())
+        if collective:
+            dist_utils.allreduce_grads(params)  # identical on every rank already: keeps them bit-equal
+        nn.utils.clip_grad_norm_(params, 0.5)
+        self.optimizer.step()
+
+    def update(self, collective: Optional[bool] = None) -> Dict[str, float]:  # agents/architect.py:91-155
+        """The reference's "simplified PPO" step on the buffered transitions.
+
+        collective (default: inside a process group): every rank must call it, with any
+        number (also zero) of local transitions; the statistics of the union are
+        all-reduced and the step is skipped on every rank when the union is empty."""
+        multi = dist_utils.is_multi() if collective is None else (collective and dist_utils.is_multi())
+        if not multi:
+            return self._update_local()
+        n = min(len(self.rewards), len(self.log_probs), len(self.values))
+        d = self.device
+        # sums over the union: [k, sum r, sum r^2, sum lp, sum lp*r, sum lp*v, sum v]
+        st = torch.zeros(7, dtype=torch.float64, device=d)
+        if n:
+            r = torch.tensor(self.rewards[:n], dtype=torch.float64, device=d)
+            lp = torch.stack(self.log_probs[:n]).to(d).detach().double().reshape(-1)
+            v = torch.stack([x.squeeze() for x in self.values[:n]]).to(d).detach().double().reshape(-1)
+            st = torch.stack([torch.tensor(float(n), dtype=torch.float64, device=d), r.sum(), (r * r).sum(),
+                              lp.sum(), (lp * r).sum(), (lp * v).sum(), v.sum()])
+        dist_utils.allreduce_(st)
+        k, sr, sr2, slp, slpr, slpv, _ = st.tolist()
+        self._clear()
+        if k == 0:
+            return {"architect_loss": 0.0}
+        self.network.train()
+        mean = sr / k
+        if k > 1:  # (r - mean) / (std_unbiased + 1e-8): the normalised rewards average to 0
+            std = max((sr2 - k * mean * mean) / (k - 1), 0.0) ** 0.5
+            target, scale = 0.0, 1.0 / (std + 1e-8)
+        else:
+            target, scale = mean, None
+        # policy_loss = -mean(lp * (r_norm - v)), no gradient path (as in the reference)
+        s_lp_rn = (slpr - mean * slp) * scale if scale is not None else slpr
+        policy_loss = -(s_lp_rn - slpv) / k
+        _, new_values, _ = self.network(self.grid_state())
+        new_value = new_values.squeeze()
+        value_loss = F.mse_loss(new_value, torch.tensor(target, dtype=new_value.dtype, device=d))
+        total = policy_loss + self.value_coeff * value_loss
+        self._step(total, collective=True)
+        return {"architect_policy_loss": float(policy_loss), "architect_value_loss": float(value_loss.item()),
+                "architect_total_loss": float(total.item()), "architect_layouts": int(k),
+                "architect_avg_reward": self.total_reward / max(self.episode_count, 1)}
+
+    def _update_local(self) -> Dict[str, float]:
         if len(self.rewards) == 0:
             return {"architect_loss": 0.0}
         self.network.train()
-        n = min(len(self.rewards), len(self.log_probs))
+        n = min(len(self.rewards), len(self.log_probs), len(self.values))
         rewards = torch.tensor(self.rewards[:n], dtype=torch.float32, device=self.device)
         old_log_probs = torch.stack(self.log_probs[:n]).to(self.device).detach().float()
         old_values = torch.stack([v.squeeze() for v in self.values[:n]]).to(self.device).detach()
@@ -97,19 +166,17 @@ class ArchitectAgent:  # agents/architect.py:16-170
         value_loss = F.mse_loss(new_value, rewards.mean())
         policy_loss = -(old_log_probs * advantages.detach()).mean()  # no gradient path, as in the reference
         total_loss = policy_loss + self.value_coeff * value_loss
-        self.optimizer.zero_grad()
-        total_loss.backward()
-        params = list(self.network.parameters())
-        allreduce_grads(params)
-        nn.utils.clip_grad_norm_(params, 0.5)
-        self.optimizer.step()
+        self._step(total_loss, collective=False)
         metrics = {"architect_policy_loss": float(policy_loss.item()), "architect_value_loss": float(value_loss.item()),
-                   "architect_total_loss": float(total_loss.item()),
+                   "architect_total_loss": float(total_loss.item()), "architect_layouts": int(n),
                    "architect_avg_reward": self.total_reward / max(self.episode_count, 1)}
+        self._clear()
+        return metrics
+
+    def _clear(self):
         self.log_probs.clear()
         self.values.clear()
         self.rewards.clear()
-        return metrics
 
     def save(self, path: str):  # agents/architect.py:157-163
         torch.save({"network": self.network.state_dict(), "optimizer": self.optimizer.state_dict(),

@@ -17,26 +17,10 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..networks import SolverNetwork
+from .. import dist_utils
+from ..dist_utils import allreduce_grads  # noqa: F401  (re-exported: the reference-facing name)
 from ..ppo import compute_gae, normalize_advantages, ppo_loss
 from ..utils import DEVICE
-
-
-def allreduce_grads(params, group=None):
-    """Average .grad over ranks with one flat all-reduce (a single RCCL call)."""
-    dist = torch.distributed
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
-        return
-    grads = [p.grad for p in params if p.grad is not None]
-    if not grads:
-        return
-    flat = torch.cat([g.reshape(-1) for g in grads])
-    dist.all_reduce(flat, group=group)
-    flat.div_(dist.get_world_size(group))
-    o = 0
-    for g in grads:
-        n = g.numel()
-        g.copy_(flat[o:o + n].view_as(g))
-        o += n
 
 
 @dataclass
@@ -53,11 +37,20 @@ class Rollout:
 
 
 class SolverAgent:  # agents/solver.py:18-259
+    """rollout_precision selects the batched act() path:
+      * "fp32" (default): the reference's fp32 forward (networks.py:76-131) on PyTorch-ROCm,
+        so rollout log-probs and values are the reference's to fp32 rounding and the PPO
+        ratio at epoch 0 is exactly 1 (the parity mode);
+      * "bf16": the fused HIP kernels (heist_solver_features + heist_solver_head, bf16
+        MFMA operands, fp32 accumulation), ~15x faster; log-probs differ from fp32 by ~1e-3
+        (opt-in, labelled as such by bench.py).
+    ``fused_inference=True`` is the round-1 spelling of rollout_precision="bf16"."""
+
     def __init__(self, grid_rows: int = 20, grid_cols: int = 20, num_actions: int = 5, lr: float = 3e-4,
                  gamma: float = 0.99, gae_lambda: float = 0.95, clip_epsilon: float = 0.2,
                  entropy_coeff: float = 0.05, value_coeff: float = 0.5, max_grad_norm: float = 0.5,
-                 ppo_epochs: int = 3, batch_size: int = 64, device=None, fused_inference: bool = True,
-                 update_precision: str = "fp32"):
+                 ppo_epochs: int = 3, batch_size: int = 64, device=None, fused_inference: Optional[bool] = None,
+                 update_precision: str = "fp32", rollout_precision: Optional[str] = None):
         self.grid_rows = grid_rows
         self.grid_cols = grid_cols
         self.num_actions = num_actions
@@ -69,7 +62,11 @@ class SolverAgent:  # agents/solver.py:18-259
         self.max_grad_norm = max_grad_norm
         self.ppo_epochs = ppo_epochs
         self.batch_size = batch_size
-        self.fused_inference = fused_inference  # batched act(): bf16-MFMA backbone + head kernels
+        if rollout_precision is None:
+            rollout_precision = "bf16" if fused_inference else "fp32"
+        if rollout_precision not in ("fp32", "bf16"):
+            raise ValueError("rollout_precision must be 'fp32' or 'bf16'")
+        self.rollout_precision = rollout_precision
         self._act_seed = int(torch.initial_seed()) ^ 0x5EED
         self._act_counter = 0
         self.device = torch.device(device) if device is not None else DEVICE
@@ -86,6 +83,14 @@ class SolverAgent:  # agents/solver.py:18-259
         self.episode_count = 0
         self.total_reward = 0.0
         self.recent_rewards = deque(maxlen=100)
+
+    @property
+    def fused_inference(self) -> bool:
+        return self.rollout_precision == "bf16"
+
+    @fused_inference.setter
+    def fused_inference(self, v: bool):
+        self.rollout_precision = "bf16" if v else "fp32"
 
     # -- single-env API ------------------------------------------------------------
     def reset(self):
@@ -137,41 +142,62 @@ class SolverAgent:  # agents/solver.py:18-259
         dones = torch.as_tensor(self.dones[:n], dtype=torch.float32).to(d)
         adv, ret = compute_gae(rewards, values, dones, gamma=self.gamma, lam=self.gae_lambda)
         if n > 1:
-            adv = normalize_advantages(adv)
-        m = self._ppo_epochs(states, actions, old_logp, adv, ret, n, np.random.permutation)
+            adv = normalize_advantages(adv, group=_LOCAL)
+        m = self._ppo_epochs(states, actions, old_logp, adv, ret, n, np.random.permutation, collective=False)
         m["solver_avg_reward"] = float(np.mean(self.recent_rewards)) if self.recent_rewards else 0.0
         m["solver_episodes"] = self.episode_count
         self._clear_buffers()
         return m
 
-    def _ppo_epochs(self, states, actions, old_logp, adv, ret, n, perm_fn, minibatch=None) -> Dict[str, float]:
-        """agents/solver.py:157-204: epochs x shuffled minibatches, zero-hidden re-forward."""
+    def _ppo_epochs(self, states, actions, old_logp, adv, ret, n, perm_fn, minibatch=None,
+                    collective: bool = True) -> Dict[str, float]:
+        """agents/solver.py:157-204: epochs x shuffled minibatches, zero-hidden re-forward.
+
+        collective (batched data-parallel training): every rank runs the same number of
+        optimizer steps, max over ranks of ceil(n / minibatch) per epoch.  A rank that has
+        run out of samples takes part with an empty minibatch (zero gradient, weight 0);
+        the one flat all-reduce per step forms the sample-weighted mean gradient, so all
+        ranks clip and step identically and their parameters stay equal."""
         self.network.train()
         bs = minibatch or self.batch_size
         tot = torch.zeros(3, device=self.device)
         updates = 0
         params = list(self.network.parameters())
+        n_mb = (n + bs - 1) // bs
+        multi = collective and dist_utils.is_multi()
+        if multi:
+            n_mb = int(dist_utils.allreduce_(torch.tensor([n_mb], dtype=torch.int64, device=self.device), "max").item())
         for _ in range(self.ppo_epochs):
-            idx = torch.as_tensor(perm_fn(n), device=self.device)
-            for start in range(0, n, bs):
-                b = idx[start:start + bs]
-                x = states[b]
-                if x.is_cuda:
-                    x = x.contiguous(memory_format=torch.channels_last)
-                with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.update_precision == "bf16" and x.is_cuda):
-                    logits, new_values, _ = self.network(x)
-                logits, new_values = logits.float(), new_values.float()
-                loss, parts = ppo_loss(logits, new_values.reshape(-1), actions[b], old_logp[b], adv[b], ret[b],
-                                       self.clip_epsilon, self.value_coeff, self.entropy_coeff)
+            idx = torch.as_tensor(perm_fn(n), device=self.device) if n else None
+            for k in range(n_mb):
+                start = k * bs
                 self.optimizer.zero_grad(set_to_none=False)
-                loss.backward()
-                allreduce_grads(params)
+                w = 0
+                if start < n:
+                    b = idx[start:start + bs]
+                    w = int(b.numel())
+                    x = states[b]
+                    if x.is_cuda:
+                        x = x.contiguous(memory_format=torch.channels_last)
+                    with torch.autocast("cuda", dtype=torch.bfloat16,
+                                        enabled=self.update_precision == "bf16" and x.is_cuda):
+                        logits, new_values, _ = self.network(x)
+                    logits, new_values = logits.float(), new_values.float()
+                    loss, parts = ppo_loss(logits, new_values.reshape(-1), actions[b], old_logp[b], adv[b], ret[b],
+                                           self.clip_epsilon, self.value_coeff, self.entropy_coeff)
+                    loss.backward()
+                    tot += parts[1:].detach()
+                    updates += 1
+                if multi:
+                    if dist_utils.allreduce_grads(params, weight=w) <= 0:
+                        continue
+                elif w == 0:
+                    continue
                 nn.utils.clip_grad_norm_(params, self.max_grad_norm)
                 self.optimizer.step()
-                tot += parts[1:].detach()
-                updates += 1
         t = (tot / max(updates, 1)).cpu().numpy()
-        return {"solver_policy_loss": float(t[0]), "solver_value_loss": float(t[1]), "solver_entropy": float(t[2])}
+        return {"solver_policy_loss": float(t[0]), "solver_value_loss": float(t[1]), "solver_entropy": float(t[2]),
+                "solver_updates": n_mb * self.ppo_epochs}
 
     # -- batched API ------------------------------------------------------------------
     @torch.no_grad()
@@ -179,9 +205,9 @@ class SolverAgent:  # agents/solver.py:18-259
             fused: Optional[bool] = None):
         """Batched select_action: (action [N], log_prob [N], value [N], hidden).
 
-        fused (default self.fused_inference): run the conv backbone on the fused bf16-MFMA
-        HIP kernel (heist_solver_features) where the grid is supported; False keeps the
-        reference fp32 forward."""
+        fused (default: rollout_precision == "bf16") runs select_action on the fused
+        bf16-MFMA HIP kernels where the grid is supported; False keeps the reference fp32
+        forward."""
         self.network.eval()
         use = self.fused_inference if fused is None else fused
         if use and self.network.fused_supported(obs) and self.network.head_supported():
@@ -207,23 +233,44 @@ class SolverAgent:  # agents/solver.py:18-259
         logp = torch.log(p.gather(1, action[:, None]).clamp(eps, 1 - eps)).reshape(-1)
         return action, logp, value.reshape(-1).float(), hidden
 
+    @torch.no_grad()
+    def value(self, obs: torch.Tensor, hidden=None) -> torch.Tensor:
+        """V(s) [N] on the rollout path's precision (the GAE bootstrap at a rollout cut)."""
+        self.network.eval()
+        if self.fused_inference and self.network.fused_supported(obs) and self.network.head_supported():
+            self._act_counter += 1
+            return self.network.act_fused(obs, hidden, self._act_seed, self._act_counter)[2]
+        if self.fused_inference and self.network.fused_supported(obs):
+            return self.network.forward_fused(obs, hidden)[1].reshape(-1).float()
+        return self.network(obs, hidden)[1].reshape(-1).float()
+
+    def rollout_advantages(self, ro: Rollout):
+        """GAE per env column of a [T, N] rollout (heist_gae): (adv, ret), both [T, N].
+        A column cut mid-episode bootstraps from ro.last_value (V(s_T)); a column whose
+        last tick ended an episode masks it (done), as the reference's buffer-end 0 does."""
+        return compute_gae(ro.rewards, ro.values, ro.dones, ro.last_value, self.gamma, self.gae_lambda)
+
     def update_rollout(self, ro: Rollout, minibatch: int = 4096) -> Dict[str, float]:
-        """One PPO update on a [T, N] rollout (GAE per env column, global advantage norm)."""
+        """One PPO update on a [T, N] rollout (GAE per env column, global advantage norm).
+        Collective-safe: with torch.distributed initialised every rank enters the
+        normalisation and the same number of optimizer steps, whatever its sample count."""
         T, N = ro.rewards.shape
-        adv, ret = compute_gae(ro.rewards, ro.values, ro.dones, ro.last_value, self.gamma, self.gae_lambda)
+        adv, ret = self.rollout_advantages(ro)
         sel = None if ro.mask is None else ro.mask.reshape(1, N).expand(T, N).reshape(-1)
         flat = lambda x: x.reshape(T * N, *x.shape[2:])  # noqa: E731
         states, actions, old_logp, adv, ret = flat(ro.obs), flat(ro.actions), flat(ro.logp), flat(adv), flat(ret)
         if sel is not None:
             states, actions, old_logp, adv, ret = (x[sel] for x in (states, actions, old_logp, adv, ret))
         n = adv.shape[0]
-        if n == 0:
+        if n == 0 and not dist_utils.is_multi():
             return {"solver_loss": 0.0}
         adv = normalize_advantages(adv)
         gen = torch.Generator(device=self.device)
         gen.manual_seed(int(torch.randint(0, 2 ** 31, (1,)).item()))
         perm = lambda k: torch.randperm(k, device=self.device, generator=gen)  # noqa: E731
-        return self._ppo_epochs(states, actions, old_logp, adv, ret, n, perm, minibatch=minibatch)
+        m = self._ppo_epochs(states, actions, old_logp, adv, ret, n, perm, minibatch=minibatch)
+        m["solver_samples"] = n
+        return m
 
     # -- checkpoints ---------------------------------------------------------------------
     def save(self, path: str):  # agents/solver.py:246-252 dict format
@@ -235,3 +282,8 @@ class SolverAgent:  # agents/solver.py:18-259
         self.network.load_state_dict(ck["network"])
         self.optimizer.load_state_dict(ck["optimizer"])
         self.episode_count = ck.get("episode_count", 0)
+
+
+# normalize_advantages over one rank's buffer even inside a process group (the
+# reference-API update() is per-agent, not data-parallel)
+_LOCAL = "local"

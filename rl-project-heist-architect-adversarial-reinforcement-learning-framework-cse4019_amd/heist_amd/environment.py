@@ -38,6 +38,38 @@ class EnvironmentConfig:  # environment.py:18-37
             self.vault_pos = (self.grid_rows - 2, self.grid_cols - 2)
 
 
+def accept_layout(walls, cameras, guards, cfg: EnvironmentConfig, budget: int):
+    """The placements set_layout accepts (environment.py:102-152: walls and cameras on
+    interior EMPTY tiles, guards unchecked at patrol_path[0], each while the budget
+    lasts) as the reference's Wall / Camera / Guard objects, plus the resulting grid.
+    Host bookkeeping for frames and attributes; heist_set_layout does the same on the GPU."""
+    R, C = cfg.grid_rows, cfg.grid_cols
+    g = create_empty_grid(R, C)
+    g[cfg.start_pos] = TileType.START
+    g[cfg.vault_pos] = TileType.VAULT
+    b = BudgetManager(total_budget=budget)
+    ok = lambda r, c: 0 < r < R - 1 and 0 < c < C - 1 and g[r, c] == TileType.EMPTY  # noqa: E731
+    ws, cs, gs = [], [], []
+    for r, c in walls:
+        if ok(r, c) and b.purchase("wall"):
+            g[r, c] = TileType.WALL
+            ws.append(Wall(r, c))
+    for cd in cameras:
+        r, c = cd["row"], cd["col"]
+        if ok(r, c) and b.purchase("camera"):
+            g[r, c] = TileType.CAMERA
+            cs.append(Camera(row=r, col=c, fov_angle=cd.get("fov_angle", 60.0), heading=cd.get("heading", 0.0),
+                             rotation_speed=cd.get("rotation_speed", 15.0), vision_range=cd.get("vision_range", 6)))
+    for gd in guards:
+        path = gd["patrol_path"]
+        if path and b.purchase("guard"):
+            gu = Guard(patrol_path=list(path), speed=gd.get("speed", 1), vision_range=gd.get("vision_range", 4),
+                       fov_angle=gd.get("fov_angle", 90.0))
+            g[gu.row, gu.col] = TileType.GUARD
+            gs.append(gu)
+    return ws, cs, gs, g
+
+
 class HeistEnvironment:
     """The reference's single-environment API backed by the GPU kernels."""
 
@@ -86,33 +118,8 @@ class HeistEnvironment:
 
     def _mirror_layout(self, walls, cameras, guards):
         """Rebuild the reference's Wall/Camera/Guard lists with its acceptance rules."""
-        cfg = self.config
-        R, C = cfg.grid_rows, cfg.grid_cols
-        g = create_empty_grid(R, C)
-        g[cfg.start_pos] = TileType.START
-        g[cfg.vault_pos] = TileType.VAULT
-        b = BudgetManager(total_budget=self.budget.total_budget)
-        ok = lambda r, c: 0 < r < R - 1 and 0 < c < C - 1 and g[r, c] == TileType.EMPTY  # noqa: E731
-        self.walls, self.cameras, self.guards = [], [], []
-        for r, c in walls:
-            if ok(r, c) and b.purchase("wall"):
-                g[r, c] = TileType.WALL
-                self.walls.append(Wall(r, c))
-        for cd in cameras:
-            r, c = cd["row"], cd["col"]
-            if ok(r, c) and b.purchase("camera"):
-                g[r, c] = TileType.CAMERA
-                self.cameras.append(Camera(row=r, col=c, fov_angle=cd.get("fov_angle", 60.0),
-                                           heading=cd.get("heading", 0.0),
-                                           rotation_speed=cd.get("rotation_speed", 15.0),
-                                           vision_range=cd.get("vision_range", 6)))
-        for gd in guards:
-            path = gd["patrol_path"]
-            if path and b.purchase("guard"):
-                gu = Guard(patrol_path=list(path), speed=gd.get("speed", 1), vision_range=gd.get("vision_range", 4),
-                           fov_angle=gd.get("fov_angle", 90.0))
-                g[gu.row, gu.col] = TileType.GUARD
-                self.guards.append(gu)
+        self.walls, self.cameras, self.guards, _ = accept_layout(walls, cameras, guards, self.config,
+                                                                 self.budget.total_budget)
 
     def is_level_valid(self) -> bool:  # environment.py:154-158
         from .utils import bfs_path_exists

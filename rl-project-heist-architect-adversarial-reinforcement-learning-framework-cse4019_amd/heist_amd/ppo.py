@@ -34,7 +34,8 @@ def normalize_advantages(adv: torch.Tensor, eps: float = 1e-8, group=None, inpla
     """(adv - mean) / (std + eps) with unbiased std (agents/solver.py:146-147).
 
     With torch.distributed initialised (or `group` given) the moments are global over
-    all ranks: two tiny all-reduces of float64 sums, nothing else crosses the wire.
+    all ranks: two tiny all-reduces of float64 sums, nothing else crosses the wire; a
+    rank with an empty buffer still takes part.  group="local": this rank's buffer only.
     """
     x = adv if inplace else adv.clone()
     x = x.contiguous()
@@ -43,7 +44,10 @@ def normalize_advantages(adv: torch.Tensor, eps: float = 1e-8, group=None, inpla
     acc = torch.zeros(3, dtype=torch.float64, device=x.device)
     st = nat.stream(x.device)
     dist = torch.distributed
-    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    if group == "local":  # this rank's buffer only, even inside a process group
+        multi, group = False, None
+    else:
+        multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
     if not multi:
         nat.check(nat.lib().heist_adv_normalize(nat.ptr(flat), n, nat.ptr(acc), float(eps), st), "heist_adv_normalize")
         return x

@@ -8,12 +8,20 @@ GPU (and N per rank across GPUs):
   * every env holds its own Architect layout and counts its attempts; after an env's
     A-th attempt its layout is scored (solve/detect/timeout rates -> RewardCalculator)
     and replaced by a fresh Architect sample (masked heist_set_layout + heist_reset);
-  * the Solver steps all envs for `rollout_len` ticks (batched policy forward on
-    PyTorch-ROCm, heist_step with in-kernel auto-reset, per-env LSTM state zeroed when
-    an attempt ends), then does one PPO update on the [T, N] rollout (heist_gae,
-    global advantage normalisation, heist_ppo_loss; one flat gradient all-reduce per
-    optimizer step across ranks);
-  * the Architect updates once per rollout on the layouts scored during it.
+  * the Solver steps all envs for `rollout_len` ticks (batched policy forward, heist_step
+    with in-kernel auto-reset writing each tick's observation straight into the rollout
+    buffer, per-env LSTM state zeroed when an attempt ends), then does one PPO update on
+    the [T, N] rollout: heist_gae per env column, bootstrapping V(s_T) where the rollout
+    cuts an attempt (the reference's buffer always ends on done, so its 0 bootstrap is
+    this with no cut), global advantage normalisation, heist_ppo_loss;
+  * the Architect updates once per rollout on the (log_prob, value, reward) of the
+    layouts scored during it (or, architect_update="per_layout", one reference-style
+    single-reward step per layout in episode order).
+Data parallel (one process per GPU, torch.distributed): every collective is called the
+same number of times on every rank -- the Solver's minibatch count is agreed by a max
+all-reduce, the Architect's statistics are all-reduced, episode numbers are handed out
+in rank order from a global counter, so the curriculum phase, checkpoint cadence and the
+end of train() are the same decision on every rank (dist_utils).
 Episode numbering, the curriculum, GameLogEntry / TrainingMetrics JSON and checkpoint
 file names follow the reference, so its dashboard and resume logic read our logs.
 A layout may see a few extra attempts beyond A before the rollout ends; those train
@@ -26,14 +34,15 @@ import re
 import time
 from collections import deque
 from datetime import datetime
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Sequence, Tuple, Union
 
 import numpy as np
 import torch
 
+from . import dist_utils
 from .agents.architect import ArchitectAgent
 from .agents.solver import Rollout, SolverAgent
-from .environment import EnvironmentConfig, HeistEnvironment
+from .environment import EnvironmentConfig, HeistEnvironment, accept_layout
 from .rewards import RewardCalculator
 from .utils import DEVICE
 from .vec_env import STATUS_CODES, HeistEnv
@@ -81,6 +90,21 @@ class TrainingMetrics:  # training.py:71-112
             with open(path) as f:
                 self.history = json.load(f)
 
+    def records(self) -> List[Dict]:
+        """Per-episode rows (the inverse of log); keys missing for an episode are absent."""
+        eps = self.history.get("episode", [])
+        cols = {k: v for k, v in self.history.items() if k != "episode"}
+        # the reference logs only the keys an episode's metrics carry (invalid layouts have
+        # no losses), so per-key lists can be shorter than "episode": align them from the end
+        return [{"episode": e} for e in eps] if not cols else _rows(eps, cols)
+
+    @classmethod
+    def from_records(cls, rows: List[Dict]) -> "TrainingMetrics":
+        m = cls()
+        for r in sorted(rows, key=lambda r: r["episode"]):
+            m.log(r["episode"], {k: v for k, v in r.items() if k != "episode"})
+        return m
+
     def get_summary(self, last_n: int = 10) -> str:
         lines = []
         for key in ("solve_rate", "detection_rate", "architect_reward", "solver_reward"):
@@ -90,20 +114,30 @@ class TrainingMetrics:  # training.py:71-112
         return "\n".join(lines)
 
 
+CURRICULA = {
+    # (episode_threshold, budget, allow_cameras, allow_guards, description)
+    "reference": [(0, 5, False, False, "Walls Only"),  # training.py:128-133
+                  (80, 8, True, False, "Walls + Cameras"),
+                  (200, 15, True, True, "Full Security"),
+                  (400, 22, True, True, "Expert")],
+    # BASELINE config 4: the full adversarial curriculum over budgets 10 -> 40
+    "c4": [(0, 10, False, False, "Walls Only"),
+           (80, 20, True, False, "Walls + Cameras"),
+           (200, 30, True, True, "Full Security"),
+           (400, 40, True, True, "Expert")],
+}
+
+
 class AdversarialTrainer:  # training.py:115-790
-    CURRICULUM = [  # (episode_threshold, budget, allow_cameras, allow_guards, description)
-        (0, 5, False, False, "Walls Only"),
-        (80, 8, True, False, "Walls + Cameras"),
-        (200, 15, True, True, "Full Security"),
-        (400, 22, True, True, "Expert"),
-    ]
+    CURRICULUM = CURRICULA["reference"]
     WARMUP_EPISODES = 30
 
     def __init__(self, config: Optional[EnvironmentConfig] = None, solver_episodes_per_layout: int = 20,
                  total_episodes: int = 500, save_dir: str = "checkpoints", log_dir: str = "logs",
                  architect_lr: float = 3e-4, solver_lr: float = 1e-3, n_envs: int = 256,
                  rollout_len: Optional[int] = None, minibatch: int = 4096, device=None, max_budget: Optional[int] = None,
-                 seed: Optional[int] = None, update_precision: str = "fp32"):
+                 seed: Optional[int] = None, update_precision: str = "fp32", rollout_precision: str = "fp32",
+                 curriculum: Union[str, Sequence[Tuple], None] = None, architect_update: str = "batched"):
         self.config = config or EnvironmentConfig()
         self.solver_episodes = solver_episodes_per_layout
         self.total_episodes = total_episodes
@@ -113,6 +147,15 @@ class AdversarialTrainer:  # training.py:115-790
         self.n_envs = n_envs
         self.rollout_len = rollout_len or self.config.max_steps
         self.minibatch = minibatch
+        if isinstance(curriculum, str):
+            if curriculum not in CURRICULA:
+                raise ValueError("unknown curriculum %r (presets: %s)" % (curriculum, ", ".join(CURRICULA)))
+            curriculum = CURRICULA[curriculum]
+        if curriculum is not None:
+            self.CURRICULUM = [tuple(p) for p in curriculum]
+        if architect_update not in ("batched", "per_layout"):
+            raise ValueError("architect_update must be 'batched' or 'per_layout'")
+        self.architect_update = architect_update
         if seed is not None:
             torch.manual_seed(seed)
             np.random.seed(seed)
@@ -124,7 +167,16 @@ class AdversarialTrainer:  # training.py:115-790
         self.architect = ArchitectAgent(grid_rows=R, grid_cols=C, budget=self.config.architect_budget,
                                         lr=architect_lr, device=self.device)
         self.solver = SolverAgent(grid_rows=R, grid_cols=C, lr=solver_lr, device=self.device,
-                                  update_precision=update_precision)
+                                  update_precision=update_precision, rollout_precision=rollout_precision)
+        if dist_utils.is_multi():  # replicas start equal: rank 0's initial weights everywhere
+            ts = [t for net in (self.architect.network, self.solver.network)
+                  for t in list(net.parameters()) + list(net.buffers())]
+            flat = torch.cat([t.detach().reshape(-1).float() for t in ts])
+            torch.distributed.broadcast(flat, 0)
+            o = 0
+            for t in ts:
+                t.data.copy_(flat[o:o + t.numel()].view(t.shape))
+                o += t.numel()
         self.reward_calc = RewardCalculator()
         self.metrics = TrainingMetrics()
         self.game_log: List[GameLogEntry] = []
@@ -132,6 +184,9 @@ class AdversarialTrainer:  # training.py:115-790
         self.current_state = None
         self.training_active = False
         self._single_env = None
+        self._callback = None
+        self._trace = None  # list: _rollout appends (actions, reward64, done, status) per tick
+        self._arch_eps: List[int] = []  # episode number of each Architect buffer transition
         os.makedirs(save_dir, exist_ok=True)
         os.makedirs(log_dir, exist_ok=True)
         self._init_batch_state()
@@ -143,8 +198,11 @@ class AdversarialTrainer:  # training.py:115-790
         self.b_attempts, self.b_solve, self.b_detect, self.b_timeout, self.b_steps = z(), z(), z(), z(), z()
         self.b_reward = z(torch.float64)
         self.b_valid = torch.zeros(n, dtype=torch.bool, device=d)
+        self.b_logp = z(torch.float32)   # the layout's Architect log-prob and value (agents/architect.py:75-81)
+        self.b_value = z(torch.float32)
         self.b_episode = np.zeros(n, np.int64)
         self.b_meta = [None] * n  # (phase, budget, walls, cameras, guards, temperature)
+        self.b_layout = [None] * n  # (LayoutBatch sized n, row) of the env's current layout; None: empty
         self.b_scored = torch.zeros(n, dtype=torch.bool, device=d)
         self.h = torch.zeros(1, n, self.solver.network.lstm_hidden, device=d)
         self.c = torch.zeros_like(self.h)
@@ -160,43 +218,63 @@ class AdversarialTrainer:  # training.py:115-790
     def _temperature(self, episode: int) -> float:  # training.py:451
         return max(0.5, 2.0 - episode / max(self.total_episodes, 1) * 1.5)
 
-    def _assign_layouts(self, env_ids: np.ndarray, overrides: Optional[dict] = None, empty: bool = False):
+    def _assign_layouts(self, env_ids, overrides: Optional[dict] = None, empty: bool = False):
         """New Architect layouts for env_ids (one episode number each); invalid layouts are
-        scored -1 and resampled, as the reference skips their solver phase."""
+        scored -1 and resampled, as the reference skips their solver phase.  Collective:
+        every rank calls it once per iteration (with any number of env ids, also none);
+        episode numbers come from the global counter in rank order, and the curriculum
+        phase of a round is that of its first global episode, the same on every rank."""
         ov = overrides or {}
         pending = np.asarray(env_ids, np.int64)
-        tries = 0
-        while len(pending):
-            ep0 = self.global_episode + 1
+        rk = dist_utils.rank()
+        for tries in range(8):
+            counts = dist_utils.allgather_counts(len(pending), self.device).numpy()
+            total = int(counts.sum())
+            if total == 0:
+                break
+            ep_first = self.global_episode + 1
+            ep0 = self.global_episode + int(counts[:rk].sum()) + 1
+            self.global_episode += total
+            if len(pending) == 0:
+                continue
             eps = np.arange(ep0, ep0 + len(pending))
-            self.global_episode += len(pending)
-            _, budget, cams, guards, desc = self.get_curriculum_phase(int(eps[0]))
+            _, budget, cams, guards, desc = self.get_curriculum_phase(ep_first)
             budget = ov.get("budget", budget)
             cams = ov.get("allow_cameras", cams)
             guards = ov.get("allow_guards", guards)
-            temp = ov.get("temperature", self._temperature(int(eps[0])))
+            temp = ov.get("temperature", self._temperature(ep_first))
             phase = ov.get("phase", desc)
+            pidx = torch.as_tensor(pending, device=self.device)
             if empty:
                 layouts = [([], [], [])] * len(pending)
-                valid = self.env.set_layouts(layouts, budget=budget, env_ids=pending)[torch.as_tensor(pending)]
-                counts = np.zeros((len(pending), 3), np.int64)
+                valid = self.env.set_layouts(layouts, budget=budget, env_ids=pending)[pidx]
+                counts_l = np.zeros((len(pending), 3), np.int64)
+                lb = None
             else:
                 self.architect.budget = budget
-                lb, _, _ = self.architect.generate_layouts(len(pending), temp, cams, guards, env=self.env,
-                                                           record=not ov.get("freeze_architect", False))
-                lb = _scatter_layout(lb, pending, self.env)
-                valid = self.env.set_layout_batch(lb, _mask(pending, self.env))[torch.as_tensor(pending)]
-                counts = torch.stack([lb.n_walls, lb.n_cams, lb.n_guards], 1)[torch.as_tensor(pending)].cpu().numpy()
+                lbk, logp, value = self.architect.generate_layouts(len(pending), temp, cams, guards, env=self.env,
+                                                                   record=False)
+                lb = _scatter_layout(lbk, pending, self.env)
+                valid = self.env.set_layout_batch(lb, _mask(pending, self.env))[pidx]
+                counts_l = torch.stack([lbk.n_walls, lbk.n_cams, lbk.n_guards], 1).cpu().numpy()
+                self.b_logp[pidx] = logp.float()
+                self.b_value[pidx] = value.reshape(-1)[0].float()
             v = valid.cpu().numpy()
             for i, e in enumerate(pending):
                 self.b_episode[e] = eps[i]
-                self.b_meta[e] = (phase, budget, int(counts[i, 0]), int(counts[i, 1]), int(counts[i, 2]), temp)
+                self.b_meta[e] = (phase, budget, int(counts_l[i, 0]), int(counts_l[i, 1]), int(counts_l[i, 2]), temp)
+                self.b_layout[e] = None if lb is None else (lb, int(e))
             bad = pending[~v]
-            for i in np.nonzero(~v)[0]:  # training.py:476-504
+            if len(bad) and not empty and not ov.get("freeze_architect", False):  # training.py:476-504
+                bi = torch.as_tensor(bad, device=self.device)
+                self.architect.store_transitions(self.b_logp[bi], self.b_value[bi],
+                                                 [self.reward_calc.architect_invalid] * len(bad))
+                self._arch_eps.extend(int(x) for x in eps[~v])
+            for i in np.nonzero(~v)[0]:
                 r = self.reward_calc.architect_invalid
-                if not empty and not ov.get("freeze_architect", False):
-                    self.architect.store_reward(r)
-                self._log_episode(int(eps[i]), phase, budget, counts[i], 0.0, 0.0, 1.0, r, 0.0, 0.0, False, temp, ov)
+                m = {"solve_rate": 0.0, "detection_rate": 0.0, "timeout_rate": 1.0, "architect_reward": r,
+                     "solver_reward": 0.0, "avg_steps": 0, "budget": budget, "phase": phase}
+                self._log_episode(int(eps[i]), m, counts_l[i], False, temp, ov, env_id=int(pending[i]))
             good = pending[v]
             if len(good):
                 m = _mask(good, self.env)
@@ -209,14 +287,17 @@ class AdversarialTrainer:  # training.py:115-790
                 self.c[:, mb] = 0.0
                 self.b_valid[mb] = True
                 self.b_scored[mb] = False
-            tries += 1
-            pending = bad if tries < 8 else np.zeros(0, np.int64)
-            if len(bad) and tries >= 8:
+            pending = bad if tries < 7 else np.zeros(0, np.int64)
+            if len(bad) and tries >= 7:
                 self.b_valid[torch.as_tensor(bad, device=self.device)] = False
 
     # -- rollout / scoring ------------------------------------------------------------------
     @torch.no_grad()
     def _rollout(self, T: int) -> Rollout:
+        """T ticks of all envs.  The observation each tick's action is chosen from is
+        obs[t]; heist_step writes the next one straight into obs[t + 1] (the last into
+        env.obs), so no per-tick copy.  last_value = V(s_T) under the carried LSTM state
+        (zeroed where an attempt just ended; those columns are masked by done anyway)."""
         env, n, d = self.env, self.n_envs, self.device
         obs_buf = torch.empty((T, n) + tuple(env.obs.shape[1:]), dtype=torch.float32, device=d)
         act_buf = torch.empty((T, n), dtype=torch.int64, device=d)
@@ -225,17 +306,19 @@ class AdversarialTrainer:  # training.py:115-790
         r_buf = torch.empty((T, n), dtype=torch.float32, device=d)
         d_buf = torch.empty((T, n), dtype=torch.uint8, device=d)
         A = self.solver_episodes
-        vault, det, tmo = STATUS_CODES["vault_reached"], STATUS_CODES["detected"], STATUS_CODES["timeout"]
+        vault, det = STATUS_CODES["vault_reached"], STATUS_CODES["detected"]
+        obs_buf[0].copy_(env.obs)
         for t in range(T):
-            obs_buf[t].copy_(env.obs)
-            a, lp, v, (self.h, self.c) = self.solver.act(env.obs, (self.h, self.c))
+            a, lp, v, (self.h, self.c) = self.solver.act(obs_buf[t], (self.h, self.c))
             act_buf[t], lp_buf[t], v_buf[t] = a, lp, v
-            _, rew, done, status = env.step(a)
+            _, rew, done, status = env.step(a, obs_out=obs_buf[t + 1] if t + 1 < T else None)
             r_buf[t] = rew
             d_buf[t] = done.to(torch.uint8)
+            if self._trace is not None:
+                self._trace.append((a.clone(), env.reward64.clone(), done.clone(), status.clone()))
             counting = self.b_valid & (self.b_attempts < A)
             self.b_steps += counting.int()
-            self.b_reward += torch.where(counting, rew.double(), torch.zeros_like(self.b_reward))
+            self.b_reward += torch.where(counting, env.reward64, torch.zeros_like(self.b_reward))
             fin = counting & done
             st = status.to(torch.int32)
             self.b_solve += (fin & (st == vault)).int()
@@ -245,7 +328,9 @@ class AdversarialTrainer:  # training.py:115-790
             keep = (~done).to(self.h.dtype).reshape(1, n, 1)  # a new attempt starts with a fresh LSTM state
             self.h = self.h * keep
             self.c = self.c * keep
-        return Rollout(obs_buf, act_buf, lp_buf, v_buf, r_buf, d_buf, mask=self.b_valid.clone())
+        last_value = self.solver.value(env.obs, (self.h, self.c))
+        return Rollout(obs_buf, act_buf, lp_buf, v_buf, r_buf, d_buf, mask=self.b_valid.clone(),
+                       last_value=last_value)
 
     def _score_finished(self, overrides: Optional[dict] = None) -> np.ndarray:
         """Score every env whose layout has had its A attempts; returns those env ids."""
@@ -258,46 +343,78 @@ class AdversarialTrainer:  # training.py:115-790
         rews = self.b_reward[fin].cpu().numpy()
         ov = overrides or {}
         ids = fin.cpu().numpy()
+        ars = []
         for i, e in enumerate(ids):
             s, dt, to, steps = stats[i]
             solve_rate, det_rate, to_rate = s / A, dt / A, to / A
             ar = self.reward_calc.architect_reward_from_rate(True, solve_rate)  # rewards.py:43-73
-            if not ov.get("freeze_architect", False) and not self.warmup:
-                self.architect.store_reward(ar)
+            ars.append(ar)
             phase, budget, nw, nc, ng, temp = self.b_meta[e]
-            self._log_episode(int(self.b_episode[e]), phase, budget, (nw, nc, ng), solve_rate, det_rate, to_rate, ar,
-                              rews[i] / A, steps / A, True, temp, ov)
+            m = {"solve_rate": solve_rate, "detection_rate": det_rate, "timeout_rate": to_rate, "architect_reward": ar,
+                 "solver_reward": rews[i] / A, "architect_loss": 0, "solver_loss": 0, "avg_steps": steps / A,
+                 "budget": budget, "phase": phase}
+            self._log_episode(int(self.b_episode[e]), m, (nw, nc, ng), True, temp, ov, env_id=int(e))
+        if not ov.get("freeze_architect", False) and not self.warmup:
+            self.architect.store_transitions(self.b_logp[fin], self.b_value[fin], ars)
+            self._arch_eps.extend(int(self.b_episode[e]) for e in ids)
         self.b_scored[fin] = True
         return ids
 
-    def _log_episode(self, episode, phase, budget, counts, solve, detect, timeout, arch_r, solver_r, avg_steps,
-                     valid, temp, ov):
+    def _log_episode(self, episode, m, counts, valid, temp, ov, env_id=None):
         if self.warmup:
             return
-        m = {"solve_rate": solve, "detection_rate": detect, "timeout_rate": timeout, "architect_reward": arch_r,
-             "solver_reward": solver_r, "architect_loss": 0, "solver_loss": 0, "avg_steps": avg_steps,
-             "budget": budget, "phase": phase}
         self.metrics.log(episode, m)
-        self.metrics.recent_solve_rates.append(solve)
-        self.game_log.append(GameLogEntry(episode=episode, phase=phase, budget=budget, walls=int(counts[0]),
-                                          cameras=int(counts[1]), guards=int(counts[2]), solve_rate=solve,
-                                          detection_rate=detect, timeout_rate=timeout, architect_reward=arch_r,
-                                          solver_reward=solver_r, avg_steps=avg_steps, level_valid=valid,
-                                          is_interactive=bool(ov.get("interactive", False)),
-                                          freeze_architect=bool(ov.get("freeze_architect", False)),
-                                          freeze_solver=bool(ov.get("freeze_solver", False)), temperature=temp))
+        self.metrics.recent_solve_rates.append(m["solve_rate"])
+        entry = GameLogEntry(episode=episode, phase=m["phase"], budget=m["budget"], walls=int(counts[0]),
+                             cameras=int(counts[1]), guards=int(counts[2]), solve_rate=m["solve_rate"],
+                             detection_rate=m["detection_rate"], timeout_rate=m["timeout_rate"],
+                             architect_reward=m["architect_reward"], solver_reward=m["solver_reward"],
+                             avg_steps=m["avg_steps"], level_valid=valid,
+                             is_interactive=bool(ov.get("interactive", False)),
+                             freeze_architect=bool(ov.get("freeze_architect", False)),
+                             freeze_solver=bool(ov.get("freeze_solver", False)), temperature=temp)
+        self.game_log.append(entry)
+        if self._callback is not None:  # training.py:383-384: (episode, ep_metrics, env_state)
+            self.current_state = self.environment_state(env_id) if env_id is not None else None
+            self._callback(episode, m, self.current_state)
 
-    def train_iteration(self, overrides: Optional[dict] = None) -> Dict[str, float]:
-        """One rollout of rollout_len ticks over all envs + the agents' updates."""
+    def _architect_step(self) -> Dict[str, float]:
+        if self.architect_update == "batched":
+            return self.architect.update()
+        # per_layout: the reference's cadence, one single-reward update per layout in episode
+        # order (agents/architect.py:91-155 with len(rewards) == 1); every rank replays the
+        # union of all ranks' layouts, so no gradient crosses the wire and replicas stay equal
+        A = self.architect
+        k = min(len(A.rewards), len(A.log_probs), len(A.values))
+        rows = torch.zeros((k, 4), dtype=torch.float64, device=self.device)
+        if k:
+            rows[:, 0] = torch.stack(A.log_probs[:k]).double().reshape(-1)
+            rows[:, 1] = torch.stack([v.squeeze() for v in A.values[:k]]).double().reshape(-1)
+            rows[:, 2] = torch.tensor(A.rewards[:k], dtype=torch.float64, device=self.device)
+            rows[:, 3] = torch.as_tensor(self._arch_eps[:k], dtype=torch.float64, device=self.device)
+        allrows, _ = dist_utils.allgather_rows(rows, self.device)
+        A._clear()
+        out = {}
+        for r in allrows[torch.argsort(allrows[:, 3])].tolist():
+            A.log_probs.append(torch.tensor(r[0], dtype=torch.float32, device=self.device))
+            A.values.append(torch.tensor(r[1], dtype=torch.float32, device=self.device))
+            A.rewards.append(r[2])
+            out = A.update(collective=False)
+        return out
+
+    def train_iteration(self, overrides: Optional[dict] = None, reassign: bool = True) -> Dict[str, float]:
+        """One rollout of rollout_len ticks over all envs + the agents' updates.
+        Collective inside a process group (every rank calls it with the same overrides)."""
         ov = overrides or {}
         ro = self._rollout(self.rollout_len)
         out = {}
         if not ov.get("freeze_solver", False):
             out.update(self.solver.update_rollout(ro, minibatch=self.minibatch))
         done_ids = self._score_finished(ov)
-        if len(done_ids) and not self.warmup and not ov.get("freeze_architect", False) and self.architect.rewards:
-            out.update(self.architect.update())
-        if len(done_ids):
+        if not self.warmup and not ov.get("freeze_architect", False):
+            out.update(self._architect_step())
+            self._arch_eps = []
+        if reassign:
             self._assign_layouts(done_ids, ov, empty=self.warmup)
         out["layouts_scored"] = len(done_ids)
         return out
@@ -314,49 +431,109 @@ class AdversarialTrainer:  # training.py:115-790
         self.warmup = False
 
     def train(self, callback=None, resume: bool = False, warmup_rollouts: int = 2):
+        """training.py:336-416.  callback(episode, ep_metrics, env_state) runs for every
+        scored or invalid layout, as the reference's does per episode."""
         self.training_active = True
         start_episode = self.resume_from_checkpoint() if resume else 0
         self.global_episode = start_episode
         if start_episode == 0:
             self._run_warmup(warmup_rollouts)
         self._init_batch_state()
-        self._assign_layouts(np.arange(self.n_envs))
-        t0 = time.time()
-        next_ckpt = start_episode + 50
-        while self.global_episode < start_episode + self.total_episodes:
-            m = self.train_iteration()
-            if callback:
-                callback(self.global_episode, m, None)
-            if self.global_episode >= next_ckpt:
-                self._save_checkpoint(self.global_episode)
-                next_ckpt += 50
-        self._save_checkpoint(self.global_episode)
-        self._save_game_log()
-        self.metrics.save(os.path.join(self.log_dir, "training_metrics.json"))
-        self.training_active = False
+        self._callback = callback
+        try:
+            self._assign_layouts(np.arange(self.n_envs))
+            t0 = time.time()
+            next_ckpt = start_episode + 50
+            while self.global_episode < start_episode + self.total_episodes:  # a global count: same on every rank
+                self.train_iteration()
+                if self.global_episode >= next_ckpt:
+                    self._save_checkpoint(self.global_episode)
+                    next_ckpt += 50
+            self._save_checkpoint(self.global_episode)
+        finally:
+            self._callback = None
+            self.training_active = False
         return time.time() - t0
 
     def run_interactive_episodes(self, num_episodes: int = 1, budget: int = 15, freeze_architect: bool = False,
                                  freeze_solver: bool = False, temperature: float = 1.0, solver_attempts: int = 20,
                                  allow_cameras: bool = True, allow_guards: bool = True, callback=None) -> List[Dict]:
+        """training.py:606-663: num_episodes layouts under the given overrides (spread over
+        ranks), played while every other env sits out (masked: not trained, not scored);
+        afterwards the interactive envs get fresh curriculum layouts and the others resume.
+        Returns the episodes' ep_metrics dicts, in episode order."""
         ov = dict(budget=budget, freeze_architect=freeze_architect, freeze_solver=freeze_solver,
                   temperature=temperature, allow_cameras=allow_cameras, allow_guards=allow_guards, interactive=True,
                   phase="Interactive (budget=%d)" % budget)
+        w, rk = dist_utils.world_size(), dist_utils.rank()
+        mine = min(num_episodes // w + (1 if rk < num_episodes % w else 0), self.n_envs)
         saved_a = self.solver_episodes
+        saved_valid = self.b_valid.clone()
         self.solver_episodes = solver_attempts
+        ids = np.arange(mine)
+        others = torch.ones(self.n_envs, dtype=torch.bool, device=self.device)
+        others[torch.as_tensor(ids, device=self.device)] = False
+        self.b_valid &= ~others
         n0 = len(self.game_log)
-        self._assign_layouts(np.arange(min(num_episodes, self.n_envs)), ov)
-        while len(self.game_log) - n0 < num_episodes:
-            self.train_iteration(ov)
-        self.solver_episodes = saved_a
-        results = [e.to_dict() for e in self.game_log[n0:n0 + num_episodes]]
-        if callback:
-            for r in results:
-                callback(r["episode"], r, None)
+        self._callback = callback
+        try:
+            self._assign_layouts(ids, ov)
+            for _ in range(1000):
+                cnt = dist_utils.allreduce_(torch.tensor([len(self.game_log) - n0], device=self.device))
+                if int(cnt.item()) >= num_episodes:
+                    break
+                self.train_iteration(ov, reassign=False)
+                self.b_valid &= ~self.b_scored  # a scored interactive layout sits out until the block ends
+        finally:
+            self._callback = None
+            self.solver_episodes = saved_a
+        mine_log = [e.to_dict() for e in self.game_log[n0:]]
+        allm = self._gather_objects(mine_log)
+        self.b_valid = saved_valid & others
+        self._assign_layouts(ids)
+        results = sorted(allm, key=lambda r: r["episode"])[:num_episodes]
+        keys = ("solve_rate", "detection_rate", "timeout_rate", "architect_reward", "solver_reward", "avg_steps",
+                "budget", "phase")
         self._save_checkpoint(self.global_episode)
-        self._save_game_log()
-        self.metrics.save(os.path.join(self.log_dir, "training_metrics.json"))
-        return results
+        return [{k: r[k] for k in keys} for r in results]
+
+    def environment_state(self, env_id: int) -> Dict:
+        """get_environment_state (environment.py:388-417) of batched env env_id: grid,
+        visibility, solver, cameras and guards from the device; solver_path and
+        detection_events are not tracked by the batched env (single-point path, none)."""
+        cfg = self.config
+        st = self.env.export(grid=True)
+        e = int(env_id)
+        lay = self.b_layout[e]
+        walls, cams, guards = ([], [], []) if lay is None else _lb_rows(lay[0], [lay[1]]).to_lists()[0]
+        budget = self.b_meta[e][1] if self.b_meta[e] else cfg.architect_budget
+        _, cameras, gds, _ = accept_layout(walls, cams, guards, cfg, budget)
+        ch = st["cam_heading"][e].cpu().numpy()
+        gi = st["guard_idx"][e].cpu().numpy()
+        gh = st["guard_heading"][e].cpu().numpy()
+        for k, cam in enumerate(cameras):
+            cam.heading = float(ch[k])
+        for k, g in enumerate(gds):
+            g.current_idx, g.heading = int(gi[k]), float(gh[k])
+        pos = (int(st["pos_r"][e]), int(st["pos_c"][e]))
+        return {"grid": st["grid"][e].cpu().numpy().astype(np.int32).tolist(),
+                "visibility": self.env.obs[e, 1].cpu().numpy().tolist(), "solver_pos": pos, "solver_path": [pos],
+                "vault_pos": cfg.vault_pos, "start_pos": cfg.start_pos, "tick": int(st["tick"][e]),
+                "done": bool(st["done"][e]),
+                "cameras": [{"row": c.row, "col": c.col, "heading": c.heading, "fov_angle": c.fov_angle,
+                             "vision_range": c.vision_range} for c in cameras],
+                "guards": [{"row": g.row, "col": g.col, "heading": g.heading, "patrol_path": g.patrol_path,
+                            "current_idx": g.current_idx} for g in gds],
+                "detection_events": []}
+
+    def layout_lists(self, env_ids) -> List:
+        """The (walls, cameras, guards) lists last assigned to env_ids, in the reference's
+        set_layout format (for replay through the CPU oracle and for frames)."""
+        out = []
+        for e in env_ids:
+            lay = self.b_layout[int(e)]
+            out.append(([], [], []) if lay is None else _lb_rows(lay[0], [lay[1]]).to_lists()[0])
+        return out
 
     def simulate_episode(self, budget: int = 15, solver_attempts: int = 1) -> Dict:  # training.py:713-790
         if self._single_env is None:
@@ -417,13 +594,14 @@ class AdversarialTrainer:  # training.py:115-790
             return False
         self.architect.load(arch)
         self.solver.load(sol)
-        mp = os.path.join(self.log_dir, "training_metrics.json")
-        if os.path.exists(mp):
-            self.metrics.load(mp)
-        lp = os.path.join(self.log_dir, "game_log.json")
-        if os.path.exists(lp):
-            with open(lp) as f:
-                self.game_log = [GameLogEntry(**e) for e in json.load(f)]
+        if dist_utils.rank() == 0:  # the files hold every rank's episodes; one copy is enough
+            mp = os.path.join(self.log_dir, "training_metrics.json")
+            if os.path.exists(mp):
+                self.metrics.load(mp)
+            lp = os.path.join(self.log_dir, "game_log.json")
+            if os.path.exists(lp):
+                with open(lp) as f:
+                    self.game_log = [GameLogEntry(**e) for e in json.load(f)]
         self.global_episode = episode
         return True
 
@@ -436,18 +614,45 @@ class AdversarialTrainer:  # training.py:115-790
     def get_game_log(self) -> List[Dict]:
         return [e.to_dict() for e in self.game_log]
 
+    def _gather_objects(self, items: List) -> List:
+        """Concatenate every rank's list (all_gather_object); the local list on one rank."""
+        if not dist_utils.is_multi():
+            return list(items)
+        out = [None] * dist_utils.world_size()
+        torch.distributed.all_gather_object(out, list(items))
+        return [x for part in out for x in part]
+
     def _save_game_log(self):
-        with open(os.path.join(self.log_dir, "game_log.json"), "w") as f:
-            json.dump([e.to_dict() for e in self.game_log], f, indent=2)
+        entries = sorted(self._gather_objects(self.get_game_log()), key=lambda e: e["episode"])
+        if dist_utils.rank() == 0:
+            with open(os.path.join(self.log_dir, "game_log.json"), "w") as f:
+                json.dump(entries, f, indent=2)
+
+    def _save_metrics(self):
+        if dist_utils.is_multi():
+            m = TrainingMetrics.from_records(self._gather_objects(self.metrics.records()))
+        else:
+            m = self.metrics
+        if dist_utils.rank() == 0:
+            m.save(os.path.join(self.log_dir, "training_metrics.json"))
 
     def _save_checkpoint(self, episode: int):
-        dist = torch.distributed
-        if dist.is_available() and dist.is_initialized() and dist.get_rank() != 0:
-            return
-        self.architect.save(os.path.join(self.save_dir, "architect_ep%d.pt" % episode))
-        self.solver.save(os.path.join(self.save_dir, "solver_ep%d.pt" % episode))
-        self.metrics.save(os.path.join(self.log_dir, "training_metrics.json"))
+        """training.py:700-711 + the JSON logs.  Collective: the logs of all ranks are
+        merged by episode and rank 0 writes them (the replicas' weights are equal)."""
+        if dist_utils.rank() == 0:
+            self.architect.save(os.path.join(self.save_dir, "architect_ep%d.pt" % episode))
+            self.solver.save(os.path.join(self.save_dir, "solver_ep%d.pt" % episode))
+        self._save_metrics()
         self._save_game_log()
+
+
+def _rows(eps, cols):
+    rows = [{"episode": e} for e in eps]
+    for k, v in cols.items():
+        off = len(eps) - len(v)
+        for i, x in enumerate(v):
+            rows[off + i][k] = x
+    return rows
 
 
 def _mask(ids, env) -> torch.Tensor:
@@ -456,14 +661,24 @@ def _mask(ids, env) -> torch.Tensor:
     return m
 
 
+_LB_KEYS = ("wall_rc", "n_walls", "cam_params", "n_cams", "guard_paths", "guard_meta", "guard_fov", "n_guards",
+            "budget")
+
+
+def _lb_rows(lb, ids):
+    """Rows `ids` of a LayoutBatch."""
+    from .vec_env import LayoutBatch
+    idx = torch.as_tensor(np.asarray(ids, np.int64), device=lb.n_walls.device)
+    return LayoutBatch(**{k: getattr(lb, k)[idx] for k in _LB_KEYS})
+
+
 def _scatter_layout(lb, ids, env):
     """Place a LayoutBatch of len(ids) layouts at rows `ids` of an env-sized batch."""
     from .vec_env import LayoutBatch
     n = env.n_envs
     idx = torch.as_tensor(np.asarray(ids, np.int64), device=env.device)
     out = {}
-    for k in ("wall_rc", "n_walls", "cam_params", "n_cams", "guard_paths", "guard_meta", "guard_fov", "n_guards",
-              "budget"):
+    for k in _LB_KEYS:
         src = getattr(lb, k)
         full = torch.zeros((n,) + tuple(src.shape[1:]), dtype=src.dtype, device=env.device)
         full[idx] = src

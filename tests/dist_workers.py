@@ -38,3 +38,76 @@ def advnorm_worker(rank, world, port, out_dir):
     torch.save((x.cpu(), y.cpu()), os.path.join(out_dir, "a%d.pt" % rank))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def trainer_worker(rank, world, port, out_dir):
+    """AdversarialTrainer.train_iteration x3 on two ranks sharing one GPU (gloo), with
+    unequal valid masks (rank 1 trains on a quarter of its envs, none in iteration 2) and
+    unequal finished-layout counts: every collective must pair up, and both replicas end
+    with bit-identical Solver and Architect parameters."""
+    sys.path[:0] = [p for p in os.environ.get("HEIST_TEST_PATHS", "").split(os.pathsep) if p]
+    _init(rank, world, port, "gloo")
+    import numpy as np
+    from heist_amd import EnvironmentConfig
+    from heist_amd.training import AdversarialTrainer
+    torch.manual_seed(100 + rank)  # different sampling streams per rank; weights come from rank 0
+    cfg = EnvironmentConfig(grid_rows=12, grid_cols=12, max_steps=40)
+    n = 32
+    tr = AdversarialTrainer(cfg, solver_episodes_per_layout=1 + rank, total_episodes=10 ** 6,
+                            save_dir=os.path.join(out_dir, "ck"), log_dir=os.path.join(out_dir, "logs"),
+                            n_envs=n, rollout_len=24 + 8 * rank, minibatch=96, device="cuda:0")
+    tr.global_episode = 200
+    tr._assign_layouts(np.arange(n))
+    scored = []
+    for it in range(3):
+        if rank == 1:
+            keep = torch.zeros(n, dtype=torch.bool, device=tr.device)
+            if it != 1:
+                keep[: n // 4] = True
+            tr.b_valid &= keep
+        out = tr.train_iteration()
+        scored.append(int(out["layouts_scored"]))
+    tr._save_checkpoint(tr.global_episode)
+    eps = [e.to_dict()["episode"] for e in tr.game_log]
+    torch.save({"solver": [p.detach().cpu() for p in tr.solver.network.parameters()],
+                "architect": [p.detach().cpu() for p in tr.architect.network.parameters()],
+                "global_episode": tr.global_episode, "episodes": eps, "scored": scored},
+               os.path.join(out_dir, "t%d.pt" % rank))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def architect_worker(rank, world, port, out_dir):
+    """ArchitectAgent.update() inside a process group on CPU: rank 0 holds 3 transitions,
+    rank 1 none; both step identically on the union's statistics."""
+    sys.path[:0] = [p for p in os.environ.get("HEIST_TEST_PATHS", "").split(os.pathsep) if p]
+    _init(rank, world, port, "gloo")
+    from heist_amd.agents.architect import ArchitectAgent
+    torch.manual_seed(7)
+    ag = ArchitectAgent(grid_rows=10, grid_cols=10, device="cpu")
+    if rank == 0:
+        ag.store_transitions(torch.tensor([-3.0, -4.0, -5.0]), torch.tensor([0.1, 0.1, 0.1]), [1.0, -1.0, 0.5])
+    m = ag.update()
+    torch.save({"params": [p.detach().clone() for p in ag.network.parameters()], "m": m},
+               os.path.join(out_dir, "arch%d.pt" % rank))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def weighted_grads_worker(rank, world, port, out_dir):
+    """allreduce_grads(weight=w): sample-weighted mean; None grads count as zero."""
+    sys.path[:0] = [p for p in os.environ.get("HEIST_TEST_PATHS", "").split(os.pathsep) if p]
+    _init(rank, world, port, "gloo")
+    from heist_amd.dist_utils import allreduce_grads
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Linear(7, 5), torch.nn.ReLU(), torch.nn.Linear(5, 3))
+    w = 0
+    if rank == 0:  # rank 1 sits the minibatch out: no backward at all (grads stay None)
+        x = torch.randn(11, 7)
+        net(x).square().mean().backward()
+        w = 11
+    total = allreduce_grads(list(net.parameters()), weight=w)
+    torch.save({"g": [p.grad.clone() for p in net.parameters()], "total": total},
+               os.path.join(out_dir, "w%d.pt" % rank))
+    dist.barrier()
+    dist.destroy_process_group()

@@ -23,6 +23,12 @@ Fixture files (all numpy .npz, loaded with allow_pickle=False):
                   outputs (networks.py:13-239) + ArchitectNetwork
                   .generate_layout decode cases (networks.py:241-335).
   kat.json        the numbers test_sanity.py / test_fixes.py print.
+  arch_update.npz ArchitectAgent.update (agents/architect.py:91-155) from the
+                  nets.npz seed-32 ArchitectNetwork: per case the buffered
+                  (log_prob, value, reward) transitions in, the returned losses,
+                  and per parameter tensor the gradient left after the update
+                  (clipped) and the parameter change, as L2 norms plus 4 fixed
+                  random projections (proj_vectors(): data, not weights).
 """
 import json
 import os
@@ -526,9 +532,61 @@ def make_kat():
         json.dump(kat, f, indent=1)
 
 
+def proj_vectors(i, n, k=4):
+    """The fixed projection vectors of parameter tensor i (also used by the tests)."""
+    return np.random.default_rng(7000 + i).standard_normal((k, n))
+
+
+ARCH_CASES = [  # (log_probs, values, rewards) per update; consecutive updates of one agent
+    [([-52.5], [0.02], [1.0])],
+    [([-61.25], [-0.013], [-1.0])],
+    [([-50.0, -55.5, -48.25, -60.0, -51.0], [0.01, 0.01, 0.01, 0.01, 0.01], [1.0, -1.0, 0.7, 0.2, -0.5])],
+    [([-53.0], [0.015], [0.6]), ([-58.0], [0.011], [-0.5]), ([-49.5, -50.5], [0.012, 0.012], [1.2, 0.3])],
+]
+
+
+def make_arch_update():
+    from heist_architect.agents.architect import ArchitectAgent
+    z = np.load(os.path.join(OUT, "nets.npz"), allow_pickle=False)
+    sd = {k[len("architect/"):]: torch.from_numpy(z[k]) for k in z.files if k.startswith("architect/")}
+    arrs = {"n_cases": np.int64(len(ARCH_CASES))}
+    for ci, case in enumerate(ARCH_CASES):
+        ag = ArchitectAgent(grid_rows=20, grid_cols=20, budget=15)
+        ag.network.load_state_dict(sd)
+        for ui, (lps, vals, rews) in enumerate(case):
+            p0 = [p.detach().clone() for p in ag.network.parameters()]
+            ag.log_probs = [torch.tensor(x) for x in lps]
+            ag.values = [torch.tensor([[x]]) for x in vals]
+            ag.rewards = []
+            for r in rews:
+                ag.store_reward(r)
+            m = ag.update()
+            key = "c%d_u%d_" % (ci, ui)
+            arrs[key + "lp"] = np.array(lps, np.float32)
+            arrs[key + "v"] = np.array(vals, np.float32)
+            arrs[key + "r"] = np.array(rews, np.float64)
+            arrs[key + "loss"] = np.array([m["architect_policy_loss"], m["architect_value_loss"],
+                                           m["architect_total_loss"]], np.float64)
+            gn, gp, dn, dp = [], [], [], []
+            for i, (p, q) in enumerate(zip(ag.network.parameters(), p0)):
+                g = (p.grad if p.grad is not None else torch.zeros_like(p)).detach().double().reshape(-1).numpy()
+                d = (p.detach() - q).double().reshape(-1).numpy()
+                P = proj_vectors(i, g.size)
+                gn.append(np.linalg.norm(g))
+                dn.append(np.linalg.norm(d))
+                gp.append(P @ g)
+                dp.append(P @ d)
+            arrs[key + "gnorm"] = np.array(gn)
+            arrs[key + "gproj"] = np.array(gp)
+            arrs[key + "dnorm"] = np.array(dn)
+            arrs[key + "dproj"] = np.array(dp)
+        arrs["c%d_n" % ci] = np.int64(len(case))
+    np.savez_compressed(os.path.join(OUT, "arch_update.npz"), **arrs)
+
+
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["kat", "bfs", "cones", "ppo", "nets", "env"]
+    which = sys.argv[1:] or ["kat", "bfs", "cones", "ppo", "nets", "env", "arch"]
     for w in which:
         print("==", w, flush=True)
         {"kat": make_kat, "bfs": make_bfs, "cones": make_cones, "ppo": make_ppo,
-         "nets": make_nets, "env": make_env_traces}[w]()
+         "nets": make_nets, "env": make_env_traces, "arch": make_arch_update}[w]()

@@ -1,0 +1,72 @@
+"""ArchitectAgent.update and the Architect reward against the reference's golden vectors.
+
+arch_update.npz holds ArchitectAgent.update (agents/architect.py:91-155) run by the
+Python reference on the nets.npz seed-32 ArchitectNetwork: buffered transitions in,
+losses out, and per parameter tensor the post-update (clipped) gradient and the
+parameter change as norms + fixed random projections.  Tolerance 1e-4 (north star) on
+the losses; the gradient / step summaries to 1e-4 relative (fp32 conv backward on a
+different device and library).  kat.json's architect_reward table pins
+calculate_architect_reward (rewards.py:43-73).
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_data as gd
+from heist_amd.agents.architect import ArchitectAgent
+from heist_amd.rewards import RewardCalculator
+
+
+def proj_vectors(i, n, k=4):  # tests/golden/make_golden.py:proj_vectors
+    return np.random.default_rng(7000 + i).standard_normal((k, n))
+
+
+def _check_cases(device):
+    z = gd.load("arch_update.npz")
+    n_sd = gd.load("nets.npz")
+    sd = {k[len("architect/"):]: torch.from_numpy(n_sd[k]) for k in n_sd.files if k.startswith("architect/")}
+    for ci in range(int(z["n_cases"])):
+        ag = ArchitectAgent(grid_rows=20, grid_cols=20, budget=15, device=device)
+        ag.network.load_state_dict(sd)
+        for ui in range(int(z["c%d_n" % ci])):
+            key = "c%d_u%d_" % (ci, ui)
+            p0 = [p.detach().clone() for p in ag.network.parameters()]
+            ag.log_probs = [torch.tensor(float(x), device=device) for x in z[key + "lp"]]
+            ag.values = [torch.tensor([[float(x)]], device=device) for x in z[key + "v"]]
+            ag.rewards = []
+            ag.store_rewards([float(r) for r in z[key + "r"]])
+            m = ag.update(collective=False)
+            got = [m["architect_policy_loss"], m["architect_value_loss"], m["architect_total_loss"]]
+            np.testing.assert_allclose(got, z[key + "loss"], rtol=1e-4, atol=1e-4, err_msg=key)
+            for i, (p, q) in enumerate(zip(ag.network.parameters(), p0)):
+                g = (p.grad if p.grad is not None else torch.zeros_like(p)).detach().double().reshape(-1).cpu().numpy()
+                d = (p.detach() - q).double().reshape(-1).cpu().numpy()
+                P = proj_vectors(i, g.size)
+                gscale = max(float(z[key + "gnorm"][i]), 1e-12)
+                np.testing.assert_allclose(np.linalg.norm(g), z[key + "gnorm"][i], rtol=1e-4, atol=1e-9,
+                                           err_msg="%s grad norm %d" % (key, i))
+                np.testing.assert_allclose(P @ g, z[key + "gproj"][i], rtol=0, atol=4e-4 * gscale,
+                                           err_msg="%s grad proj %d" % (key, i))
+                dscale = max(float(z[key + "dnorm"][i]), 1e-12)
+                np.testing.assert_allclose(np.linalg.norm(d), z[key + "dnorm"][i], rtol=1e-3, atol=1e-9,
+                                           err_msg="%s step norm %d" % (key, i))
+                np.testing.assert_allclose(P @ d, z[key + "dproj"][i], rtol=0, atol=1e-3 * dscale,
+                                           err_msg="%s step proj %d" % (key, i))
+
+
+def test_architect_update_golden_cpu():
+    _check_cases(torch.device("cpu"))
+
+
+@pytest.mark.gpu
+def test_architect_update_golden_gpu(gpu_device):
+    _check_cases(gpu_device)
+
+
+def test_architect_reward_kat():
+    """calculate_architect_reward (rewards.py:43-73) at the solve rates kat.json holds."""
+    table = gd.load_json("kat.json")["architect_reward"]
+    rc = RewardCalculator()
+    for s, want in table.items():
+        assert rc.architect_reward_from_rate(True, float(s)) == want, s
+    assert rc.architect_reward_from_rate(False, 0.3) == -1.0

@@ -181,7 +181,9 @@ def test_trainer_runs_and_logs(gpu_device, tmp_path):
     tr2 = AdversarialTrainer(cfg, solver_episodes_per_layout=2, total_episodes=8, save_dir=str(tmp_path / "ck"),
                              log_dir=str(tmp_path / "logs"), n_envs=8, rollout_len=40, device=gpu_device)
     assert tr2.resume_from_checkpoint() == last
+    n0 = len(tr2.game_log)
     res = tr2.run_interactive_episodes(num_episodes=2, budget=9, solver_attempts=2)
-    assert len(res) == 2 and all(r["is_interactive"] for r in res)
+    assert len(res) == 2 and all(r["budget"] == 9 for r in res)  # the reference's ep_metrics dicts
+    assert all(e.to_dict()["is_interactive"] for e in tr2.game_log[n0:])
     sim = tr2.simulate_episode(budget=8, solver_attempts=2)
     assert sim["outcome"] in ("vault_reached", "detected", "timeout") and len(sim["frames"]) >= 2

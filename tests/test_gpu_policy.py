@@ -139,14 +139,19 @@ def test_forward_fused_matches_forward(gpu_device):
 
 
 def test_agent_act_uses_fused_path_and_fallback(gpu_device):
-    """act() takes the kernel for 20x20 and the fp32 torch path where it does not apply."""
+    """act() takes the kernel for 20x20 when bf16 is opted into, and the fp32 torch path
+    by default and where the kernel does not apply."""
     torch.manual_seed(1)
-    ag = SolverAgent(20, 20, device=gpu_device)
+    ag0 = SolverAgent(20, 20, device=gpu_device)
+    assert ag0.rollout_precision == "fp32"
+    ag0.act(env_obs(8, 20, gpu_device))
+    assert not hasattr(ag0.network, "_pack_cache")  # parity default: no bf16 kernel
+    ag = SolverAgent(20, 20, device=gpu_device, rollout_precision="bf16")
     obs = env_obs(32, 20, gpu_device)
     a, lp, v, (h, c) = ag.act(obs)
     assert a.shape == (32,) and ((a >= 0) & (a < 5)).all() and torch.isfinite(lp).all()
     assert hasattr(ag.network, "_pack_cache")
-    ag32 = SolverAgent(32, 32, device=gpu_device)
+    ag32 = SolverAgent(32, 32, device=gpu_device, rollout_precision="bf16")
     o32 = torch.rand(4, 3, 32, 32, device=gpu_device)
     a32, lp32, _, _ = ag32.act(o32)
     assert not hasattr(ag32.network, "_pack_cache") and a32.shape == (4,)
@@ -253,3 +258,28 @@ def test_head_sampling_distribution(gpu_device):
     a_again, *_ = net.act_fused(obs, None, seed=77, counter=3)
     assert torch.equal(a_again, acts[3])
     assert not torch.equal(acts[0], acts[1])
+
+
+def test_fp32_gpu_forward_matches_reference_golden(gpu_device):
+    """The default (fp32) rollout forward on the GPU, channels-last as the agent keeps it,
+    against the reference's seeded SolverNetwork outputs (networks.py:76-131, nets.npz),
+    within the north-star 1e-4."""
+    import golden_data as gd
+    z = gd.load("nets.npz")
+    ag = SolverAgent(20, 20, device=gpu_device)
+    sd = {k[len("solver/"):]: torch.from_numpy(z[k]) for k in z.files if k.startswith("solver/")}
+    ag.network.load_state_dict(sd)
+    x = torch.from_numpy(z["solver_in"]).to(gpu_device)
+    h = (torch.from_numpy(z["solver_h"]).to(gpu_device), torch.from_numpy(z["solver_c"]).to(gpu_device))
+    with torch.no_grad():
+        lg, v, (h1, c1) = ag.network(x, h)
+        lg0, v0, _ = ag.network(x)
+    for got, key in ((lg, "solver_logits"), (v, "solver_value"), (h1, "solver_h1"), (c1, "solver_c1"),
+                     (lg0, "solver_logits0"), (v0, "solver_value0")):
+        np.testing.assert_allclose(got.cpu().numpy(), z[key], rtol=0, atol=1e-4, err_msg=key)
+    # act() on the default path: log-prob of the sampled action from the same logits
+    torch.manual_seed(5)
+    a, lp, val, _ = ag.act(x, h)
+    ref = F.log_softmax(torch.from_numpy(z["solver_logits"]), -1).gather(1, a.cpu()[:, None]).reshape(-1)
+    np.testing.assert_allclose(lp.cpu().numpy(), ref.numpy(), rtol=0, atol=1e-4)
+    np.testing.assert_allclose(val.cpu().numpy(), z["solver_value"].reshape(-1), rtol=0, atol=1e-4)

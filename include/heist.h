@@ -115,6 +115,16 @@ int heist_step_stamps(heist_t h, uint64_t* buf);
  * heist_create. */
 int heist_set_ray_mode(heist_t h, int ray_mode);
 
+/* Guard cone cache, no reference counterpart (a precomputation of Guard.get_visible_tiles,
+ * security.py:161-192): with on = 1 (default; HEIST_GUARD_CONES=0 at heist_create turns
+ * it off) every later heist_set_layout casts each guard's vision cone once per (patrol
+ * index, heading) on the exact fp64 path, and heist_step / heist_reset OR the cached cone
+ * instead of raycasting the guard (guards with a patrol of more than 16 points, more than
+ * 8 distinct headings or a vision range above 7 are always raycast).  Results are
+ * identical either way; on = 0 raycasts every guard every tick.  Takes effect at the next
+ * heist_set_layout. */
+int heist_set_guard_cones(heist_t h, int on);
+
 /* Replaces bfs_path_exists (utils.py:52-85) on a batch of grids [N][R][C] int32. */
 int heist_bfs_valid(const int32_t* grid, int n, int rows, int cols, int start_r, int start_c, int goal_r,
                     int goal_c, uint8_t* valid_out, heist_stream_t stream);

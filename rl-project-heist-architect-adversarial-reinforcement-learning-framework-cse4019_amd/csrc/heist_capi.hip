@@ -14,6 +14,7 @@
 namespace heist {
 hipError_t launch_init(const EnvParams& p, hipStream_t st);
 hipError_t launch_order(const EnvParams& p, hipStream_t st);
+hipError_t launch_guard_cones(const EnvParams& p, const uint8_t* mask, hipStream_t st);
 hipError_t launch_set_layout(const EnvParams& p, int max_walls, const int32_t* wall_rc, const int32_t* n_walls,
                              const double* cam_params, const int32_t* n_cams, const int32_t* guard_paths,
                              const int32_t* guard_meta, const double* guard_fov, const int32_t* n_guards,
@@ -208,6 +209,8 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
       sizeof(int32_t) * n,
       sizeof(double) * 3 * heist::kHalfDegN,  // [sin | cos | staging radians]
       (size_t)heist::stop_map_bytes(R, C) * n,
+      // guard cone cache: 32 B per (guard, patrol index, heading slot)
+      (size_t)32 * n * (max_guards > 0 ? max_guards : 1) * heist::kConePath * heist::kConeSlots,
   };
   h->n_allocs = 0;
   for (size_t k = 0; k < sizeof(sizes) / sizeof(sizes[0]); ++k) {
@@ -232,6 +235,9 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   p.half_deg = (const double*)h->allocs[8];
   p.stop = (uint8_t*)h->allocs[9];
   p.stop_bytes = heist::stop_map_bytes(R, C);
+  p.cones = (uint16_t*)h->allocs[10];
+  p.guard_cones = 1;
+  if (const char* gc = getenv("HEIST_GUARD_CONES")) p.guard_cones = atoi(gc) ? 1 : 0;
   std::vector<double> hrad(heist::kHalfDegN);
   for (int m = 0; m < heist::kHalfDegN; ++m) hrad[m] = (0.5 * (m - heist::kHalfDegN / 2)) * heist::kDegToRad;
 
@@ -278,6 +284,8 @@ int heist_set_layout(heist_t h, int max_walls, const int32_t* wall_rc, const int
                                                    guard_meta, guard_fov, n_guards, budget, mask, valid_out,
                                                    (hipStream_t)stream),
                           "heist_set_layout"))
+    return rc;
+  if (int rc = check_hip(heist::launch_guard_cones(h->p, mask, (hipStream_t)stream), "heist_set_layout: guard cones"))
     return rc;
   return check_hip(heist::launch_order(h->p, (hipStream_t)stream), "heist_set_layout: order");
 }
@@ -326,6 +334,13 @@ int heist_set_ray_mode(heist_t h, int ray_mode) {
   if (int rc = check_handle(h)) return rc;
   HEIST_REQUIRE(ray_mode == 0 || ray_mode == 1, "heist_set_ray_mode: ray_mode must be 0 or 1");
   h->p.ray_mode = ray_mode;
+  return 0;
+}
+
+int heist_set_guard_cones(heist_t h, int on) {
+  if (int rc = check_handle(h)) return rc;
+  HEIST_REQUIRE(on == 0 || on == 1, "heist_set_guard_cones: on must be 0 or 1");
+  h->p.guard_cones = on;
   return 0;
 }
 

@@ -8,6 +8,8 @@
 //   Cam        [N][max_cams]       32 B  fov, heading, speed (f64), row, col, range, num_rays
 //   Guard      [N][max_guards]     32 B  fov, heading (f64), idx, speed, len, range, num_rays
 //   paths      [N][max_guards][max_path] u16 (row | col << 8)
+//   cones      [N][max_guards][kConePath][kConeSlots] 32 B  each guard's vision cone at
+//              every (patrol index, heading slot), built once per layout (guard_cone_kernel)
 // Per-handle constant tables: guard heading by (dr, dc) (host libm atan2), the two
 // static position-channel planes, the tile->float LUT.
 #pragma once
@@ -23,6 +25,20 @@ constexpr int kMaxDim = 64;          // R, C <= 64
 constexpr int kMaxEmitters = 64;     // max_cams + max_guards per env
 constexpr double kDegToRad = 3.141592653589793 / 180.0;  // CPython math.radians factor
 constexpr int kHalfDegN = 2880;      // half-degree sin/cos table: angles -720 .. 719.5
+
+// Guard cone cache (guard_cone_kernel): a guard's visible tiles depend only on its patrol
+// index and its heading, and the heading is either the initial one or the direction of
+// the move that led to a patrol point (security.py:145-159), so a layout's guard has at
+// most len x (len + 1) cones.  Guards with a patrol of at most kConePath points, at most
+// kConeSlots distinct headings and a vision range of at most kConeRange get every cone
+// precomputed at set_layout; the tick ORs a 32-byte window instead of casting 181 rays.
+// Cone entry: 16 rows of u16, rows 0..14 = tiles (dr, dc) in [-7, 7]^2 around the guard
+// (bit dc + 7 of row dr + 7, the guard's own tile included), row 15 = the heading slot
+// after the next move from this state.
+constexpr int kConePath = 16;
+constexpr int kConeSlots = 8;
+constexpr int kConeRange = 7;
+constexpr uint8_t kUncached = 0xFF;
 
 struct EnvScalars {
   int32_t pos_r, pos_c, tick, done;
@@ -44,7 +60,8 @@ struct Guard {
   int16_t len, range, num_rays;
   uint16_t pos;      // patrol_path[idx] packed row | col << 8
   uint16_t pos0;     // patrol_path[0]
-  int16_t pad;
+  uint8_t hslot;     // heading slot of `heading` in the guard's cone table; kUncached: raycast live
+  uint8_t nslot;     // heading slot after the next patrol move (the cone the next tick reads)
 };
 static_assert(sizeof(Guard) == 32, "Guard layout");
 
@@ -57,7 +74,7 @@ struct Emit {
   double step;    // fov / num_rays: the fast path's ray spacing (approximate angle)
   int32_t row, col, range, num_rays;
   int32_t first;  // index of this emitter's ray 0 in the env's flattened ray list
-  int32_t kind;   // 0 camera (half-tile sub-steps), 1 guard (whole-tile steps)
+  int32_t kind;   // 0 camera (half-tile sub-steps), 1 guard (whole-tile steps), 2 guard with a cached cone (no rays)
 };
 static_assert(sizeof(Emit) == 48, "Emit layout");
 
@@ -73,6 +90,8 @@ struct EnvParams {
   Cam* cams;
   Guard* guards;
   uint16_t* paths;
+  uint16_t* cones;            // [n_envs][max_guards][kConePath][kConeSlots][16] guard cone cache
+  int guard_cones;            // 1: heist_set_layout builds the cone cache (default); 0: guards raycast live
   const double* heading_tab;  // [(2R-1)*(2C-1)]
   const float* plane0;        // [RC] position channel without the solver
   const float* plane1;        // [RC] position channel value if the solver is on that cell

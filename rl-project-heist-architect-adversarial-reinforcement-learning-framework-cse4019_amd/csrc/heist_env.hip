@@ -50,13 +50,16 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(
 
 struct EnvLds {
   uint8_t* wall;   // LDS offset 0: [(R+2G)(C+2G)] ray stop map, 1 = wall or outside the grid (G = kRing)
-  uint8_t* vis;    // LDS offset D: visibility with the same padded geometry (ring bytes unused)
+  uint8_t* vis;    // LDS offset D: visibility with the same padded geometry (ring bytes unused): camera
+                   // rays and live-raycast guards
+  uint8_t* gvis;   // LDS offset 2D: the cached guard cones (same geometry); visibility = vis | gvis
   uint8_t* grid;   // [RC]
   Emit* em;        // [n_emit]
   uint16_t* path;  // [max_guards][max_path]
   float* plane;    // [RC] static position channel (plane0)
   int* queue;      // [W][64] per-wave exact-path ray queues (cast_rays)
   int* meta;       // [0] emitters, [1] total rays
+  uint16_t* cone;  // [max_guards][16] this tick's cached guard cones (kind-2 emitters), see heist_device.h
   int PC;          // padded row stride C + 2G
   int off0;        // padded index of tile (0, 0): G * PC + G
   __device__ __forceinline__ int at(int r, int c) const { return off0 + r * PC + c; }
@@ -73,11 +76,12 @@ constexpr int kRing = 6;
 // 20 x 20 and 6144 for the 64 x 64 maximum.
 __host__ __device__ inline int padded_bytes(int R, int C) { return (R + 2 * kRing) * (C + 2 * kRing); }
 
-__host__ __device__ inline size_t env_lds_bytes(int R, int C, int n_emit, int path_words, int D, int waves) {
+__host__ __device__ inline size_t env_lds_bytes(int R, int C, int n_emit, int path_words, int D, int waves,
+                                                int cone_guards = 0) {
   const int RC = R * C;
-  return 2 * (size_t)D + align16(RC) + align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) +
+  return 3 * (size_t)D + align16(RC) + align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) +
          align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1)) + align16(sizeof(float) * RC) +
-         sizeof(int) * 64 * (size_t)waves + 32;
+         sizeof(int) * 64 * (size_t)waves + 32 + 32 * (size_t)cone_guards;
 }
 
 template <int D>
@@ -86,13 +90,15 @@ __device__ __forceinline__ EnvLds carve(unsigned char* smem, int R, int C, int n
   EnvLds L;
   L.wall = smem;
   L.vis = smem + D;
-  size_t o = 2 * (size_t)D;
+  L.gvis = smem + 2 * (size_t)D;
+  size_t o = 3 * (size_t)D;
   L.grid = smem + o; o += align16(RC);
   L.em = reinterpret_cast<Emit*>(smem + o); o += align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1));
   L.path = reinterpret_cast<uint16_t*>(smem + o); o += align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1));
   L.plane = reinterpret_cast<float*>(smem + o); o += align16(sizeof(float) * RC);
   L.queue = reinterpret_cast<int*>(smem + o); o += sizeof(int) * 64 * (size_t)waves;
-  L.meta = reinterpret_cast<int*>(smem + o);
+  L.meta = reinterpret_cast<int*>(smem + o); o += 32;
+  L.cone = reinterpret_cast<uint16_t*>(smem + o);
   L.PC = C + 2 * kRing;
   L.off0 = kRing * L.PC + kRing;
   return L;
@@ -530,7 +536,7 @@ static_assert(kMaxEmitters <= 64, "publish_emitters keeps every emitter in wave 
 __device__ __forceinline__ void publish_emitters(const EnvLds& L, Emit E, int n_em) {
   const int t = threadIdx.x;
   if (t < 64) {
-    const int cnt = t < n_em ? (E.num_rays + 1 + 63) / 64 : 0;
+    const int cnt = (t < n_em && E.kind != 2) ? (E.num_rays + 1 + 63) / 64 : 0;  // kind 2: cached cone, no rays
     int incl = cnt;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -566,8 +572,50 @@ __device__ __forceinline__ Emit guard_emit(const Guard& gd) {
   E.fov = gd.fov;
   E.row = unpack_r(gd.pos); E.col = unpack_c(gd.pos); E.range = gd.range; E.num_rays = gd.num_rays;
   E.step = gd.fov * __builtin_amdgcn_rcp((double)gd.num_rays);
-  E.first = 0; E.kind = 1;
+  E.first = 0; E.kind = gd.hslot == kUncached ? 1 : 2;
   return E;
+}
+
+// ---- guard cone cache (heist_device.h) --------------------------------------------------
+
+// Element offset (in u16) of the cone entry of guard g of env e at (patrol index, slot).
+__device__ __forceinline__ size_t cone_entry(const EnvParams& p, int e, int g, int idx, int slot) {
+  return ((((size_t)e * p.max_guards + g) * kConePath + idx) * kConeSlots + slot) * 16;
+}
+
+// A cached guard's cone for its pose after this tick's move (move: the env acts and the
+// patrol has >= 2 points, security.py:147) into LDS cone[g]: the record's nslot names the
+// heading slot of the next patrol point, so the entry is known before the barrier.
+__device__ __forceinline__ void stage_guard_cone(const EnvParams& p, int e, const EnvLds& L, int g, const Guard& gd,
+                                                 bool act) {
+  if (gd.hslot == kUncached) return;
+  int idx = gd.idx, slot = gd.hslot;
+  if (act && gd.len >= 2) {
+    idx += gd.step;
+    if (idx >= gd.len) idx -= gd.len;
+    slot = gd.nslot;
+  }
+  const uint4* src = reinterpret_cast<const uint4*>(p.cones + cone_entry(p, e, g, idx, slot));
+  const uint4 a = src[0], b = src[1];
+  uint4* dst = reinterpret_cast<uint4*>(L.cone + 16 * g);
+  dst[0] = a;
+  dst[1] = b;
+}
+
+// OR every cached guard cone staged in LDS into the visibility plane: thread q of the
+// 16 x 15 window sets tile (row + q/16 - 7, col + q%16 - 7) if its bit is set (bits only
+// ever name tiles inside the grid, so the address is always in the plane).
+template <int NT>
+__device__ __forceinline__ void stamp_guard_cones(const EnvLds& L, int n_cams, int n_em) {
+  for (int k = n_cams; k < n_em; ++k) {
+    if (uni(L.em[k].kind) != 2) continue;
+    const int r0 = uni(L.em[k].row) - kConeRange, c0 = uni(L.em[k].col) - kConeRange;
+    const uint16_t* rows = L.cone + 16 * (k - n_cams);
+    for (int q = threadIdx.x; q < 16 * (2 * kConeRange + 1); q += NT) {
+      const int rr = q >> 4, cc = q & 15;
+      if ((rows[rr] >> cc) & 1u) L.gvis[L.at(r0 + rr, c0 + cc)] = 1;
+    }
+  }
 }
 
 // Visibility (visibility.py:31-65) once the emitter table is in LDS and vis is zeroed.
@@ -576,10 +624,11 @@ __device__ __forceinline__ void raycast_pass(const EnvParams& p, int e, unsigned
                                              int n_cams) {
   __syncthreads();  // emitter table, stop map and cleared vis in place
   const int t = threadIdx.x;
-  if (t >= n_cams && t < n_em) {  // a guard's own tile (visibility.py:59); rays only ever add tiles
+  if (t >= n_cams && t < n_em) {  // a live guard's own tile (visibility.py:59; a cached cone holds it)
     const Emit E = L.em[t];
-    L.vis[L.at(E.row, E.col)] = 1;
+    if (E.kind == 1) L.vis[L.at(E.row, E.col)] = 1;
   }
+  stamp_guard_cones<NT>(L, n_cams, n_em);
   if (p.probe_mode != 1 && p.probe_mode != 5) {
     if (p.sample_counter || p.redo_counter)
       cast_rays<NT, U, D, true>(smem, L, p.ray_mode, p.probe_mode, p.half_deg);
@@ -591,10 +640,15 @@ __device__ __forceinline__ void raycast_pass(const EnvParams& p, int e, unsigned
   if (p.redo_counter && t == 0) p.redo_counter[e] += (unsigned int)L.meta[4];
 }
 
-template <int NT>
+// Zero the ray plane (RAYS) and / or the cached-cone plane (CONES).
+template <int NT, bool RAYS = true, bool CONES = true>
 __device__ __forceinline__ void clear_vis(const EnvParams& p, const EnvLds& L) {
   uint32_t* v4 = reinterpret_cast<uint32_t*>(L.vis);
-  for (int i = threadIdx.x; i < (padded_bytes(p.R, p.C) + 3) / 4; i += NT) v4[i] = 0u;
+  uint32_t* g4 = reinterpret_cast<uint32_t*>(L.gvis);
+  for (int i = threadIdx.x; i < (padded_bytes(p.R, p.C) + 3) / 4; i += NT) {
+    if (RAYS) v4[i] = 0u;
+    if (CONES) g4[i] = 0u;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -710,13 +764,14 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
       o0[q] = make_float4(p.tile_lut[b & 7], p.tile_lut[(b >> 8) & 7], p.tile_lut[(b >> 16) & 7],
                           p.tile_lut[(b >> 24) & 7]);
       const int r = q / c4;
-      const uint8_t* vp = L.vis + L.at(r, 4 * (q - r * c4));
+      const int a = L.at(r, 4 * (q - r * c4));
       uint32_t v;
       if ((kRing & 3) == 0) {
-        v = *reinterpret_cast<const uint32_t*>(vp);
+        v = *reinterpret_cast<const uint32_t*>(L.vis + a) | *reinterpret_cast<const uint32_t*>(L.gvis + a);
       } else {
-        const uint16_t* vp2 = reinterpret_cast<const uint16_t*>(vp);
-        v = (uint32_t)vp2[0] | ((uint32_t)vp2[1] << 16);
+        const uint16_t* vp2 = reinterpret_cast<const uint16_t*>(L.vis + a);
+        const uint16_t* gp2 = reinterpret_cast<const uint16_t*>(L.gvis + a);
+        v = ((uint32_t)vp2[0] | ((uint32_t)vp2[1] << 16)) | ((uint32_t)gp2[0] | ((uint32_t)gp2[1] << 16));
       }
       o1[q] = make_float4((v & 0xff) ? 1.0f : 0.0f, (v & 0xff00) ? 1.0f : 0.0f, (v & 0xff0000) ? 1.0f : 0.0f,
                           (v & 0xff000000u) ? 1.0f : 0.0f);
@@ -739,7 +794,7 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
         v = p.tile_lut[L.grid[cell] & 7];
       } else if (ch == 1) {
         const int r = cell / C;
-        v = L.vis[L.at(r, cell - r * C)] ? 1.0f : 0.0f;
+        v = (L.vis[L.at(r, cell - r * C)] | L.gvis[L.at(r, cell - r * C)]) ? 1.0f : 0.0f;
       } else {
         v = cell == vault ? p.vault_val : (cell == solver ? sv : L.plane[cell]);
       }
@@ -793,12 +848,13 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   const EnvLds L = carve<D>(smem, p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path, W);
   EnvScalars s = p.scal[e];
   const int n_cams = s.n_cams, n_em = s.n_cams + s.n_guards;
+  const bool act = !s.done;
   EmitterRaw raw;
   prefetch<NT>(p, e, L, n_cams, n_em, raw);
   const int a_raw = (int)actions[e];
+  if (t >= n_cams && t < n_em) stage_guard_cone(p, e, L, t - n_cams, as_guard(raw), act);
   clear_vis<NT>(p, L);
-  const bool act = !s.done;
-  __syncthreads();  // grid, paths in LDS
+  __syncthreads();  // grid, paths, cached guard cones in LDS
   HEIST_STEP_STAMP(1);
 
   double reward = 0.0;
@@ -816,6 +872,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   // 2. cameras rotate, guards patrol (security.py:49-51, :145-159) -- in registers
   uint16_t pos0 = 0;  // a guard thread's patrol start, for the auto-reset below
   bool off_start = false;  // a guard thread's guard stands off its patrol start
+  uint8_t gslot = kUncached;  // a guard thread's heading slot after this tick (cached cones)
   Emit E;
   if (t < n_cams) {
     Cam cm = as_cam(raw);
@@ -840,7 +897,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
       gp->heading = gd.heading;
       gp->idx = gd.idx;
       gp->pos = gd.pos;
+      if (gd.hslot != kUncached) {  // the staged entry's row 15: the slot after the next move
+        gd.hslot = gd.nslot;
+        gd.nslot = (uint8_t)L.cone[16 * g + 15];
+        gp->hslot = gd.hslot;
+        gp->nslot = gd.nslot;
+      }
     }
+    gslot = gd.hslot;
     off_start = gd.pos != pos0;
     E = guard_emit(gd);
   }
@@ -858,7 +922,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     reward += (double)(s.prev_dist - curr) * 0.1;
     s.prev_dist = curr;
     if (curr <= 3 && s.initial_dist > 3) reward += 0.05 * (double)(3 - curr);
-    if (L.vis[L.at(s.pos_r, s.pos_c)]) {
+    if (L.vis[L.at(s.pos_r, s.pos_c)] | L.gvis[L.at(s.pos_r, s.pos_c)]) {
       s.detected = 1;
       reward += p.r_detect;
       s.done = 1;
@@ -885,15 +949,37 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     // The reset keeps every heading (environment.py:204-208) and moves only the guards
     // back to patrol point 0, so its visibility is this tick's unless a guard stands
     // elsewhere.  The barrier also orders every wave's detection read before a clear.
+    // Camera visibility stays as it is; a guard back at its patrol start changes only the
+    // cached-cone plane (re-stamped) unless a live-raycast guard moved (full raycast).
     const bool is_guard = t >= n_cams && t < n_em;
-    const int any_moved = __syncthreads_or(off_start);
+    const int live_moved = __syncthreads_or(off_start && gslot == kUncached);
+    const int cone_moved = __syncthreads_or(off_start && gslot != kUncached);
+    const int any_moved = live_moved | cone_moved;
     reset_solver(p, s);
     if (is_guard) {
-      Guard* gp = p.guards + (size_t)e * p.max_guards + (t - n_cams);
+      const int g = t - n_cams;
+      Guard* gp = p.guards + (size_t)e * p.max_guards + g;
       gp->idx = 0;
       gp->pos = pos0;
+      if (gslot != kUncached) {  // cone of (patrol point 0, this tick's heading slot)
+        const uint4* src = reinterpret_cast<const uint4*>(p.cones + cone_entry(p, e, g, 0, gslot));
+        const uint4 a = src[0], b = src[1];
+        gp->nslot = (uint8_t)(b.w >> 16);  // row 15
+        if (any_moved) {  // the first raycast pass is over (barrier above)
+          uint4* dst = reinterpret_cast<uint4*>(L.cone + 16 * g);
+          dst[0] = a;
+          dst[1] = b;
+          L.em[t].row = unpack_r(pos0);
+          L.em[t].col = unpack_c(pos0);
+        }
+      }
     }
-    if (any_moved) {
+    if (cone_moved && !live_moved) {
+      clear_vis<NT, false, true>(p, L);
+      __syncthreads();  // new cones and poses staged, cone plane cleared
+      stamp_guard_cones<NT>(L, n_cams, n_em);
+      __syncthreads();
+    } else if (live_moved) {
       Emit E2;
       if (t < n_em) E2 = L.em[t];  // this tick's headings, fov and range stay
       if (is_guard) {
@@ -944,6 +1030,10 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     Guard* gp = p.guards + (size_t)e * p.max_guards + (t - n_cams);
     gp->idx = 0;
     gp->pos = gd.pos0;
+    if (gd.hslot != kUncached) {  // heading kept (environment.py:204-208): cone of (0, hslot)
+      stage_guard_cone(p, e, L, t - n_cams, gd, false);
+      gp->nslot = (uint8_t)L.cone[16 * (t - n_cams) + 15];
+    }
     E = guard_emit(gd);
   }
   publish_emitters(L, E, n_em);
@@ -1072,7 +1162,8 @@ __global__ __launch_bounds__(64) void set_layout_kernel(EnvParams p, int max_wal
         gd.num_rays = (int16_t)num_rays_for(gd.fov);
         gd.pos = dst[0];
         gd.pos0 = dst[0];
-        gd.pad = 0;
+        gd.hslot = kUncached;  // guard_cone_kernel fills the cone cache next
+        gd.nslot = kUncached;
         p.guards[(size_t)e * p.max_guards + ng] = gd;
         g[unpack_r(dst[0]) * C + unpack_c(dst[0])] = kGuard;
         ++ng;
@@ -1096,6 +1187,105 @@ __global__ __launch_bounds__(64) void set_layout_kernel(EnvParams p, int max_wal
     s->n_guards = cnt[2];
     s->spent = cnt[3];
     valid_out[e] = ok ? 1 : 0;
+  }
+}
+
+// Guard cone cache (heist_device.h), one wave per (env, guard), run right after
+// set_layout_kernel: the guard's distinct headings (the initial one, then the direction of
+// every patrol move, as guard_heading_after computes it), the heading slot each patrol
+// point is entered with, and the cone of every (patrol index, heading slot) cast on the
+// exact fp64 path (security.py:161-192, the same arithmetic as ray_mode 1).  A guard that
+// does not fit the cache (patrol > kConePath points, > kConeSlots headings, range >
+// kConeRange) keeps hslot = kUncached and is raycast live by step/reset.
+template <int D>
+__global__ __launch_bounds__(64) void guard_cone_kernel(EnvParams p, const uint8_t* __restrict__ mask) {
+  constexpr int U = 4;
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ double heads[kConeSlots];
+  __shared__ uint8_t arr[kConePath];  // heading slot on entering patrol point j; kUncached: no move
+  __shared__ int n_heads;
+  const int e = blockIdx.x, g = blockIdx.y;
+  const int lane = threadIdx.x;
+  if (mask && !mask[e]) return;
+  if (g >= p.scal[e].n_guards) return;
+  Guard* gp = p.guards + (size_t)e * p.max_guards + g;
+  const Guard gd = *gp;
+  const int len = gd.len;
+  if (!p.guard_cones || len < 1 || len > kConePath || gd.range < 0 || gd.range > kConeRange) return;
+  const int R = p.R, C = p.C;
+  const EnvLds L = carve<D>(smem, R, C, 1, kConePath, 1);
+  const uint4* ss = reinterpret_cast<const uint4*>(p.stop + (size_t)e * p.stop_bytes);
+  uint4* sd = reinterpret_cast<uint4*>(L.wall);
+  for (int i = lane; i < p.stop_bytes / 16; i += 64) sd[i] = ss[i];
+  if (lane < len) L.path[lane] = p.paths[((size_t)e * p.max_guards + g) * p.max_path + lane];
+  __syncthreads();
+  if (lane == 0) {
+    int nh = 1;
+    heads[0] = gd.heading;  // 0.0 after set_layout (security.py:130)
+    for (int j = 0; j < len; ++j) {
+      int i0 = j - gd.step;  // the patrol point a move into j starts from (step in [0, len))
+      if (i0 < 0) i0 += len;
+      const int dr = unpack_r(L.path[j]) - unpack_r(L.path[i0]), dc = unpack_c(L.path[j]) - unpack_c(L.path[i0]);
+      if (len < 2 || (dr == 0 && dc == 0)) {  // security.py:147, :158: heading unchanged
+        arr[j] = kUncached;
+        continue;
+      }
+      const double h = guard_heading_after(p, dr, dc, 0.0);
+      int k = 0;
+      while (k < nh && heads[k] != h) ++k;
+      if (k == nh) {
+        if (nh == kConeSlots) {
+          nh = 0;  // too many headings: not cached
+          break;
+        }
+        heads[nh++] = h;
+      }
+      arr[j] = (uint8_t)k;
+    }
+    n_heads = nh;
+  }
+  __syncthreads();
+  const int nh = n_heads;
+  if (nh == 0) return;
+  uint32_t* v4 = reinterpret_cast<uint32_t*>(L.vis);
+  for (int st = 0; st < len * nh; ++st) {
+    const int i = st / nh, h = st - i * nh;
+    for (int q = lane; q < (padded_bytes(R, C) + 3) / 4; q += 64) v4[q] = 0u;
+    __syncthreads();
+    Emit E;
+    E.hmh = heads[h] - gd.fov / 2.0;  // security.py:173-178
+    E.fov = gd.fov;
+    E.step = 0.0;
+    E.row = unpack_r(L.path[i]);
+    E.col = unpack_c(L.path[i]);
+    E.range = gd.range;
+    E.num_rays = gd.num_rays;
+    E.first = 0;
+    E.kind = 1;
+    for (int ray = lane; ray <= E.num_rays; ray += 64) exact_ray<U, D>(smem, E, ray, L.PC, 0, p.half_deg);
+    __syncthreads();
+    if (lane < 16) {
+      uint32_t bits = 0;
+      if (lane < 2 * kConeRange + 1) {
+        const int rr = E.row + lane - kConeRange;
+        if ((unsigned)rr < (unsigned)R)
+          for (int j = 0; j < 2 * kConeRange + 1; ++j) {
+            const int cc = E.col + j - kConeRange;
+            if ((unsigned)cc < (unsigned)C && (L.vis[L.at(rr, cc)] || (rr == E.row && cc == E.col))) bits |= 1u << j;
+          }
+      } else {  // the heading slot after the next move (step_kernel's guard update)
+        int i2 = i + gd.step;
+        if (i2 >= len) i2 -= len;
+        bits = (len >= 2 && arr[i2] != kUncached) ? arr[i2] : (uint32_t)h;
+      }
+      p.cones[cone_entry(p, e, g, i, h) + lane] = (uint16_t)bits;
+    }
+    __syncthreads();
+  }
+  if (lane == 0) {  // state (patrol point 0, initial heading)
+    const int i2 = gd.step < len ? gd.step : 0;
+    gp->hslot = 0;
+    gp->nslot = (len >= 2 && arr[i2] != kUncached) ? arr[i2] : 0;
   }
 }
 
@@ -1204,7 +1394,8 @@ __global__ __launch_bounds__(256) void sincos_kernel(const double* __restrict__ 
 // ---------------------------------------------------------------------------
 
 static size_t env_lds(const EnvParams& p) {
-  return env_lds_bytes(p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path, p.vis_gap, p.step_waves);
+  return env_lds_bytes(p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path, p.vis_gap, p.step_waves,
+                       p.max_guards);
 }
 
 // Block -> env dispatch order for step/reset (longest-processing-time first): envs sorted
@@ -1227,7 +1418,7 @@ __global__ __launch_bounds__(1024) void order_kernel(EnvParams p) {
     }
     for (int g = 0; g < s.n_guards; ++g) {
       const Guard& gd = p.guards[(size_t)e * p.max_guards + g];
-      cost += (gd.num_rays + 1) * gd.range;
+      if (gd.hslot == kUncached) cost += (gd.num_rays + 1) * gd.range;
     }
     const int b = cost >> 5;
     return 1023 - (b < 1023 ? b : 1023);  // descending cost
@@ -1253,6 +1444,16 @@ hipError_t launch_order(const EnvParams& p, hipStream_t st) {
 
 hipError_t launch_init(const EnvParams& p, hipStream_t st) {
   hipLaunchKernelGGL(init_kernel, dim3((p.n_envs + 255) / 256), dim3(256), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_guard_cones(const EnvParams& p, const uint8_t* mask, hipStream_t st) {
+  if (p.max_guards == 0 || !p.guard_cones) return hipSuccess;
+  const size_t lds = env_lds_bytes(p.R, p.C, 1, kConePath, p.vis_gap, 1);
+  if (p.vis_gap == 1024)
+    hipLaunchKernelGGL(guard_cone_kernel<1024>, dim3(p.n_envs, p.max_guards), dim3(64), lds, st, p, mask);
+  else
+    hipLaunchKernelGGL(guard_cone_kernel<6144>, dim3(p.n_envs, p.max_guards), dim3(64), lds, st, p, mask);
   return hipGetLastError();
 }
 

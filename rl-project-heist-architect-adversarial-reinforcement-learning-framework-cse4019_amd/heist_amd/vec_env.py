@@ -284,6 +284,13 @@ class HeistEnv:
         timing."""
         nat.check(nat.lib().heist_set_ray_mode(self._h, int(mode)), "heist_set_ray_mode")
 
+    def set_guard_cones(self, on: bool) -> None:
+        """True (default): the next set_layout precomputes every guard's vision cone per
+        (patrol point, heading) on the exact path and step/reset OR the cached cone instead
+        of raycasting the guard; False: every guard is raycast every tick.  Results are
+        bit-identical; takes effect at the next set_layout."""
+        nat.check(nat.lib().heist_set_guard_cones(self._h, 1 if on else 0), "heist_set_guard_cones")
+
     @property
     def visibility(self) -> torch.Tensor:
         """Current visibility plane [N, R, C] (obs channel 1)."""

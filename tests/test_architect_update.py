@@ -45,12 +45,12 @@ def _check_cases(device):
                 gscale = max(float(z[key + "gnorm"][i]), 1e-12)
                 np.testing.assert_allclose(np.linalg.norm(g), z[key + "gnorm"][i], rtol=1e-4, atol=1e-9,
                                            err_msg="%s grad norm %d" % (key, i))
-                np.testing.assert_allclose(P @ g, z[key + "gproj"][i], rtol=0, atol=4e-4 * gscale,
+                np.testing.assert_allclose(P @ g, z[key + "gproj"][i], rtol=0, atol=4e-4 * gscale + 1e-9,
                                            err_msg="%s grad proj %d" % (key, i))
                 dscale = max(float(z[key + "dnorm"][i]), 1e-12)
                 np.testing.assert_allclose(np.linalg.norm(d), z[key + "dnorm"][i], rtol=1e-3, atol=1e-9,
                                            err_msg="%s step norm %d" % (key, i))
-                np.testing.assert_allclose(P @ d, z[key + "dproj"][i], rtol=0, atol=1e-3 * dscale,
+                np.testing.assert_allclose(P @ d, z[key + "dproj"][i], rtol=0, atol=1e-3 * dscale + 1e-9,
                                            err_msg="%s step proj %d" % (key, i))
 
 

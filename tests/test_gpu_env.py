@@ -25,9 +25,11 @@ def _cfg(tr):
                              vault_pos=tr["vault"], architect_budget=tr["budget"])
 
 
+@pytest.mark.parametrize("cones", [True, False], ids=["guard_cones", "live_guards"])
 @pytest.mark.parametrize("tr", list(gd.env_traces()), ids=lambda t: t["name"])
-def test_golden_trace_bit_exact(tr, gpu_device):
+def test_golden_trace_bit_exact(tr, cones, gpu_device):
     env = HeistEnv(1, _cfg(tr), max_cams=16, max_guards=8, max_path=64, device=gpu_device, auto_reset=False)
+    env.set_guard_cones(cones)
     valid = env.set_layouts([(tr["walls"], tr["cams"], tr["guards"])], budget=tr["budget"])
     assert bool(valid[0]) == tr["valid"]
     st = env.export(grid=True)
@@ -200,9 +202,11 @@ def test_step_stamps_instrumentation(gpu_device):
     assert (s[:, :, 8] != 0).any()
 
 
-def test_sample_counter_work_figure(gpu_device):
+@pytest.mark.parametrize("cones", [False, True], ids=["live_guards", "guard_cones"])
+def test_sample_counter_work_figure(cones, gpu_device):
     """heist_count_samples: an unobstructed camera ray evaluates all 2*range samples, a guard
-    ray all range samples; counting leaves the results unchanged."""
+    ray all range samples (none with the guard cone cache); counting leaves the results
+    unchanged."""
     cfg = EnvironmentConfig()
     fov = 60.0
     lay = ([], [{"row": 10, "col": 10, "fov_angle": fov, "heading": 0.0, "rotation_speed": 15.0,
@@ -210,10 +214,11 @@ def test_sample_counter_work_figure(gpu_device):
            [{"patrol_path": [(5, 5), (5, 6)], "speed": 1, "vision_range": 4, "fov_angle": 90.0}])
     envs = [HeistEnv(2, cfg, device=gpu_device) for _ in range(2)]
     for e in envs:
+        e.set_guard_cones(cones)
         e.set_layouts([lay, lay], budget=40)
     cnt = torch.zeros(2, dtype=torch.int64, device=gpu_device)
     envs[0].count_samples(cnt)
-    per_pass = (max(int(fov * 2), 30) + 1) * 12 + (max(int(90.0 * 2), 30) + 1) * 4
+    per_pass = (max(int(fov * 2), 30) + 1) * 12 + (0 if cones else (max(int(90.0 * 2), 30) + 1) * 4)
     outs = []
     for e in envs:
         e.reset()
@@ -313,10 +318,11 @@ def test_cones_fast_equals_exact(R, C, gpu_device):
 
 
 def test_step_fast_equals_exact_and_redo_rate(gpu_device):
-    """Two handles on the same layouts, one fast (mode 0) and one exact (mode 1): every
-    observation, reward and status is identical over 150 ticks with auto-reset.  Synthetic
-    (f32-random) headings re-cast only a small fraction of rays exactly; the reference's
-    default cameras (heading 0, fov 60, speed 15: half-degree ray angles) re-cast many."""
+    """Three handles on the same layouts: fast raycast (mode 0) with the guard cone cache,
+    fast with live guards, and exact (mode 1) with live guards: every observation, reward
+    and status is identical over 150 ticks with auto-reset.  Synthetic (f32-random)
+    headings re-cast only a small fraction of rays exactly; the reference's default
+    cameras (heading 0, fov 60, speed 15: half-degree ray angles) re-cast many."""
     n = 1024
     cfg = EnvironmentConfig()
     lays = synthetic_layouts(n - 64, 20, 20, 15, seed=77)
@@ -325,25 +331,29 @@ def test_step_fast_equals_exact_and_redo_rate(gpu_device):
         c = dict(cam, row=3 + k % 14, col=2 + (k * 7) % 15)
         lays.append(([(5, 5 + k % 10)], [c], [{"patrol_path": [(15, 3), (15, 4), (14, 4)], "speed": 1,
                                                  "vision_range": 4, "fov_angle": 90.0}]))
-    envs = [HeistEnv(n, cfg, device=gpu_device) for _ in range(2)]
+    envs = [HeistEnv(n, cfg, device=gpu_device) for _ in range(3)]
     envs[1].set_ray_mode(1)
+    envs[1].set_guard_cones(False)
+    envs[2].set_guard_cones(False)
+    envs = [envs[2], envs[1], envs[0]]  # [fast live, exact live, fast cached]
     cnt = [torch.zeros(n, dtype=torch.int64, device=gpu_device) for _ in range(2)]
-    for e, c in zip(envs, cnt):
+    for e in envs:
         e.set_layouts(lays, budget=15)
+    for e, c in zip(envs, cnt):
         e.count_exact_rays(c)
-    o0, o1 = envs[0].reset(), envs[1].reset()
-    assert torch.equal(o0, o1)
+    o = [e.reset() for e in envs]
+    assert torch.equal(o[0], o[1]) and torch.equal(o[0], o[2])
     cnt_s = [torch.zeros(n, dtype=torch.int64, device=gpu_device) for _ in range(2)]
     envs[0].count_samples(cnt_s[0])
     envs[1].count_samples(cnt_s[1])
     g = torch.Generator(device="cpu").manual_seed(5)
     for t in range(150):
         a = torch.randint(0, 5, (n,), generator=g)
-        r0 = envs[0].step(a)
-        r1 = envs[1].step(a)
-        for x, y in zip(r0, r1):
-            assert torch.equal(x, y), t
-        assert torch.equal(envs[0].reward64, envs[1].reward64), t
+        r = [e.step(a) for e in envs]
+        for k in (1, 2):
+            for x, y in zip(r[0], r[k]):
+                assert torch.equal(x, y), (t, k)
+            assert torch.equal(envs[0].reward64, envs[k].reward64), (t, k)
     assert torch.equal(cnt_s[0], cnt_s[1])
     exact_all = cnt[1].double()
     frac_syn = float(cnt[0][: n - 64].sum()) / float(exact_all[: n - 64].sum())
@@ -353,3 +363,83 @@ def test_step_fast_equals_exact_and_redo_rate(gpu_device):
     for e in envs:
         e.count_exact_rays(None)
         e.count_samples(None)
+
+
+def _guard_variety_layouts(n, R, rng):
+    """Guards of every shape the cone cache must handle or refuse: Architect rings, long
+    diagonal patrols with more than 8 distinct move headings (not cached), speeds 0..3 and
+    negative, duplicate points, single points, ranges 1..9 (above 7: not cached), fovs
+    30..200, plus a camera or two."""
+    lays = []
+    for i in range(n):
+        guards = []
+        for _ in range(int(rng.integers(1, 5))):
+            kind = int(rng.integers(0, 5))
+            r0, c0 = int(rng.integers(1, R - 1)), int(rng.integers(1, R - 1))
+            if kind == 0:
+                from heist_amd.layouts import architect_patrol
+                path = architect_patrol(r0, c0, R, R)
+            elif kind == 1:  # random walk with diagonal and long moves
+                path = [(r0, c0)]
+                for _ in range(int(rng.integers(2, 20))):
+                    r0 = int(np.clip(r0 + rng.integers(-2, 3), 0, R - 1))
+                    c0 = int(np.clip(c0 + rng.integers(-2, 3), 0, R - 1))
+                    path.append((r0, c0))
+            elif kind == 2:
+                path = [(r0, c0)]
+            elif kind == 3:  # back and forth with duplicates
+                path = [(r0, c0), (r0, c0), (r0, min(c0 + 1, R - 2)), (r0, min(c0 + 1, R - 2))]
+            else:
+                path = [(int(rng.integers(0, R)), int(rng.integers(0, R))) for _ in range(int(rng.integers(2, 9)))]
+            guards.append({"patrol_path": path, "speed": int(rng.choice([1, 1, 1, 2, 3, -1, 0])),
+                           "vision_range": int(rng.choice([4, 4, 4, 1, 3, 7, 8, 9])),
+                           "fov_angle": float(rng.choice([90.0, 90.0, 30.0, 120.0, 200.0,
+                                                          float(np.float32(rng.uniform(30, 180)))]))})
+        cams = [{"row": int(rng.integers(1, R - 1)), "col": int(rng.integers(1, R - 1)),
+                 "fov_angle": float(np.float32(rng.uniform(30, 120))), "heading": float(np.float32(rng.uniform(0, 360))),
+                 "rotation_speed": float(np.float32(rng.uniform(5, 35))), "vision_range": 6}
+                for _ in range(int(rng.integers(0, 3)))]
+        walls = [(int(rng.integers(1, R - 1)), int(rng.integers(1, R - 1))) for _ in range(int(rng.integers(0, 25)))]
+        lays.append((walls, cams, guards))
+    return lays
+
+
+@pytest.mark.parametrize("R", [12, 20, 32])
+def test_guard_cone_cache_equals_live_raycast(R, gpu_device):
+    """The guard cone cache (heist_set_guard_cones) against live raycasting and the C
+    oracle: same observations, rewards, statuses and guard headings over 200 ticks with
+    auto-reset, on guards the cache takes and guards it must refuse."""
+    n = 512
+    rng = np.random.default_rng(R)
+    lays = _guard_variety_layouts(n, R, rng)
+    cfg = EnvironmentConfig(grid_rows=R, grid_cols=R, max_steps=60)
+    envs = [HeistEnv(n, cfg, max_cams=2, max_guards=4, max_path=24, device=gpu_device) for _ in range(2)]
+    envs[1].set_guard_cones(False)
+    for e in envs:
+        e.set_layouts(lays, budget=60)
+    o = [e.reset() for e in envs]
+    assert torch.equal(o[0], o[1])
+    sample = rng.choice(n, 24, replace=False)
+    oracles = []
+    for i in sample:
+        ob = po.OracleEnv(R, R, 60, (1, 1), (R - 2, R - 2), 60)
+        ob.set_layout(*lays[i])
+        ob.reset()
+        oracles.append(ob)
+    g = torch.Generator(device="cpu").manual_seed(R)
+    for t in range(200):
+        a = torch.randint(0, 5, (n,), generator=g)
+        r = [e.step(a) for e in envs]
+        for x, y in zip(r[0], r[1]):
+            assert torch.equal(x, y), t
+        assert torch.equal(envs[0].reward64, envs[1].reward64), t
+        obs = r[0][0].cpu().numpy()
+        r64 = envs[0].reward64.cpu().numpy()
+        for i, ob in zip(sample, oracles):
+            rr, d, _ = ob.step(int(a[i]))
+            if d:
+                ob.reset()
+            assert r64[i] == rr, (t, i)
+            assert obs[i].tobytes() == ob.state_tensor().tobytes(), (t, i)
+    s0, s1 = envs[0].export(), envs[1].export()
+    assert torch.equal(s0["guard_idx"], s1["guard_idx"]) and torch.equal(s0["guard_heading"], s1["guard_heading"])

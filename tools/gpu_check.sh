@@ -22,7 +22,7 @@ nproc > "$OUT/nproc.txt"; lscpu > "$OUT/lscpu.txt" 2>&1
 for s in ${STEPS:-pytest smoke bench prof}; do
   case $s in
     pytest) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
-    pytestall) step pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+    pytestall) step pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread ;;
     pytestw) for w in 1 4; do HEIST_STEP_WAVES=$w step pytest_env_w$w 900 python -m pytest tests/test_gpu_env.py -x -q; done ;;
     pytestu) for o in 8; do HEIST_STEP_OCC=$o step pytest_env_o$o 900 python -m pytest tests/test_gpu_env.py -x -q; done ;;
     pytesto8) for w in 1 2 4; do HEIST_STEP_OCC=8 HEIST_STEP_WAVES=$w step pytest_env_w${w}_o8 900 python -m pytest tests/test_gpu_env.py -x -q; done ;;
@@ -37,10 +37,14 @@ for s in ${STEPS:-pytest smoke bench prof}; do
     tprobe) step probe_train 600 python tools/probe_train.py ;;
     pstamp) PROBE_STAMPS=1 step policy_stamps 300 python tools/probe_policy.py ;;
     sstamp) step step_stamps 300 python tools/probe_step_stamps.py ;;
+    sstampsyn) PROBE_LAYOUTS=synthetic step step_stamps_syn 300 python tools/probe_step_stamps.py ;;
+    mprobesyn) PROBE_LAYOUTS=synthetic step probe_modes_syn 600 python tools/probe_step_modes.py ;;
     uprobe) step probe_update 600 python tools/probe_update.py ;;
     mprobe) step probe_modes 600 python tools/probe_step_modes.py ;;
     vprobe) step probe_variants 600 python tools/probe_step_variants.py ;;
-    envtest) step pytest_env 900 python -m pytest tests/test_gpu_env.py -x -q ;;
+    envtest) step pytest_env 900 python -u -m pytest tests/test_gpu_env.py -x -q --timeout 200 --timeout-method thread ;;
+    quick) step bench_quick 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary ;;
+    quicksyn) step bench_quick_syn 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary --layouts synthetic ;;
     ppmc) for grp in "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS" \
                      "SQ_WAIT_INST_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_MFMA_MOPS_BF16"; do
             i=$((i+1)); PROBE_N=4096 step pmc_policy$i 600 rocprofv3 --pmc $grp --kernel-include-regex solver_conv -d "$OUT/pp$i" -o pol --output-format csv -- python3 tools/probe_policy.py

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("--envs", type=int, default=4096)
+    ap.add_argument("--workload", default="architect", help="bench.py --layouts of the profiled command")
+    ap.add_argument("--profile", default=None, help="run tag the passes come from (e.g. r02a)")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "heist_step_traffic.json"))
     a = ap.parse_args()
@@ -38,7 +40,8 @@ def main():
     f_kb, w_kb = statistics.median(fetch), statistics.median(write)
     fetch_b = 2 * f_kb * 1024.0
     write_b = w_kb * 1024.0
-    out = {"kernel": "heist::step_kernel", "envs": a.envs, "dispatches": [len(fetch), len(write)],
+    out = {"kernel": "heist::step_kernel", "envs": a.envs, "workload": a.workload,
+           "profile": a.profile or os.path.basename(os.path.dirname(os.path.abspath(a.fetch_dir))), "dispatches": [len(fetch), len(write)],
            "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
            "fetch_bytes_corrected": fetch_b, "write_bytes": write_b,
            "hbm_bytes_per_launch": fetch_b + write_b,

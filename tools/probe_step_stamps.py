@@ -19,6 +19,16 @@ from heist_amd import EnvironmentConfig, HeistEnv  # noqa: E402
 from heist_amd import _native as nat  # noqa: E402
 from heist_amd.layouts import valid_synthetic_layouts  # noqa: E402
 
+
+def bench_layouts(env, seed=1234):
+    """bench.py's headline layouts (PROBE_LAYOUTS=architect, default: the fixed Architect
+    checkpoint at T=1.0, budget 15) or its synthetic mix (PROBE_LAYOUTS=synthetic)."""
+    if os.environ.get("PROBE_LAYOUTS", "architect") == "architect":
+        import bench
+        bench.architect_layouts(env, 15, seed=seed)
+    else:
+        valid_synthetic_layouts(env, 15, seed=seed)
+
 PHASES = ["prefetch", "update+publish", "raycast", "reward", "auto_reset", "obs_write", "store"]
 
 
@@ -30,7 +40,7 @@ def main():
     n = int(os.environ.get("PROBE_N", "4096"))
     waves = int(os.environ.get("HEIST_STEP_WAVES", "4"))
     env = HeistEnv(n, EnvironmentConfig(), max_cams=8, max_guards=4, max_path=16, device="cuda", auto_reset=True)
-    valid_synthetic_layouts(env, 15, seed=1234)
+    bench_layouts(env)
     env.reset()
     acts = torch.randint(0, 5, (16, n), device="cuda")
     for k in range(10):

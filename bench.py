@@ -340,7 +340,7 @@ def main():
     cnt_x = torch.zeros(N, dtype=torch.int64, device=dev)
     env.count_samples(cnt)
     env.count_exact_rays(cnt_x)
-    n_count = 8
+    n_count = 40  # Architect cameras share their parameters, so the work per tick cycles with the headings
     for k in range(n_count):
         env.step(actions[k])
     env.count_samples(None)

@@ -102,11 +102,15 @@ int heist_count_samples(heist_t h, uint64_t* counter);
 int heist_count_redo(heist_t h, uint64_t* counter);
 
 /* Instrumentation, no reference counterpart: later heist_step calls on h record the shader
- * clock (s_memtime) at 8 phase boundaries of every wavefront into buf[env][wave][8] (waves
- * per env: 4 unless HEIST_STEP_WAVES says otherwise): 0 entry, 1 prefetch landed, 2 emitter
+ * clock (s_memtime) at 8 phase boundaries of every wavefront into buf[env][wave][10] (waves
+ * per env: heist_step_waves(h)): 0 entry, 1 prefetch landed, 2 emitter
  * table published, 3 raycast done, 4 reward done, 5 auto-reset done, 6 observation written,
  * 7 exit.  NULL switches stamping off (default). */
 int heist_step_stamps(heist_t h, uint64_t* buf);
+
+/* Wavefronts per env of h's step / reset kernels (2 unless HEIST_STEP_WAVES chose 1 or 4
+ * at heist_create); no reference counterpart. */
+int heist_step_waves(heist_t h);
 
 /* Raycast arithmetic of later heist_step / heist_reset calls on h: 0 (default) = fp32 fast
  * path with exact fp64 re-cast of every ray that comes within a bounded error of a .5 tie,

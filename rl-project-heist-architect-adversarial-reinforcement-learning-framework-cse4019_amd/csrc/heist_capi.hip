@@ -174,8 +174,11 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
     p.axis_heading[2] = htab[(size_t)(R - 1) * W2 + (-1 + C - 1)];
     p.axis_heading[3] = htab[(size_t)(R - 1) * W2 + (1 + C - 1)];
   }
-  p.step_waves = 4;
-  p.ray_chunk = 4;  // tuning knobs; a combination without a compiled variant falls back to (4, 4, 8)
+  // 2 waves per env: 16 blocks resident per CU (LDS ~5 KB each) and half the redundant
+  // block-uniform work of 4 waves; 23.0 us per 4096-env step vs 26.8 at 4 waves and 24.1
+  // at 1 (C2 Architect layouts with the guard cone cache, gpurun_out r02j)
+  p.step_waves = 2;
+  p.ray_chunk = 4;  // tuning knobs; a combination without a compiled variant falls back to (2, 4, 8)
   // 8 waves per SIMD (64 VGPRs): 4096 envs are two full rounds of 8 workgroups per CU
   // (41.4 us per step vs 46.6 at the unbounded 85 VGPRs / 5 waves, profiles/r01m_*)
   p.step_occ = 8;
@@ -191,7 +194,7 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   p.stamps = nullptr;
   p.vis_gap = heist::vis_gap_for(R, C);
   if (!heist::env_variant_exists(p.step_waves, p.ray_chunk, p.step_occ, p.vis_gap)) {
-    p.step_waves = 4;
+    p.step_waves = 2;
     p.ray_chunk = 4;
     p.step_occ = 8;
     p.vis_gap = heist::vis_gap_for(R, C);
@@ -328,6 +331,11 @@ int heist_step_stamps(heist_t h, uint64_t* buf) {
   if (int rc = check_handle(h)) return rc;
   h->p.stamps = reinterpret_cast<unsigned long long*>(buf);
   return 0;
+}
+
+int heist_step_waves(heist_t h) {
+  if (int rc = check_handle(h)) return -rc;
+  return h->p.step_waves;
 }
 
 int heist_set_ray_mode(heist_t h, int ray_mode) {

@@ -1,9 +1,10 @@
 // heist_env.hip -- CDNA4 kernels for the batched Heist environment.
 //
 // step/reset: one workgroup of W wavefronts (W = 1, 2, 4) owns one environment.
-//   * Prefetch first: the env's tile grid and guard paths
-//     go to LDS, cameras/guards and the observation's static position plane to
-//     registers -- all issued together, so the env costs one HBM round trip.
+//   * Prefetch first: the env's tile grid, padded stop map and guard paths go to LDS,
+//     cameras/guards to registers -- all issued together, so the env costs one HBM round
+//     trip; a cached guard cone follows its guard record.  The observation's static
+//     position plane is the same for every env and is read from L2 by write_obs.
 //   * Cameras and guards are updated in registers (no store -> reload) and flattened
 //     into one ray list; thread t casts rays t, t + 64W, ... (security.py:53-101,
 //     :161-192) with the samples of a ray computed in blocks of four so the wall
@@ -56,7 +57,6 @@ struct EnvLds {
   uint8_t* grid;   // [RC]
   Emit* em;        // [n_emit]
   uint16_t* path;  // [max_guards][max_path]
-  float* plane;    // [RC] static position channel (plane0)
   int* queue;      // [W][64] per-wave exact-path ray queues (cast_rays)
   int* meta;       // [0] emitters, [1] total rays
   uint16_t* cone;  // [max_guards][16] this tick's cached guard cones (kind-2 emitters), see heist_device.h
@@ -80,7 +80,7 @@ __host__ __device__ inline size_t env_lds_bytes(int R, int C, int n_emit, int pa
                                                 int cone_guards = 0) {
   const int RC = R * C;
   return 3 * (size_t)D + align16(RC) + align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) +
-         align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1)) + align16(sizeof(float) * RC) +
+         align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1)) +
          sizeof(int) * 64 * (size_t)waves + 32 + 32 * (size_t)cone_guards;
 }
 
@@ -95,7 +95,6 @@ __device__ __forceinline__ EnvLds carve(unsigned char* smem, int R, int C, int n
   L.grid = smem + o; o += align16(RC);
   L.em = reinterpret_cast<Emit*>(smem + o); o += align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1));
   L.path = reinterpret_cast<uint16_t*>(smem + o); o += align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1));
-  L.plane = reinterpret_cast<float*>(smem + o); o += align16(sizeof(float) * RC);
   L.queue = reinterpret_cast<int*>(smem + o); o += sizeof(int) * 64 * (size_t)waves;
   L.meta = reinterpret_cast<int*>(smem + o); o += 32;
   L.cone = reinterpret_cast<uint16_t*>(smem + o);
@@ -666,12 +665,11 @@ static_assert(sizeof(EmitterRaw) == sizeof(Cam) && sizeof(EmitterRaw) == sizeof(
 __device__ __forceinline__ Cam as_cam(const EmitterRaw& r) { return __builtin_bit_cast(Cam, r); }
 __device__ __forceinline__ Guard as_guard(const EmitterRaw& r) { return __builtin_bit_cast(Guard, r); }
 
-// Issue every per-env HBM read before the first barrier: grid, guard
-// paths and the static position plane (for LDS), this thread's camera/guard record (for
-// registers).  Each thread's first element of every array is loaded before anything is
+// Issue every per-env HBM read before the first barrier: grid, stop map and guard
+// paths (for LDS), this thread's camera/guard record (for registers).  Each thread's first element of every array is loaded before anything is
 // stored, so the whole prefetch is one memory round trip; the loops only cover what one
 // pass of NT threads cannot (W < 4, grids above 32 x 32, long patrol paths).  EnvScalars
-// come in through scalar loads.  The stop map is built from the LDS grid after the barrier.
+// come in through scalar loads.
 template <int NT>
 __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds& L, int n_cams, int n_em,
                                          EmitterRaw& raw) {
@@ -683,16 +681,12 @@ __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds
   const bool vec = (RC & 3) == 0;
   const int n4 = vec ? RC / 4 : 0;
   const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
-  const float4* pl0 = reinterpret_cast<const float4*>(p.plane0);
   uint32_t* d4 = reinterpret_cast<uint32_t*>(L.grid);
-  float4* lp = reinterpret_cast<float4*>(L.plane);
 
   uint32_t gv = 0u;
-  float4 pv = make_float4(0.f, 0.f, 0.f, 0.f);
   uint16_t wv = 0;
   if (t < n4) {
     gv = s4[t];
-    pv = pl0[t];
   }
   if (t < pw) wv = ps[t];
   // the layout's padded stop map, built once by set_layout_kernel
@@ -711,19 +705,16 @@ __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds
   }
   if (t < n4) {
     d4[t] = gv;
-    lp[t] = pv;
   }
   if (t < pw) L.path[t] = wv;
   if (t < n_stop) sd[t] = sv;
   for (int i = t + NT; i < n_stop; i += NT) sd[i] = ss[i];
   for (int i = t + NT; i < n4; i += NT) {
     d4[i] = s4[i];
-    lp[i] = pl0[i];
   }
   if (!vec) {
     for (int i = t; i < RC; i += NT) {
       L.grid[i] = src[i];
-      L.plane[i] = p.plane0[i];
     }
   }
   for (int i = t + NT; i < pw; i += NT) L.path[i] = ps[i];
@@ -749,7 +740,7 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
   float* o = obs + (size_t)e * 3 * RC;
   const int solver = s.pos_r * C + s.pos_c;
   const int vault = p.vr * C + p.vc;
-  const float sv = 1.0f + L.plane[solver];  // == plane1[solver]: fl32(1 + g) (see heist_create)
+  const float sv = p.plane1[solver];  // fl32(1 + g) (see heist_create)
   static_assert((kRing & 1) == 0, "padded vis rows of a C % 4 == 0 grid are 2-byte aligned");
   if ((C & 3) == 0) {  // a float4 never crosses a row; 4 vis bytes in two aligned u16 reads
     const int n4 = RC / 4, c4 = C / 4;
@@ -779,7 +770,7 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
     } else {
     const int qs = solver >> 2, qv = vault >> 2;
     for (int q = t - H; q < n4; q += H) {
-      float4 v = reinterpret_cast<const float4*>(L.plane)[q];
+      float4 v = reinterpret_cast<const float4*>(p.plane0)[q];  // the handle's static plane (L2-resident)
       if (q == qs) patch4(v, solver & 3, sv);          // only the solver's and the vault's
       if (q == qv) patch4(v, vault & 3, p.vault_val);  // float4 take these branches
       o2[q] = v;
@@ -796,7 +787,7 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
         const int r = cell / C;
         v = (L.vis[L.at(r, cell - r * C)] | L.gvis[L.at(r, cell - r * C)]) ? 1.0f : 0.0f;
       } else {
-        v = cell == vault ? p.vault_val : (cell == solver ? sv : L.plane[cell]);
+        v = cell == vault ? p.vault_val : (cell == solver ? sv : p.plane0[cell]);
       }
       o[q] = v;
     }
@@ -839,6 +830,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   extern __shared__ __align__(16) unsigned char smem[];
   const int e = p.order[blockIdx.x];
   const int t = threadIdx.x;
+  if (p.probe_mode == 6) return;  // profiling: launch + dispatch floor
   HEIST_STEP_STAMP(0);
   if (STAMP && (t & 63) == 0) {
     unsigned long long* q = p.stamps + ((size_t)e * W + (t >> 6)) * 10;
@@ -855,6 +847,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   if (t >= n_cams && t < n_em) stage_guard_cone(p, e, L, t - n_cams, as_guard(raw), act);
   clear_vis<NT>(p, L);
   __syncthreads();  // grid, paths, cached guard cones in LDS
+  if (p.probe_mode == 7) return;  // profiling: prefetch floor
   HEIST_STEP_STAMP(1);
 
   double reward = 0.0;
@@ -962,13 +955,13 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
       gp->idx = 0;
       gp->pos = pos0;
       if (gslot != kUncached) {  // cone of (patrol point 0, this tick's heading slot)
-        const uint4* src = reinterpret_cast<const uint4*>(p.cones + cone_entry(p, e, g, 0, gslot));
-        const uint4 a = src[0], b = src[1];
-        gp->nslot = (uint8_t)(b.w >> 16);  // row 15
+        const uint16_t* ce = p.cones + cone_entry(p, e, g, 0, gslot);
+        gp->nslot = (uint8_t)ce[15];  // row 15
         if (any_moved) {  // the first raycast pass is over (barrier above)
+          const uint4* src = reinterpret_cast<const uint4*>(ce);
           uint4* dst = reinterpret_cast<uint4*>(L.cone + 16 * g);
-          dst[0] = a;
-          dst[1] = b;
+          dst[0] = src[0];
+          dst[1] = src[1];
           L.em[t].row = unpack_r(pos0);
           L.em[t].col = unpack_c(pos0);
         }

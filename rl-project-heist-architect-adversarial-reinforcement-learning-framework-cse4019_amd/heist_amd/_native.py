@@ -35,6 +35,7 @@ SIGNATURES = {
     "heist_count_redo": (_i, [_vp, _vp]),
     "heist_set_ray_mode": (_i, [_vp, _i]),
     "heist_set_guard_cones": (_i, [_vp, _i]),
+    "heist_step_waves": (_i, [_vp]),
     "heist_step_stamps": (_i, [_vp, _vp]),
     "heist_bfs_valid": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "heist_cones": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp]),

@@ -5,7 +5,8 @@ Python reference on the nets.npz seed-32 ArchitectNetwork: buffered transitions 
 losses out, and per parameter tensor the post-update (clipped) gradient and the
 parameter change as norms + fixed random projections.  Tolerance 1e-4 (north star) on
 the losses; the gradient / step summaries to 1e-4 relative (fp32 conv backward on a
-different device and library).  kat.json's architect_reward table pins
+different device and library); parameters whose gradient is cancellation noise (below
+1e-6 of the largest) get only Adam's lr bound on their step.  kat.json's architect_reward table pins
 calculate_architect_reward (rewards.py:43-73).
 """
 import numpy as np
@@ -38,6 +39,7 @@ def _check_cases(device):
             m = ag.update(collective=False)
             got = [m["architect_policy_loss"], m["architect_value_loss"], m["architect_total_loss"]]
             np.testing.assert_allclose(got, z[key + "loss"], rtol=1e-4, atol=1e-4, err_msg=key)
+            gmax = float(np.max(z[key + "gnorm"]))
             for i, (p, q) in enumerate(zip(ag.network.parameters(), p0)):
                 g = (p.grad if p.grad is not None else torch.zeros_like(p)).detach().double().reshape(-1).cpu().numpy()
                 d = (p.detach() - q).double().reshape(-1).cpu().numpy()
@@ -47,6 +49,11 @@ def _check_cases(device):
                                            err_msg="%s grad norm %d" % (key, i))
                 np.testing.assert_allclose(P @ g, z[key + "gproj"][i], rtol=0, atol=4e-4 * gscale + 1e-9,
                                            err_msg="%s grad proj %d" % (key, i))
+                if float(z[key + "gnorm"][i]) < 1e-6 * gmax:
+                    # a gradient at fp32 cancellation-noise level (both sides): Adam turns it
+                    # into a step of noise, |m_hat / sqrt(v_hat)| <= (1 - b1) / sqrt(1 - b2) per element
+                    assert np.abs(d).max() <= ag.optimizer.param_groups[0]["lr"] * 3.17, (key, i)
+                    continue
                 dscale = max(float(z[key + "dnorm"][i]), 1e-12)
                 np.testing.assert_allclose(np.linalg.norm(d), z[key + "dnorm"][i], rtol=1e-3, atol=1e-9,
                                            err_msg="%s step norm %d" % (key, i))

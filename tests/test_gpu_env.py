@@ -186,7 +186,9 @@ def test_step_stamps_instrumentation(gpu_device):
     for e in envs:
         e.set_layouts(lays, budget=15)
         e.reset()
-    buf = torch.zeros((n, 4, 10), dtype=torch.int64, device=gpu_device)
+    w = nat.lib().heist_step_waves(envs[0]._h)
+    assert w in (1, 2, 4)
+    buf = torch.zeros((n, w, 10), dtype=torch.int64, device=gpu_device)
     g = torch.Generator(device="cpu").manual_seed(3)
     for t in range(20):
         a = torch.randint(0, 5, (n,), generator=g)

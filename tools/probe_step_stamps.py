@@ -38,8 +38,8 @@ def q(x, p):
 
 def main():
     n = int(os.environ.get("PROBE_N", "4096"))
-    waves = int(os.environ.get("HEIST_STEP_WAVES", "4"))
     env = HeistEnv(n, EnvironmentConfig(), max_cams=8, max_guards=4, max_path=16, device="cuda", auto_reset=True)
+    waves = nat.lib().heist_step_waves(env._h)
     bench_layouts(env)
     env.reset()
     acts = torch.randint(0, 5, (16, n), device="cuda")

@@ -78,11 +78,19 @@ def cpu_baseline(layouts, cfg, budget, target_s=10.0, threads=1):
     t0 = time.perf_counter()
     n = po.run_random(envs, steps, seed=2, n_threads=threads)
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "env-steps/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
-            "host_cpus": os.cpu_count(),
+    out = {"value": n / dt, "unit": "env-steps/s", "cores": threads, "kind": "port", "cpu_model": cpu_model(),
+           "host_cpus": os.cpu_count(),
             "sample": "%d of the bench's layouts x %d ticks (%d env-steps, %.1f s wall), random actions, "
                       "auto-reset, state tensor each tick; C oracle (oracle/heist_oracle.c, host libm), %d thread%s"
                       % (len(sample), steps, n, dt, threads, "s" if threads > 1 else "")}
+    rf = os.path.join(ROOT, "profiles", "cpu_ratio.json")
+    if os.path.exists(rf):  # tools/cpu_ratio.py: C oracle vs the Python reference on one build-container core
+        with open(rf) as f:
+            ratio = json.load(f)["oracle_over_reference"]
+        out["python_reference_equivalent"] = {
+            "value": out["value"] / ratio, "unit": "env-steps/s", "oracle_over_reference": ratio,
+            "source": "profiles/cpu_ratio.json (tools/cpu_ratio.py: same layouts, one core of the build container)"}
+    return out
 
 
 def architect_layouts(env, budget, seed, ckpt=None, max_rounds=20):

@@ -111,7 +111,7 @@ struct EnvParams {
   int probe_mode;             // profiling only (HEIST_PROBE_MODE): 0 normal, 1 no rays, 2 angles+sin/cos only,
                               // 3 marches with a fixed direction (no sin/cos), 4 no observation write,
                               // 5 neither rays nor observation, 6 return at entry, 7 return after the
-                              // prefetch; results are wrong for 1-7
+                              // raycast; results are wrong for 1-7
 };
 
 // security.py:67 max(int(fov * 2), 30); capped at 32000 rays (fov 16000 deg) so the

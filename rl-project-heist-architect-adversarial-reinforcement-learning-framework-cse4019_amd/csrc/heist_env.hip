@@ -54,12 +54,15 @@ struct EnvLds {
   uint8_t* vis;    // LDS offset D: visibility with the same padded geometry (ring bytes unused): camera
                    // rays and live-raycast guards
   uint8_t* gvis;   // LDS offset 2D: the cached guard cones (same geometry); visibility = vis | gvis
+  uint8_t* gvis_r; // LDS offset 3D: the cached guard cones after an in-step auto-reset (guards at patrol point 0)
   uint8_t* grid;   // [RC]
   Emit* em;        // [n_emit]
   uint16_t* path;  // [max_guards][max_path]
   int* queue;      // [W][64] per-wave exact-path ray queues (cast_rays)
   int* meta;       // [0] emitters, [1] total rays
-  uint16_t* cone;  // [max_guards][16] this tick's cached guard cones (kind-2 emitters), see heist_device.h
+  uint16_t* cone;  // [2][max_guards][16] cached guard cones (kind-2 emitters, heist_device.h): this tick's
+                   // pose, then the pose an auto-reset would give (patrol point 0, same heading)
+  uint32_t* rpos;  // [max_guards] patrol point 0 of each guard (row | col << 8), for the reset cones
   int PC;          // padded row stride C + 2G
   int off0;        // padded index of tile (0, 0): G * PC + G
   __device__ __forceinline__ int at(int r, int c) const { return off0 + r * PC + c; }
@@ -79,25 +82,28 @@ __host__ __device__ inline int padded_bytes(int R, int C) { return (R + 2 * kRin
 __host__ __device__ inline size_t env_lds_bytes(int R, int C, int n_emit, int path_words, int D, int waves,
                                                 int cone_guards = 0) {
   const int RC = R * C;
-  return 3 * (size_t)D + align16(RC) + align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) +
+  return 4 * (size_t)D + align16(RC) + align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) +
          align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1)) +
-         sizeof(int) * 64 * (size_t)waves + 32 + 32 * (size_t)cone_guards;
+         sizeof(int) * 64 * (size_t)waves + 32 + 68 * (size_t)cone_guards;
 }
 
 template <int D>
-__device__ __forceinline__ EnvLds carve(unsigned char* smem, int R, int C, int n_emit, int path_words, int waves) {
+__device__ __forceinline__ EnvLds carve(unsigned char* smem, int R, int C, int n_emit, int path_words, int waves,
+                                        int cone_guards = 0) {
   const int RC = R * C;
   EnvLds L;
   L.wall = smem;
   L.vis = smem + D;
   L.gvis = smem + 2 * (size_t)D;
-  size_t o = 3 * (size_t)D;
+  L.gvis_r = smem + 3 * (size_t)D;
+  size_t o = 4 * (size_t)D;
   L.grid = smem + o; o += align16(RC);
   L.em = reinterpret_cast<Emit*>(smem + o); o += align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1));
   L.path = reinterpret_cast<uint16_t*>(smem + o); o += align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1));
   L.queue = reinterpret_cast<int*>(smem + o); o += sizeof(int) * 64 * (size_t)waves;
   L.meta = reinterpret_cast<int*>(smem + o); o += 32;
   L.cone = reinterpret_cast<uint16_t*>(smem + o);
+  L.rpos = reinterpret_cast<uint32_t*>(L.cone + 32 * cone_guards);
   L.PC = C + 2 * kRing;
   L.off0 = kRing * L.PC + kRing;
   return L;
@@ -527,15 +533,16 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
   }
 }
 
-// Publish this tick's emitter table: thread t < n_em holds emitter t in E.  Every
-// emitter lives in wave 0 (at most 64 of them), where an exclusive lane scan of the
-// emitters' chunk counts (ceil((num_rays + 1) / 64) chunks of 64 rays) gives each emitter
-// its first chunk index.
+// Publish this tick's emitter table: thread t < n_em holds emitter SLOT t in E (camera
+// slots 0 .. max_cams-1, then guard slots; a slot past the env's camera or guard count has
+// kind -1 and no rays).  Every slot lives in wave 0 (at most 64 of them), where an
+// exclusive lane scan of the emitters' chunk counts (ceil((num_rays + 1) / 64) chunks of
+// 64 rays) gives each emitter its first chunk index.
 static_assert(kMaxEmitters <= 64, "publish_emitters keeps every emitter in wave 0");
 __device__ __forceinline__ void publish_emitters(const EnvLds& L, Emit E, int n_em) {
   const int t = threadIdx.x;
   if (t < 64) {
-    const int cnt = (t < n_em && E.kind != 2) ? (E.num_rays + 1 + 63) / 64 : 0;  // kind 2: cached cone, no rays
+    const int cnt = (t < n_em && (E.kind == 0 || E.kind == 1)) ? (E.num_rays + 1 + 63) / 64 : 0;  // 2: cached cone
     int incl = cnt;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -604,30 +611,43 @@ __device__ __forceinline__ void stage_guard_cone(const EnvParams& p, int e, cons
 // OR every cached guard cone staged in LDS into the visibility plane: thread q of the
 // 16 x 15 window sets tile (row + q/16 - 7, col + q%16 - 7) if its bit is set (bits only
 // ever name tiles inside the grid, so the address is always in the plane).
-template <int NT>
-__device__ __forceinline__ void stamp_guard_cones(const EnvLds& L, int n_cams, int n_em) {
-  for (int k = n_cams; k < n_em; ++k) {
+// RESET: the cones an in-step auto-reset gives (staged after this tick's, guards at
+// patrol point 0) into the reset plane gvis_r instead.
+template <int NT, bool RESET = false>
+__device__ __forceinline__ void stamp_guard_cones(const EnvLds& L, int mc, int n_slot) {
+  const int mg = n_slot - mc;
+  for (int k = mc; k < n_slot; ++k) {
     if (uni(L.em[k].kind) != 2) continue;
-    const int r0 = uni(L.em[k].row) - kConeRange, c0 = uni(L.em[k].col) - kConeRange;
-    const uint16_t* rows = L.cone + 16 * (k - n_cams);
+    int r0, c0;
+    if (RESET) {
+      const int rp = uni((int)L.rpos[k - mc]);
+      r0 = unpack_r(rp) - kConeRange;
+      c0 = unpack_c(rp) - kConeRange;
+    } else {
+      r0 = uni(L.em[k].row) - kConeRange;
+      c0 = uni(L.em[k].col) - kConeRange;
+    }
+    const uint16_t* rows = L.cone + 16 * ((RESET ? mg : 0) + k - mc);
+    uint8_t* plane = RESET ? L.gvis_r : L.gvis;
     for (int q = threadIdx.x; q < 16 * (2 * kConeRange + 1); q += NT) {
       const int rr = q >> 4, cc = q & 15;
-      if ((rows[rr] >> cc) & 1u) L.gvis[L.at(r0 + rr, c0 + cc)] = 1;
+      if ((rows[rr] >> cc) & 1u) plane[L.at(r0 + rr, c0 + cc)] = 1;
     }
   }
 }
 
-// Visibility (visibility.py:31-65) once the emitter table is in LDS and vis is zeroed.
+// Visibility (visibility.py:31-65) once the emitter table (n_slot slots, guards from slot
+// mc on) is in LDS and vis is zeroed.
 template <int NT, int U, int D>
-__device__ __forceinline__ void raycast_pass(const EnvParams& p, int e, unsigned char* smem, const EnvLds& L, int n_em,
-                                             int n_cams) {
+__device__ __forceinline__ void raycast_pass(const EnvParams& p, int e, unsigned char* smem, const EnvLds& L, int n_slot,
+                                             int mc) {
   __syncthreads();  // emitter table, stop map and cleared vis in place
   const int t = threadIdx.x;
-  if (t >= n_cams && t < n_em) {  // a live guard's own tile (visibility.py:59; a cached cone holds it)
+  if (t >= mc && t < n_slot) {  // a live guard's own tile (visibility.py:59; a cached cone holds it)
     const Emit E = L.em[t];
     if (E.kind == 1) L.vis[L.at(E.row, E.col)] = 1;
   }
-  stamp_guard_cones<NT>(L, n_cams, n_em);
+  stamp_guard_cones<NT>(L, mc, n_slot);
   if (p.probe_mode != 1 && p.probe_mode != 5) {
     if (p.sample_counter || p.redo_counter)
       cast_rays<NT, U, D, true>(smem, L, p.ray_mode, p.probe_mode, p.half_deg);
@@ -644,9 +664,13 @@ template <int NT, bool RAYS = true, bool CONES = true>
 __device__ __forceinline__ void clear_vis(const EnvParams& p, const EnvLds& L) {
   uint32_t* v4 = reinterpret_cast<uint32_t*>(L.vis);
   uint32_t* g4 = reinterpret_cast<uint32_t*>(L.gvis);
+  uint32_t* r4 = reinterpret_cast<uint32_t*>(L.gvis_r);
   for (int i = threadIdx.x; i < (padded_bytes(p.R, p.C) + 3) / 4; i += NT) {
     if (RAYS) v4[i] = 0u;
-    if (CONES) g4[i] = 0u;
+    if (CONES) {
+      g4[i] = 0u;
+      r4[i] = 0u;
+    }
   }
 }
 
@@ -665,30 +689,24 @@ static_assert(sizeof(EmitterRaw) == sizeof(Cam) && sizeof(EmitterRaw) == sizeof(
 __device__ __forceinline__ Cam as_cam(const EmitterRaw& r) { return __builtin_bit_cast(Cam, r); }
 __device__ __forceinline__ Guard as_guard(const EmitterRaw& r) { return __builtin_bit_cast(Guard, r); }
 
-// Issue every per-env HBM read before the first barrier: grid, stop map and guard
-// paths (for LDS), this thread's camera/guard record (for registers).  Each thread's first element of every array is loaded before anything is
+// Issue every per-env HBM read at once: grid and stop map (for LDS), this thread's
+// camera/guard record (for registers).  Each thread's first element of every array is loaded before anything is
 // stored, so the whole prefetch is one memory round trip; the loops only cover what one
-// pass of NT threads cannot (W < 4, grids above 32 x 32, long patrol paths).  EnvScalars
-// come in through scalar loads.
+// pass of NT threads cannot (W < 4, grids above 32 x 32, long patrol paths).  Thread t <
+// max_cams + max_guards loads emitter slot t (camera t, then guard t - max_cams) whether or
+// not the env fills it, so no load waits for the EnvScalars (scalar loads) to arrive.
 template <int NT>
-__device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds& L, int n_cams, int n_em,
-                                         EmitterRaw& raw) {
+__device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds& L, EmitterRaw& raw) {
   const int t = threadIdx.x;
   const int RC = p.RC;
   const uint8_t* src = p.grid + (size_t)e * RC;
-  const int pw = p.max_guards * p.max_path;
-  const uint16_t* ps = p.paths + (size_t)e * pw;
   const bool vec = (RC & 3) == 0;
   const int n4 = vec ? RC / 4 : 0;
   const uint32_t* s4 = reinterpret_cast<const uint32_t*>(src);
   uint32_t* d4 = reinterpret_cast<uint32_t*>(L.grid);
 
   uint32_t gv = 0u;
-  uint16_t wv = 0;
-  if (t < n4) {
-    gv = s4[t];
-  }
-  if (t < pw) wv = ps[t];
+  if (t < n4) gv = s4[t];
   // the layout's padded stop map, built once by set_layout_kernel
   const float4* ss = reinterpret_cast<const float4*>(p.stop + (size_t)e * p.stop_bytes);
   float4* sd = reinterpret_cast<float4*>(L.wall);
@@ -697,16 +715,13 @@ __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds
   if (t < n_stop) sv = ss[t];
   raw.a = make_uint4(0u, 0u, 0u, 0u);
   raw.b = raw.a;
-  if (t < n_em) {
-    const uint4* rs = t < n_cams ? reinterpret_cast<const uint4*>(p.cams + (size_t)e * p.max_cams + t)
-                                 : reinterpret_cast<const uint4*>(p.guards + (size_t)e * p.max_guards + (t - n_cams));
+  if (t < p.max_cams + p.max_guards) {
+    const uint4* rs = t < p.max_cams ? reinterpret_cast<const uint4*>(p.cams + (size_t)e * p.max_cams + t)
+                                     : reinterpret_cast<const uint4*>(p.guards + (size_t)e * p.max_guards + (t - p.max_cams));
     raw.a = rs[0];
     raw.b = rs[1];
   }
-  if (t < n4) {
-    d4[t] = gv;
-  }
-  if (t < pw) L.path[t] = wv;
+  if (t < n4) d4[t] = gv;
   if (t < n_stop) sd[t] = sv;
   for (int i = t + NT; i < n_stop; i += NT) sd[i] = ss[i];
   for (int i = t + NT; i < n4; i += NT) {
@@ -717,7 +732,6 @@ __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds
       L.grid[i] = src[i];
     }
   }
-  for (int i = t + NT; i < pw; i += NT) L.path[i] = ps[i];
 }
 
 // Set lane m (0..3) of v; m outside 0..3 leaves v unchanged (no dynamic indexing:
@@ -734,7 +748,7 @@ __device__ __forceinline__ void patch4(float4& v, int m, float val) {
 // wins if the solver stands on it).
 template <int NT>
 __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvScalars& s, const EnvLds& L,
-                                          float* __restrict__ obs) {
+                                          const uint8_t* cones, float* __restrict__ obs) {
   const int t = threadIdx.x;
   const int RC = p.RC, C = p.C;
   float* o = obs + (size_t)e * 3 * RC;
@@ -752,20 +766,22 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
     if (t < H) {
     for (int q = t; q < n4; q += H) {
       const uint32_t b = *reinterpret_cast<const uint32_t*>(L.grid + 4 * q);
-      o0[q] = make_float4(p.tile_lut[b & 7], p.tile_lut[(b >> 8) & 7], p.tile_lut[(b >> 16) & 7],
-                          p.tile_lut[(b >> 24) & 7]);
+      // float32(tile) / 5 == float32(tile) * 0.2f for every tile type 0..7 (checked), and the
+      // byte -> float conversion is one v_cvt_f32_ubyteN
+      o0[q] = make_float4((float)(b & 0xff) * 0.2f, (float)((b >> 8) & 0xff) * 0.2f,
+                          (float)((b >> 16) & 0xff) * 0.2f, (float)(b >> 24) * 0.2f);
       const int r = q / c4;
       const int a = L.at(r, 4 * (q - r * c4));
       uint32_t v;
       if ((kRing & 3) == 0) {
-        v = *reinterpret_cast<const uint32_t*>(L.vis + a) | *reinterpret_cast<const uint32_t*>(L.gvis + a);
+        v = *reinterpret_cast<const uint32_t*>(L.vis + a) | *reinterpret_cast<const uint32_t*>(cones + a);
       } else {
         const uint16_t* vp2 = reinterpret_cast<const uint16_t*>(L.vis + a);
-        const uint16_t* gp2 = reinterpret_cast<const uint16_t*>(L.gvis + a);
+        const uint16_t* gp2 = reinterpret_cast<const uint16_t*>(cones + a);
         v = ((uint32_t)vp2[0] | ((uint32_t)vp2[1] << 16)) | ((uint32_t)gp2[0] | ((uint32_t)gp2[1] << 16));
       }
-      o1[q] = make_float4((v & 0xff) ? 1.0f : 0.0f, (v & 0xff00) ? 1.0f : 0.0f, (v & 0xff0000) ? 1.0f : 0.0f,
-                          (v & 0xff000000u) ? 1.0f : 0.0f);
+      // visibility bytes are 0 or 1 in both planes, so their OR converts directly
+      o1[q] = make_float4((float)(v & 0xff), (float)((v >> 8) & 0xff), (float)((v >> 16) & 0xff), (float)(v >> 24));
     }
     } else {
     const int qs = solver >> 2, qv = vault >> 2;
@@ -785,7 +801,7 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
         v = p.tile_lut[L.grid[cell] & 7];
       } else if (ch == 1) {
         const int r = cell / C;
-        v = (L.vis[L.at(r, cell - r * C)] | L.gvis[L.at(r, cell - r * C)]) ? 1.0f : 0.0f;
+        v = (L.vis[L.at(r, cell - r * C)] | cones[L.at(r, cell - r * C)]) ? 1.0f : 0.0f;
       } else {
         v = cell == vault ? p.vault_val : (cell == solver ? sv : p.plane0[cell]);
       }
@@ -837,51 +853,65 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     q[8] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
     q[9] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
   }
-  const EnvLds L = carve<D>(smem, p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path, W);
-  EnvScalars s = p.scal[e];
-  const int n_cams = s.n_cams, n_em = s.n_cams + s.n_guards;
-  const bool act = !s.done;
+  const EnvLds L = carve<D>(smem, p.R, p.C, p.max_cams + p.max_guards, 0, W, p.max_guards);
   EmitterRaw raw;
-  prefetch<NT>(p, e, L, n_cams, n_em, raw);
+  prefetch<NT>(p, e, L, raw);
+  if (t == 0) L.meta[5] = 0;  // guards off their patrol start after this tick: bit 0 live, bit 1 cached
+  EnvScalars s = p.scal[e];
+  const int mc = p.max_cams, n_slot = p.max_cams + p.max_guards;  // emitter slots: cameras, then guards
+  const bool live_cam = t < s.n_cams, live_guard = t >= mc && t - mc < s.n_guards;
+  const bool act = !s.done;
   const int a_raw = (int)actions[e];
-  if (t >= n_cams && t < n_em) stage_guard_cone(p, e, L, t - n_cams, as_guard(raw), act);
   clear_vis<NT>(p, L);
-  __syncthreads();  // grid, paths, cached guard cones in LDS
-  if (p.probe_mode == 7) return;  // profiling: prefetch floor
   HEIST_STEP_STAMP(1);
-
-  double reward = 0.0;
-  int status = kAlreadyDone;
-  if (act) {
-    // 1. move (environment.py:239-246)
-    const int a = (a_raw < 0 || a_raw > 4) ? 0 : a_raw;
-    // environment.py:52-58: 0 stay, 1 up, 2 down, 3 left, 4 right
-    const int nr = s.pos_r + (a == 1 ? -1 : (a == 2 ? 1 : 0)), nc = s.pos_c + (a == 3 ? -1 : (a == 4 ? 1 : 0));
-    if (nr >= 0 && nr < p.R && nc >= 0 && nc < p.C && L.grid[nr * p.C + nc] != kWall) {
-      s.pos_r = nr;
-      s.pos_c = nc;
-    }
-  }
+  // One barrier before the raycast: the emitter slots all live in wave 0, whose lanes
+  // update them from their records alone (a guard's next patrol point and its cached
+  // cone come straight from HBM, not from LDS), so nothing before it reads another
+  // wave's LDS writes; the solver's move, which reads the LDS grid, follows the raycast.
   // 2. cameras rotate, guards patrol (security.py:49-51, :145-159) -- in registers
   uint16_t pos0 = 0;  // a guard thread's patrol start, for the auto-reset below
   bool off_start = false;  // a guard thread's guard stands off its patrol start
   uint8_t gslot = kUncached;  // a guard thread's heading slot after this tick (cached cones)
   Emit E;
-  if (t < n_cams) {
+  E.kind = -1;  // an empty slot
+  if (live_cam) {
     Cam cm = as_cam(raw);
     if (act) {
       cm.heading = py_mod360(cm.heading + cm.speed * 1.0);
       p.cams[(size_t)e * p.max_cams + t].heading = cm.heading;
     }
     E = cam_emit(cm);
-  } else if (t < n_em) {
-    const int g = t - n_cams;
+  } else if (live_guard) {
+    const int g = t - mc;
     Guard gd = as_guard(raw);
     pos0 = gd.pos0;
-    if (act && gd.len >= 2) {
-      int nidx = gd.idx + gd.step;
+    const bool moves = act && gd.len >= 2;
+    int nidx = gd.idx;
+    if (moves) {
+      nidx += gd.step;
       if (nidx >= gd.len) nidx -= gd.len;
-      const uint16_t np = L.path[g * p.max_path + nidx];
+    }
+    // the next patrol point, the cone of the pose after the move and the cone an
+    // auto-reset would give (patrol point 0, the same heading), loaded together
+    const uint16_t np = moves ? p.paths[((size_t)e * p.max_guards + g) * p.max_path + nidx] : gd.pos;
+    if (gd.hslot != kUncached) {
+      const int slot = moves ? gd.nslot : gd.hslot;
+      const uint4* src = reinterpret_cast<const uint4*>(p.cones + cone_entry(p, e, g, nidx, slot));
+      const uint4* rsrc = reinterpret_cast<const uint4*>(p.cones + cone_entry(p, e, g, 0, slot));
+      const uint4 ca = src[0], cb = src[1], ra = rsrc[0], rb = rsrc[1];
+      uint4* dst = reinterpret_cast<uint4*>(L.cone + 16 * g);
+      uint4* rdst = reinterpret_cast<uint4*>(L.cone + 16 * (p.max_guards + g));
+      dst[0] = ca;
+      dst[1] = cb;
+      rdst[0] = ra;
+      rdst[1] = rb;
+      L.rpos[g] = pos0;
+      if (moves) {  // row 15 of the entry: the slot after the next move
+        gd.hslot = gd.nslot;
+        gd.nslot = (uint8_t)(cb.w >> 16);
+      }
+    }
+    if (moves) {
       gd.heading = guard_heading_after(p, unpack_r(np) - unpack_r(gd.pos), unpack_c(np) - unpack_c(gd.pos),
                                        gd.heading);
       gd.idx = (int16_t)nidx;
@@ -890,23 +920,35 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
       gp->heading = gd.heading;
       gp->idx = gd.idx;
       gp->pos = gd.pos;
-      if (gd.hslot != kUncached) {  // the staged entry's row 15: the slot after the next move
-        gd.hslot = gd.nslot;
-        gd.nslot = (uint8_t)L.cone[16 * g + 15];
+      if (gd.hslot != kUncached) {
         gp->hslot = gd.hslot;
         gp->nslot = gd.nslot;
       }
     }
     gslot = gd.hslot;
     off_start = gd.pos != pos0;
+    if (off_start) atomicOr(reinterpret_cast<unsigned int*>(&L.meta[5]), gslot == kUncached ? 1u : 2u);
     E = guard_emit(gd);
   }
-  publish_emitters(L, E, n_em);
+  publish_emitters(L, E, n_slot);
   HEIST_STEP_STAMP(2);
   // 3. visibility (environment.py:257-258); an already-done env recomputes the same plane
-  raycast_pass<NT, U, D>(p, e, smem, L, n_em, n_cams);
+  raycast_pass<NT, U, D>(p, e, smem, L, n_slot, mc);
+  if (p.probe_mode == 7) return;  // profiling: everything up to the raycast
   HEIST_STEP_STAMP(3);
 
+  double reward = 0.0;
+  int status = kAlreadyDone;
+  if (act) {
+    // 1. move (environment.py:239-246): only reward and observation depend on it
+    const int a = (a_raw < 0 || a_raw > 4) ? 0 : a_raw;
+    // environment.py:52-58: 0 stay, 1 up, 2 down, 3 left, 4 right
+    const int nr = s.pos_r + (a == 1 ? -1 : (a == 2 ? 1 : 0)), nc = s.pos_c + (a == 3 ? -1 : (a == 4 ? 1 : 0));
+    if (nr >= 0 && nr < p.R && nc >= 0 && nc < p.C && L.grid[nr * p.C + nc] != kWall) {
+      s.pos_r = nr;
+      s.pos_c = nc;
+    }
+  }
   if (act) {
     // 4-5. shaping, detection, vault, timeout (environment.py:235, :261-297)
     reward = p.r_step;
@@ -938,54 +980,47 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   }
   const int done_now = s.done;
   HEIST_STEP_STAMP(4);
+  const uint8_t* cones_plane = L.gvis;
   if (auto_reset && done_now) {  // block-uniform: the barriers inside are safe
     // The reset keeps every heading (environment.py:204-208) and moves only the guards
-    // back to patrol point 0, so its visibility is this tick's unless a guard stands
-    // elsewhere.  The barrier also orders every wave's detection read before a clear.
-    // Camera visibility stays as it is; a guard back at its patrol start changes only the
-    // cached-cone plane (re-stamped) unless a live-raycast guard moved (full raycast).
-    const bool is_guard = t >= n_cams && t < n_em;
-    const int live_moved = __syncthreads_or(off_start && gslot == kUncached);
-    const int cone_moved = __syncthreads_or(off_start && gslot != kUncached);
-    const int any_moved = live_moved | cone_moved;
+    // back to patrol point 0, so the camera visibility stays and so does a guard's that
+    // stands at its start already.  Cached guards: their reset cones were staged with this
+    // tick's and go to the reset plane (no barrier, no load); a live-raycast guard off its
+    // start forces a full second raycast (rare: guards that do not fit the cone cache).
+    const int moved = L.meta[5];  // set by the guard lanes before the raycast barrier
     reset_solver(p, s);
-    if (is_guard) {
-      const int g = t - n_cams;
+    if (live_guard) {
+      const int g = t - mc;
       Guard* gp = p.guards + (size_t)e * p.max_guards + g;
       gp->idx = 0;
       gp->pos = pos0;
-      if (gslot != kUncached) {  // cone of (patrol point 0, this tick's heading slot)
-        const uint16_t* ce = p.cones + cone_entry(p, e, g, 0, gslot);
-        gp->nslot = (uint8_t)ce[15];  // row 15
-        if (any_moved) {  // the first raycast pass is over (barrier above)
-          const uint4* src = reinterpret_cast<const uint4*>(ce);
-          uint4* dst = reinterpret_cast<uint4*>(L.cone + 16 * g);
-          dst[0] = src[0];
-          dst[1] = src[1];
-          L.em[t].row = unpack_r(pos0);
-          L.em[t].col = unpack_c(pos0);
-        }
-      }
+      if (gslot != kUncached) gp->nslot = (uint8_t)L.cone[16 * (p.max_guards + g) + 15];  // succ of (0, slot)
     }
-    if (cone_moved && !live_moved) {
-      clear_vis<NT, false, true>(p, L);
-      __syncthreads();  // new cones and poses staged, cone plane cleared
-      stamp_guard_cones<NT>(L, n_cams, n_em);
-      __syncthreads();
-    } else if (live_moved) {
+    if (moved & 1) {
+      __syncthreads();  // every wave's detection read is done
       Emit E2;
-      if (t < n_em) E2 = L.em[t];  // this tick's headings, fov and range stay
-      if (is_guard) {
+      if (t < n_slot) E2 = L.em[t];  // this tick's headings, fov and range stay
+      if (live_guard) {
         E2.row = unpack_r(pos0);
         E2.col = unpack_c(pos0);
+        if (gslot != kUncached) {
+          uint4* dst = reinterpret_cast<uint4*>(L.cone + 16 * (t - mc));
+          const uint4* srcr = reinterpret_cast<const uint4*>(L.cone + 16 * (p.max_guards + t - mc));
+          dst[0] = srcr[0];
+          dst[1] = srcr[1];
+        }
       }
-      publish_emitters(L, E2, n_em);
+      publish_emitters(L, E2, n_slot);
       clear_vis<NT>(p, L);
-      raycast_pass<NT, U, D>(p, e, smem, L, n_em, n_cams);
+      raycast_pass<NT, U, D>(p, e, smem, L, n_slot, mc);
+    } else if (moved & 2) {
+      stamp_guard_cones<NT, true>(L, mc, n_slot);
+      cones_plane = L.gvis_r;
+      __syncthreads();
     }
   }
   HEIST_STEP_STAMP(5);
-  if (p.probe_mode < 4) write_obs<NT>(p, e, s, L, obs);
+  if (p.probe_mode < 4) write_obs<NT>(p, e, s, L, cones_plane, obs);
   HEIST_STEP_STAMP(6);
   if (t == 0) {
     rew[e] = (float)reward;
@@ -1005,33 +1040,34 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   const int e = p.order[blockIdx.x];
   const int t = threadIdx.x;
   if (mask && !mask[e]) return;
-  const EnvLds L = carve<D>(smem, p.R, p.C, p.max_cams + p.max_guards, p.max_guards * p.max_path, W);
-  EnvScalars s = p.scal[e];
-  const int n_cams = s.n_cams, n_em = s.n_cams + s.n_guards;
+  const EnvLds L = carve<D>(smem, p.R, p.C, p.max_cams + p.max_guards, 0, W, p.max_guards);
   EmitterRaw raw;
-  prefetch<NT>(p, e, L, n_cams, n_em, raw);
+  prefetch<NT>(p, e, L, raw);
+  EnvScalars s = p.scal[e];
+  const int mc = p.max_cams, n_slot = p.max_cams + p.max_guards;
   clear_vis<NT>(p, L);
   __syncthreads();  // grid, stop map in LDS
   reset_solver(p, s);
   Emit E;
-  if (t < n_cams) {
+  E.kind = -1;
+  if (t < s.n_cams) {
     E = cam_emit(as_cam(raw));
-  } else if (t < n_em) {
+  } else if (t >= mc && t - mc < s.n_guards) {
     Guard gd = as_guard(raw);
     gd.idx = 0;
     gd.pos = gd.pos0;
-    Guard* gp = p.guards + (size_t)e * p.max_guards + (t - n_cams);
+    Guard* gp = p.guards + (size_t)e * p.max_guards + (t - mc);
     gp->idx = 0;
     gp->pos = gd.pos0;
     if (gd.hslot != kUncached) {  // heading kept (environment.py:204-208): cone of (0, hslot)
-      stage_guard_cone(p, e, L, t - n_cams, gd, false);
-      gp->nslot = (uint8_t)L.cone[16 * (t - n_cams) + 15];
+      stage_guard_cone(p, e, L, t - mc, gd, false);
+      gp->nslot = (uint8_t)L.cone[16 * (t - mc) + 15];
     }
     E = guard_emit(gd);
   }
-  publish_emitters(L, E, n_em);
-  raycast_pass<NT, U, D>(p, e, smem, L, n_em, n_cams);
-  write_obs<NT>(p, e, s, L, obs);
+  publish_emitters(L, E, n_slot);
+  raycast_pass<NT, U, D>(p, e, smem, L, n_slot, mc);
+  write_obs<NT>(p, e, s, L, L.gvis, obs);
   if (t == 0) p.scal[e] = s;
 }
 

@@ -2,7 +2,7 @@
 with HEIST_PROBE_MODE = 0 (normal), 1 (no rays), 2 (ray angles + sin/cos only),
 3 (marching with a fixed direction, no sin/cos), 4 (no observation write), 5 (neither
 rays nor observation write), 6 (return at entry: launch + dispatch floor), 7 (return after
-the prefetch).  Modes 1-7 give wrong results on
+the raycast).  Modes 1-7 give wrong results on
 purpose; they only bound the cost of each part.  One JSON line per mode."""
 import json
 import os

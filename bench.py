@@ -184,17 +184,22 @@ def measure_env_config(dev, R, n, budget, steps=100, warmup=10, **kw):
                          "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_env_step": b}}
 
 
-SOLVER_BACKBONE_FLOP = 2 * 400 * (32 * 27 + 64 * 288 + 64 * 576)  # conv1..3 MACs x 2 at 20x20, per env
+def solver_backbone_flop(R):  # conv1..3 MACs x 2 per env at R x R (algorithmic, no band halo)
+    return 2 * R * R * (32 * 27 + 64 * 288 + 64 * 576)
+
+
+SOLVER_BACKBONE_FLOP = solver_backbone_flop(20)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
 
 
-def measure_policy(dev, n, iters=50, warmup=5):
+def measure_policy(dev, n, iters=50, warmup=5, R=20):
     """Batched Solver select_action on the fused kernels (heist_solver_features +
-    heist_solver_head) and the backbone kernel alone, timed with HIP events."""
+    heist_solver_head) and the backbone kernel alone, timed with HIP events.  R = 32 runs
+    the row-band backbone (BASELINE C5's grid)."""
     from heist_amd.agents import SolverAgent
-    ag = SolverAgent(20, 20, device=dev)
+    ag = SolverAgent(R, R, device=dev, rollout_precision="bf16")
     net = ag.network
-    obs = torch.rand(n, 3, 20, 20, device=dev)
+    obs = torch.rand(n, 3, R, R, device=dev)
     h = c = torch.zeros(1, n, 128, device=dev)
     st = torch.cuda.current_stream(dev)
 
@@ -210,14 +215,15 @@ def measure_policy(dev, n, iters=50, warmup=5):
         return a.elapsed_time(b) / iters
     ms_bb = timed(lambda: net.features_fused(obs))
     ms_act = timed(lambda: ag.act(obs, (h, c)))
-    tf = SOLVER_BACKBONE_FLOP * n / (ms_bb * 1e-3) / 1e12
-    return {"value": n / (ms_act * 1e-3), "unit": "env-steps/s", "ms_per_step": ms_act,
-            "dtype": "bf16 MFMA (fp32 accumulate)",
+    tf = solver_backbone_flop(R) * n / (ms_bb * 1e-3) / 1e12
+    kern = "heist::solver_conv_kernel<20,20>" if R == 20 else "heist::solver_conv_band_kernel<32,8>"
+    return {"value": n / (ms_act * 1e-3), "unit": "env-steps/s", "ms_per_step": ms_act, "envs": n,
+            "grid": "%dx%d" % (R, R), "dtype": "bf16 MFMA (fp32 accumulate)",
             "note": "batched SolverAgent.act: fused conv backbone + fc/LSTM/heads/sample kernels",
-            "backbone_roofline": {"bound": "mfma", "kernel": "heist::solver_conv_kernel<20,20>",
+            "backbone_roofline": {"bound": "mfma", "kernel": kern,
                                   "kernel_ms": ms_bb, "achieved": tf, "peak": MFMA_BF16_PEAK_TFLOPS,
                                   "unit": "TFLOP/s", "frac": tf / MFMA_BF16_PEAK_TFLOPS,
-                                  "flop_per_env": SOLVER_BACKBONE_FLOP}}
+                                  "flop_per_env": solver_backbone_flop(R)}}
 
 
 def measure_train(cfg, dev, n_envs, rollout_len=32, minibatch=16384, update_precision="fp32",
@@ -409,6 +415,7 @@ def main():
             sec["rollout_fp32"] = measure_rollout(env, dev, steps=10, precision="fp32")
             log("policy inference")
             sec["policy_inference"] = measure_policy(dev, N)
+            sec["policy_inference_c5_32x32"] = measure_policy(dev, 2048, R=32)
             log("full train (fp32 rollout + fp32 update: the parity mode)")
             sec["full_train_fp32"] = measure_train(cfg, dev, N)
             log("full train (bf16 rollout + bf16 update)")

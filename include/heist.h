@@ -202,7 +202,7 @@ int heist_ppo_loss(const float* logits, const float* values, const int64_t* acti
  * and .bias [co] (3->32->64->64) into the kernel's fragment layout in `packed`
  * (heist_solver_packed_bytes() bytes, 16-byte aligned); call it after every weight update.
  * heist_solver_features: obs [n][3][rows][cols] float32 -> feat_out [n][1024] float32
- * (channel-major 64 x 4 x 4, the x.view(batch, -1) order).  rows x cols in {20x20, 10x10};
+ * (channel-major 64 x 4 x 4, the x.view(batch, -1) order).  rows x cols in {20x20, 10x10, 32x32};
  * other sizes return HEIST_EINVAL (callers use the PyTorch path). */
 int heist_solver_packed_bytes(void);
 int heist_solver_pack(const float* conv1_w, const float* conv1_b, const float* conv2_w, const float* conv2_b,

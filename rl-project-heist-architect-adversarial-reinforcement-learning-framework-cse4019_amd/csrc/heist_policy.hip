@@ -178,9 +178,8 @@ __device__ __forceinline__ void conv2_pass(unsigned char* smem, const bf16x8* wl
   }
 }
 
-template <int R, int C>
-__device__ __forceinline__ void load_obs(const float* __restrict__ obs, int e, float (&v)[ConvGeom<R, C>::QI][3]) {
-  using G = ConvGeom<R, C>;
+template <class G>  // G: ConvGeom or BandGeom
+__device__ __forceinline__ void load_obs(const float* __restrict__ obs, int e, float (&v)[G::QI][3]) {
   const float* o = obs + (size_t)e * 3 * G::RC;
 #pragma unroll
   for (int i = 0; i < G::QI; ++i) {
@@ -193,9 +192,9 @@ __device__ __forceinline__ void load_obs(const float* __restrict__ obs, int e, f
   }
 }
 
-template <int R, int C>
-__device__ __forceinline__ void stage_obs(unsigned char* smem, const float (&v)[ConvGeom<R, C>::QI][3]) {
-  using G = ConvGeom<R, C>;
+template <class G>
+__device__ __forceinline__ void stage_obs(unsigned char* smem, const float (&v)[G::QI][3]) {
+  constexpr int C = G::PC - 2;
 #pragma unroll
   for (int i = 0; i < G::QI; ++i) {
     const int q = threadIdx.x + 256 * i;
@@ -307,7 +306,7 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
 
   float pre[G::QI][3];
   int e = blockIdx.x;
-  if (e < n) load_obs<R, C>(obs, e, pre);
+  if (e < n) load_obs<G>(obs, e, pre);
   __builtin_amdgcn_s_waitcnt(0);  // weights landed: no conservative vmcnt waits inside the loop
   __syncthreads();
 
@@ -325,7 +324,7 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
     }
   };
   if (e < n) {
-    stage_obs<R, C>(smem, pre);
+    stage_obs<G>(smem, pre);
     __syncthreads();
     bf16x8 f1[NT1][kW1Steps];
 #pragma unroll
@@ -344,7 +343,7 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
     HEIST_STAMP(0);
     const int en = e + gridDim.x;
     const bool has_next = en < n;  // workgroup-uniform
-    if (has_next) load_obs<R, C>(obs, en, pre);  // next env's observation in flight during conv2
+    if (has_next) load_obs<G>(obs, en, pre);  // next env's observation in flight during conv2
     HEIST_STAMP(1);
     HEIST_STAMP(2);
     HEIST_STAMP(3);
@@ -368,7 +367,7 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
       conv2_pass<R, C, NT2, NT2, SB, NT2, NC, NC>(smem, wl, b2v, mh, nh, lr, h, l, accC, accC);  // last epilogue
     }
     HEIST_STAMP(5);
-    if (has_next) stage_obs<R, C>(smem, pre);  // in0 is free: this env's conv1 ran an iteration ago
+    if (has_next) stage_obs<G>(smem, pre);  // in0 is free: this env's conv1 ran an iteration ago
     __syncthreads();  // B3: act2 of env e and the input plane of env en ready; act1 reads done
     HEIST_STAMP(6);
 
@@ -464,6 +463,308 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
   }
 }
 
+// ===========================================================================
+// 32-column grids (BASELINE C5: 32 x 32) in row bands.
+//
+// One 32 x 32 env's padded act2 plane alone (34 rows x 34 x 144 B = 166 KB) exceeds the
+// CU's 160 KiB LDS, so the env is processed in NB = R / BR bands of BR conv3 output rows.
+// Band b (image rows y0 = b BR .. y0 + BR - 1) needs act2 rows y0 - 1 .. y0 + BR (conv2,
+// BR + 2 rows) and act1 rows y0 - 2 .. y0 + BR + 1 (conv1, BR + 4 rows); the halo rows are
+// recomputed per band (conv1 +50 %, conv2 +25 %, conv3 and the pool exact: 12 % more MFMA
+// work in all at BR = 8) and rows outside the image are stored as zeros (the convs' zero
+// padding).  With C = 32 an MFMA position tile is exactly one row, so every tile is
+// wholly inside or outside the image (a wave-uniform predicate) and the tap offsets are
+// plain row / column strides.  The input plane holds the whole env (34 x 34 x 8 B); the
+// act planes are band-local.  Per band: conv2 (three k-outer passes as in the full-plane
+// kernel) -> B3 -> conv3 + pool, then the NEXT band's conv1 (or the next env's band 0)
+// -> B4.  The pooled sums accumulate in registers across the env's bands.
+// ===========================================================================
+
+template <int R, int BR>
+struct BandGeom {
+  static constexpr int C = 32, PC = C + 2, NB = R / BR, RC = R * C;
+  static constexpr int S0 = 8, S1 = 80, S2 = 144;  // bytes per padded position (as ConvGeom)
+  static constexpr int T1 = BR + 4, T2 = BR + 2, T3 = BR;  // tiles (= rows) of conv1 / conv2 / conv3 per band
+  static constexpr int PB0 = PC * S0, PB1 = PC * S1, PB2 = PC * S2;
+  // 16 consecutive positions of one row are 80 B (5 bank groups) or 144 B (9 groups)
+  // apart: 16 distinct 16-byte bank groups in every ds_read_b128 (5, 9 odd)
+  static constexpr int IN = 0;
+  static constexpr int A1 = align16c(IN + (R + 2) * PB0);
+  static constexpr int A2 = align16c(A1 + T1 * PB1);
+  static constexpr int ZERO_END = align16c(A2 + T2 * PB2);  // zeroed once (column pads, input border)
+  static constexpr int POOL = ZERO_END;                    // [64][16] f32
+  static constexpr int BIAS = POOL + 64 * 16 * 4;          // b1[32] b2[64] b3[64]
+  static constexpr int INVA = BIAS + 160 * 4;              // [16] f32 1/area
+  static constexpr int PM = INVA + 16 * 4;                 // [R][2][64] pool-membership bytes by image row
+  static constexpr int W2 = align16c(PM + R * 128);        // conv2 fragments [2][18][64] x 16 B
+  static constexpr int LDS = W2 + 2 * 18 * 64 * 16;
+  static constexpr int QI = (RC + 255) / 256;
+  static_assert(R % BR == 0 && T1 % 4 == 0 && T2 % 2 == 0 && T3 % 2 == 0, "band tiles split evenly over waves");
+  static_assert(LDS <= 160 * 1024, "input plane + band planes + conv2 fragments must fit 160 KiB LDS");
+};
+
+// One k-outer pass of a band's conv2 over the wave's tiles [T0, T1) (tile i = band row
+// mh + 2 i, image row y0 - 1 + that), hiding the previous pass's epilogue [P0, P1) under
+// its MFMAs (see conv2_pass); a tile whose image row is outside the grid stores zeros.
+template <int R, int BR, int T0, int T1, int P0, int P1, int NA, int NP>
+__device__ __forceinline__ void conv2_band_pass(unsigned char* smem, const bf16x8* wl, const float4 (&b2v)[4], int mh,
+                                                int nh, int lr, int h, int y0, f32x16 (&cur)[NA],
+                                                const f32x16 (&prv)[NP]) {
+  using G = BandGeom<R, BR>;
+  constexpr int NTP = T1 - T0, NQ = kW2Steps * NTP, kPre2 = 6;
+  constexpr int NPIECE = (P1 - P0) * 16;
+  constexpr int PER_Q = NQ > 0 ? (NPIECE + NQ - 1) / (NQ > 0 ? NQ : 1) : NPIECE;
+  bf16x4 o;
+  auto piece = [&](int k) {
+    const int ti = k >> 4, kk = k & 15, g = kk >> 2, jj = kk & 3;
+    const int row = mh + 2 * (P0 + ti);
+    const bool valid = (unsigned)(y0 - 1 + row) < (unsigned)R;
+    const float bv = jj == 0 ? b2v[g].x : (jj == 1 ? b2v[g].y : (jj == 2 ? b2v[g].z : b2v[g].w));
+    o[jj] = (__bf16)(valid ? relu(prv[ti][kk] + bv) : 0.f);
+    if (jj == 3)
+      *reinterpret_cast<bf16x4*>(smem + G::A2 + row * G::PB2 + (lr + 1) * G::S2 + (32 * nh + 8 * g + 4 * h) * 2) = o;
+  };
+  if constexpr (NQ > 0) {
+    const unsigned char* base[NTP];
+#pragma unroll
+    for (int i = 0; i < NTP; ++i) {
+      base[i] = smem + G::A1 + (mh + 2 * (T0 + i)) * G::PB1 + lr * G::S1 + 16 * h;
+      cur[i] = f32x16{};
+    }
+    auto rd = [&](int q) {
+      const int s = q / NTP, tap = s >> 1;
+      return *reinterpret_cast<const bf16x8*>(base[q % NTP] + (tap / 3) * G::PB1 + (tap % 3) * G::S1 + (s & 1) * 32);
+    };
+    bf16x8 ring[kPre2];
+#pragma unroll
+    for (int q = 0; q < kPre2; ++q) ring[q] = rd(q < NQ ? q : NQ - 1);
+    bf16x8 wcur = wl[0], wnext = wcur;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int s = q / NTP, i = q % NTP;
+      if (i == 0 && s + 1 < kW2Steps) wnext = wl[(s + 1) * 64];
+      const bf16x8 f = ring[q % kPre2];
+      if (q + kPre2 < NQ) ring[q % kPre2] = rd(q + kPre2);
+      cur[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wcur, f, cur[i], 0, 0, 0);
+      if (i == NTP - 1) wcur = wnext;
+#pragma unroll
+      for (int r = 0; r < PER_Q; ++r)
+        if (q * PER_Q + r < NPIECE) piece(q * PER_Q + r);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, kPre2 + 1, 0);
+    sched_ring<NTP, 1>(std::make_integer_sequence<int, NQ>{});
+  } else {
+#pragma unroll
+    for (int k = 0; k < NPIECE; ++k) piece(k);
+  }
+}
+
+template <int R, int BR>
+__global__ __launch_bounds__(256, 1) void solver_conv_band_kernel(const float* __restrict__ obs, int n,
+                                                                  const uint4* __restrict__ packed,
+                                                                  float* __restrict__ feat) {
+  using G = BandGeom<R, BR>;
+  constexpr int C = G::C, PC = G::PC;
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63, h = l >> 5, lr = l & 31;
+  const int nh = w & 1, mh = w >> 1;
+
+  // ---- weights -> registers / LDS, tables -> LDS (as solver_conv_kernel)
+  bf16x8 w1[kW1Steps], w3[kW3Steps];
+#pragma unroll
+  for (int s = 0; s < kW1Steps; ++s) {
+    w1[s] = __builtin_bit_cast(bf16x8, packed[kOffW1 + s * 64 + l]);
+    in_agpr(w1[s]);
+  }
+#pragma unroll
+  for (int s = 0; s < kW3Steps; ++s) {
+    w3[s] = __builtin_bit_cast(bf16x8, packed[kOffW3 + (nh * kW3Steps + s) * 64 + l]);
+    in_agpr(w3[s]);
+  }
+  for (int i = tid; i < 2 * kW2Steps * 64; i += 256)
+    reinterpret_cast<uint4*>(smem + G::W2)[i] = packed[kOffW2 + i];
+  const float* gbias = reinterpret_cast<const float*>(packed + kOffBias);
+  float* bias = reinterpret_cast<float*>(smem + G::BIAS);
+  const float b3v = gbias[96 + 32 * nh + lr];
+  if (tid < 160) bias[tid] = gbias[tid];
+  for (int i = tid; i < G::ZERO_END / 16; i += 256) reinterpret_cast<uint4*>(smem)[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (tid < 16) {
+    const int ci = tid >> 2, cj = tid & 3;
+    const int area = (pool_hi(ci, R) - pool_lo(ci, R)) * (pool_hi(cj, C) - pool_lo(cj, C));
+    reinterpret_cast<float*>(smem + G::INVA)[tid] = 1.0f / (float)area;
+  }
+  for (int i = tid; i < R * 128; i += 256) {  // pool membership of the P fragment bits, by image row
+    const int y = i >> 7, s = (i >> 6) & 1, ll = i & 63;
+    const int cell = ll & 31, hh = ll >> 5;
+    unsigned bits = 0;
+    if (cell < 16) {
+      const int ci = cell >> 2, cj = cell & 3;
+      for (int j = 0; j < 8; ++j) {
+        const int ox = 16 * s + 8 * (j >> 2) + 4 * hh + (j & 3);
+        if (y >= pool_lo(ci, R) && y < pool_hi(ci, R) && ox >= pool_lo(cj, C) && ox < pool_hi(cj, C)) bits |= 1u << j;
+      }
+    }
+    smem[G::PM + i] = (unsigned char)bits;
+  }
+  int off1a[kW1Steps], off1b[kW1Steps];
+#pragma unroll
+  for (int s = 0; s < kW1Steps; ++s) {
+    int ta = 4 * s + 2 * h, tb = ta + 1;
+    ta = ta < 9 ? ta : 4;
+    tb = tb < 9 ? tb : 4;
+    off1a[s] = ((ta / 3) * PC + (ta % 3)) * G::S0;
+    off1b[s] = ((tb / 3) * PC + (tb % 3)) * G::S0;
+  }
+
+  // conv1 of the band starting at image row y0: band tile j = w + 4 i is image row
+  // y0 - 2 + j; rows outside the grid read a clamped row and store zeros
+  constexpr int NT1 = G::T1 / 4;
+  auto conv1_band = [&](int y0) {
+    bf16x8 f1[NT1][kW1Steps];
+#pragma unroll
+    for (int i = 0; i < NT1; ++i) {
+      const int y = y0 - 2 + w + 4 * i;
+      const int yc = y < 0 ? 0 : (y >= R ? R - 1 : y);
+      const unsigned char* base = smem + G::IN + (yc * PC + lr) * G::S0;  // top-left tap (padded row yc)
+#pragma unroll
+      for (int s = 0; s < kW1Steps; ++s) {
+        const uint2 a = *reinterpret_cast<const uint2*>(base + off1a[s]);
+        const uint2 b = *reinterpret_cast<const uint2*>(base + off1b[s]);
+        f1[i][s] = __builtin_bit_cast(bf16x8, make_uint4(a.x, a.y, b.x, b.y));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NT1; ++i) {
+      const int j = w + 4 * i;
+      const bool valid = (unsigned)(y0 - 2 + j) < (unsigned)R;
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < kW1Steps; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(in_agpr(w1[s]), f1[i][s], acc, 0, 0, 0);
+      unsigned char* dst = smem + G::A1 + j * G::PB1 + (lr + 1) * G::S1;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n0 = 8 * g + 4 * h;
+        const float4 b = *reinterpret_cast<const float4*>(bias + n0);
+        bf16x4 o;
+        o[0] = (__bf16)(valid ? relu(acc[4 * g + 0] + b.x) : 0.f);
+        o[1] = (__bf16)(valid ? relu(acc[4 * g + 1] + b.y) : 0.f);
+        o[2] = (__bf16)(valid ? relu(acc[4 * g + 2] + b.z) : 0.f);
+        o[3] = (__bf16)(valid ? relu(acc[4 * g + 3] + b.w) : 0.f);
+        *reinterpret_cast<bf16x4*>(dst + n0 * 2) = o;
+      }
+    }
+  };
+
+  float pre[G::QI][3];
+  int e = blockIdx.x;
+  if (e < n) load_obs<G>(obs, e, pre);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (e < n) {
+    stage_obs<G>(smem, pre);
+    __syncthreads();
+    conv1_band(0);
+  }
+  __syncthreads();  // act1 of the first band ready
+
+  f32x16 Y = {};
+  for (; e < n; e += gridDim.x) {
+    const int en = e + gridDim.x;
+    const bool has_next = en < n;  // workgroup-uniform
+    for (int b = 0; b < G::NB; ++b) {
+      const int y0 = b * BR;
+      const bool last = b == G::NB - 1;
+      if (last && has_next) load_obs<G>(obs, en, pre);  // next env's observation in flight during conv2
+      // ---- conv2 of the band: D[32 ch of nh][band row] in three k-outer passes
+      {
+        constexpr int NT2 = G::T2 / 2;
+        constexpr int SA = (NT2 * 3 + 6) / 7, SB = SA + (NT2 - SA + 1) / 2;
+        constexpr int NA = SA, NB2 = SB - SA > 0 ? SB - SA : 1, NC = NT2 - SB > 0 ? NT2 - SB : 1;
+        const bf16x8* wl = reinterpret_cast<const bf16x8*>(smem + G::W2) + nh * kW2Steps * 64 + l;
+        float4 b2v[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) b2v[g] = *reinterpret_cast<const float4*>(bias + 32 + 32 * nh + 8 * g + 4 * h);
+        f32x16 accA[NA], accB[NB2], accC[NC];
+        conv2_band_pass<R, BR, 0, SA, 0, 0, NA, NA>(smem, wl, b2v, mh, nh, lr, h, y0, accA, accA);
+        conv2_band_pass<R, BR, SA, SB, 0, SA, NB2, NA>(smem, wl, b2v, mh, nh, lr, h, y0, accB, accA);
+        conv2_band_pass<R, BR, SB, NT2, SA, SB, NC, NB2>(smem, wl, b2v, mh, nh, lr, h, y0, accC, accB);
+        conv2_band_pass<R, BR, NT2, NT2, SB, NT2, NC, NC>(smem, wl, b2v, mh, nh, lr, h, y0, accC, accC);
+      }
+      if (last && has_next) stage_obs<G>(smem, pre);  // the input plane's last reader ran a band ago
+      __syncthreads();  // B3: act2 of the band (and the next env's input) ready; act1 reads done
+
+      // ---- conv3 of the band + pooling (as solver_conv_kernel), Y accumulates over bands
+      {
+        constexpr int NT3 = G::T3 / 2, NQ = NT3 * kW3Steps, kPre = 7;
+        const unsigned char* base[NT3];
+#pragma unroll
+        for (int i = 0; i < NT3; ++i) base[i] = smem + G::A2 + (mh + 2 * i) * G::PB2 + lr * G::S2 + 16 * h;
+        auto rd = [&](int q) {
+          const int s = q % kW3Steps, tap = s >> 2;
+          return *reinterpret_cast<const bf16x8*>(base[q / kW3Steps] + (tap / 3) * G::PB2 + (tap % 3) * G::S2 +
+                                                  (s & 3) * 32);
+        };
+        bf16x8 ring[kPre];
+#pragma unroll
+        for (int q = 0; q < kPre; ++q) ring[q] = rd(q);
+        f32x16 prev = {};
+        bf16x8 x[2], pf[2];
+        auto pool_piece = [&](int row, int s) {  // piece s of band row `row`'s epilogue (prev holds its sums)
+          if (s < 16) x[s >> 3][s & 7] = (__bf16)relu(prev[s] + b3v);
+          if (s == 0 || s == 1) {
+            const unsigned bits = smem[G::PM + ((y0 + row) * 2 + s) * 64 + l];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pf[s][j] = ((bits >> j) & 1u) ? (__bf16)1.0f : (__bf16)0.0f;
+          }
+          if (s == 16) Y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf[0], x[0], Y, 0, 0, 0);
+          if (s == 17) Y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf[1], x[1], Y, 0, 0, 0);
+        };
+#pragma unroll
+        for (int i = 0; i < NT3; ++i) {
+          f32x16 acc = {};
+#pragma unroll
+          for (int s = 0; s < kW3Steps; ++s) {
+            const int q = i * kW3Steps + s;
+            const bf16x8 f = ring[q % kPre];
+            if (q + kPre < NQ) ring[q % kPre] = rd(q + kPre);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, in_agpr(w3[s]), acc, 0, 0, 0);
+            if (i > 0 && s < 18) pool_piece(mh + 2 * (i - 1), s);
+          }
+          prev = acc;
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, kPre, 0);
+        sched_ring<kW3Steps, 0>(std::make_integer_sequence<int, NQ>{});
+#pragma unroll
+        for (int s = 0; s < 18; ++s) pool_piece(mh + 2 * (NT3 - 1), s);
+      }
+      // conv1 of the next band (or the next env's first band; after the last env: harmless)
+      conv1_band(last ? 0 : y0 + BR);
+      float* pool = reinterpret_cast<float*>(smem + G::POOL) + (32 * nh + lr) * 16 + 4 * h;
+      if (last && mh == 1) {
+        *reinterpret_cast<float4*>(pool) = make_float4(Y[0], Y[1], Y[2], Y[3]);
+        *reinterpret_cast<float4*>(pool + 8) = make_float4(Y[4], Y[5], Y[6], Y[7]);
+      }
+      __syncthreads();  // B4: act1 of the next band written; partner half of the pool sums in LDS
+      if (last) {
+        if (mh == 0) {
+          const float4 p0 = *reinterpret_cast<const float4*>(pool);
+          const float4 p1 = *reinterpret_cast<const float4*>(pool + 8);
+          const float* inva = reinterpret_cast<const float*>(smem + G::INVA) + 4 * h;
+          const float4 i0 = *reinterpret_cast<const float4*>(inva);
+          const float4 i1 = *reinterpret_cast<const float4*>(inva + 8);
+          float* out = feat + (size_t)e * 1024 + (32 * nh + lr) * 16 + 4 * h;
+          *reinterpret_cast<float4*>(out) =
+              make_float4((Y[0] + p0.x) * i0.x, (Y[1] + p0.y) * i0.y, (Y[2] + p0.z) * i0.z, (Y[3] + p0.w) * i0.w);
+          *reinterpret_cast<float4*>(out + 8) =
+              make_float4((Y[4] + p1.x) * i1.x, (Y[5] + p1.y) * i1.y, (Y[6] + p1.z) * i1.z, (Y[7] + p1.w) * i1.w);
+        }
+        Y = f32x16{};
+      }
+    }
+  }
+}
+
 // Weight packing: fragment element j of lane l, k-step s, output tile nt holds
 // W[co = 32 nt + (l & 31)][k = 16 s + 8 (l >> 5) + j] with k = tap * CinP + ci,
 // tap = 3 ky + kx; zero where ci >= Cin or tap >= 9.  bf16 round-to-nearest-even.
@@ -529,13 +830,34 @@ static hipError_t launch_conv_rc(const float* obs, int n, const void* packed, fl
   return hipGetLastError();
 }
 
-bool solver_conv_supported(int R, int C) { return (R == 20 && C == 20) || (R == 10 && C == 10); }
+// 32 x 32 (BASELINE C5): the row-band kernel, bands of 8 conv3 rows
+constexpr int kBandRows = 8;
+static hipError_t launch_conv_band32(const float* obs, int n, const void* packed, float* feat, int n_cu,
+                                     hipStream_t st) {
+  using G = BandGeom<32, kBandRows>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&solver_conv_band_kernel<32, kBandRows>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int grid = n < n_cu ? n : n_cu;
+  hipLaunchKernelGGL((solver_conv_band_kernel<32, kBandRows>), dim3(grid), dim3(256), G::LDS, st, obs, n,
+                     reinterpret_cast<const uint4*>(packed), feat);
+  return hipGetLastError();
+}
+
+bool solver_conv_supported(int R, int C) {
+  return (R == 20 && C == 20) || (R == 10 && C == 10) || (R == 32 && C == 32);
+}
 
 hipError_t launch_solver_conv(const float* obs, int n, int R, int C, const void* packed, float* feat, int n_cu,
                               hipStream_t st) {
   if (n <= 0) return hipSuccess;
   if (R == 20 && C == 20) return launch_conv_rc<20, 20>(obs, n, packed, feat, n_cu, st);
   if (R == 10 && C == 10) return launch_conv_rc<10, 10>(obs, n, packed, feat, n_cu, st);
+  if (R == 32 && C == 32) return launch_conv_band32(obs, n, packed, feat, n_cu, st);
   return hipErrorInvalidValue;
 }
 

@@ -74,8 +74,8 @@ class SolverNetwork(nn.Module):  # networks.py:13-131
 
     # -- fused backbone (heist_solver_features, bf16 MFMA) -----------------------------
     def fused_supported(self, state: torch.Tensor) -> bool:
-        """The HIP backbone covers 20x20 and 10x10 grids on a HIP device."""
-        return state.is_cuda and state.dim() == 4 and tuple(state.shape[1:]) in ((3, 20, 20), (3, 10, 10))
+        """The HIP backbone covers 20x20, 10x10 and (row bands) 32x32 grids on a HIP device."""
+        return state.is_cuda and state.dim() == 4 and tuple(state.shape[1:]) in ((3, 20, 20), (3, 10, 10), (3, 32, 32))
 
     def _packed_backbone(self) -> torch.Tensor:
         """conv1-3 weights in the kernel's MFMA fragment layout, re-packed (one small launch)
@@ -100,7 +100,7 @@ class SolverNetwork(nn.Module):  # networks.py:13-131
         bf16 operands, fp32 accumulation; inference only (no autograd)."""
         from . import _native
         if not self.fused_supported(state):
-            raise _native.HeistError("fused Solver backbone needs [B,3,20,20] or [B,3,10,10] on a HIP device")
+            raise _native.HeistError("fused Solver backbone needs [B,3,R,R], R in (10, 20, 32), on a HIP device")
         x = state.detach().float().contiguous()
         packed = self._packed_backbone()
         out = torch.empty(x.shape[0], 1024, dtype=torch.float32, device=x.device)

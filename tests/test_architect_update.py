@@ -6,7 +6,8 @@ losses out, and per parameter tensor the post-update (clipped) gradient and the
 parameter change as norms + fixed random projections.  Tolerance 1e-4 (north star) on
 the losses; the gradient / step summaries to 1e-4 relative (fp32 conv backward on a
 different device and library); parameters whose gradient is cancellation noise (below
-1e-6 of the largest) get only Adam's lr bound on their step.  kat.json's architect_reward table pins
+1e-6 of the largest), and every parameter of a case whose value loss is itself rounding
+noise, get only Adam's lr bound on their step.  kat.json's architect_reward table pins
 calculate_architect_reward (rewards.py:43-73).
 """
 import numpy as np
@@ -40,11 +41,19 @@ def _check_cases(device):
             got = [m["architect_policy_loss"], m["architect_value_loss"], m["architect_total_loss"]]
             np.testing.assert_allclose(got, z[key + "loss"], rtol=1e-4, atol=1e-4, err_msg=key)
             gmax = float(np.max(z[key + "gnorm"]))
+            # a case whose value loss is rounding noise (normalised rewards average to 0 and
+            # the value head already sits at that target): every gradient is fp32
+            # cancellation noise, which Adam (|g| ~ eps) turns into device-dependent steps
+            noise_case = float(z[key + "loss"][1]) < 1e-12
             for i, (p, q) in enumerate(zip(ag.network.parameters(), p0)):
                 g = (p.grad if p.grad is not None else torch.zeros_like(p)).detach().double().reshape(-1).cpu().numpy()
                 d = (p.detach() - q).double().reshape(-1).cpu().numpy()
                 P = proj_vectors(i, g.size)
                 gscale = max(float(z[key + "gnorm"][i]), 1e-12)
+                if noise_case:  # gradients scale with a rounding-noise residual: bounded, not compared
+                    assert np.linalg.norm(g) < 1e-6, (key, i)
+                    assert np.abs(d).max() <= ag.optimizer.param_groups[0]["lr"] * 3.17, (key, i)
+                    continue
                 np.testing.assert_allclose(np.linalg.norm(g), z[key + "gnorm"][i], rtol=1e-4, atol=1e-9,
                                            err_msg="%s grad norm %d" % (key, i))
                 np.testing.assert_allclose(P @ g, z[key + "gproj"][i], rtol=0, atol=4e-4 * gscale + 1e-9,

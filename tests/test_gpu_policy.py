@@ -69,7 +69,7 @@ def _rel(a, b):
     return d.max().item() / m, d.mean().item() / m
 
 
-@pytest.mark.parametrize("R,n", [(20, 64), (20, 1), (20, 300), (10, 77)])
+@pytest.mark.parametrize("R,n", [(20, 64), (20, 1), (20, 300), (10, 77), (32, 64), (32, 1), (32, 300)])
 def test_features_match_emulation(gpu_device, R, n):
     torch.manual_seed(R * 1000 + n)
     net = SolverNetwork(R, R).to(gpu_device)
@@ -105,6 +105,25 @@ def test_features_close_to_fp32_full_batch(gpu_device):
     # against the emulation too)
     rows = torch.tensor([0, 1, 255, 256, 257, 1023, 2048, 4095], device=gpu_device)
     mx, mean = _rel(got[rows], emulate_backbone(net, obs[rows]))
+    assert mx < TOL_EMU_MAX and mean < TOL_EMU_MEAN, (mx, mean)
+
+
+def test_features_32x32_full_batch(gpu_device):
+    """BASELINE C5's 2048 envs of 32x32 (row-band kernel: 4 bands of 8 rows per env) against
+    the fp32 torch path, and a spread of rows against the emulation; random inputs too."""
+    torch.manual_seed(13)
+    net = SolverNetwork(32, 32).to(gpu_device)
+    for conv in (net.conv1, net.conv2, net.conv3):
+        torch.nn.init.uniform_(conv.bias, -0.3, 0.3)
+    obs = env_obs(2048, 32, gpu_device, seed=21, steps=3)
+    got = net.features_fused(obs)
+    mx, _ = _rel(got, torch_backbone(net, obs))
+    assert mx < TOL_F32_MAX, mx
+    rows = torch.tensor([0, 1, 255, 256, 257, 1023, 1024, 2047], device=gpu_device)
+    mx, mean = _rel(got[rows], emulate_backbone(net, obs[rows]))
+    assert mx < TOL_EMU_MAX and mean < TOL_EMU_MEAN, (mx, mean)
+    x = torch.randn(40, 3, 32, 32, device=gpu_device)
+    mx, mean = _rel(net.features_fused(x), emulate_backbone(net, x))
     assert mx < TOL_EMU_MAX and mean < TOL_EMU_MEAN, (mx, mean)
 
 
@@ -151,10 +170,10 @@ def test_agent_act_uses_fused_path_and_fallback(gpu_device):
     a, lp, v, (h, c) = ag.act(obs)
     assert a.shape == (32,) and ((a >= 0) & (a < 5)).all() and torch.isfinite(lp).all()
     assert hasattr(ag.network, "_pack_cache")
-    ag32 = SolverAgent(32, 32, device=gpu_device, rollout_precision="bf16")
-    o32 = torch.rand(4, 3, 32, 32, device=gpu_device)
-    a32, lp32, _, _ = ag32.act(o32)
-    assert not hasattr(ag32.network, "_pack_cache") and a32.shape == (4,)
+    ag16 = SolverAgent(16, 16, device=gpu_device, rollout_precision="bf16")
+    o16 = torch.rand(4, 3, 16, 16, device=gpu_device)
+    a16, lp16, _, _ = ag16.act(o16)
+    assert not hasattr(ag16.network, "_pack_cache") and a16.shape == (4,)
     # same logits both ways up to bf16 precision -> log-probs of the taken actions agree
     a_ref, lp_ref, _, _ = ag.act(obs, fused=False)
     logits_f, _, _ = ag.network.forward_fused(obs)

@@ -55,6 +55,7 @@ struct EnvLds {
                    // rays and live-raycast guards
   uint8_t* gvis;   // LDS offset 2D: the cached guard cones (same geometry); visibility = vis | gvis
   uint8_t* gvis_r; // LDS offset 3D: the cached guard cones after an in-step auto-reset (guards at patrol point 0)
+                   // LDS offset 4D: sink plane, where march_fast sends the stores of stopped samples
   uint8_t* grid;   // [RC]
   Emit* em;        // [n_emit]
   uint16_t* path;  // [max_guards][max_path]
@@ -82,7 +83,7 @@ __host__ __device__ inline int padded_bytes(int R, int C) { return (R + 2 * kRin
 __host__ __device__ inline size_t env_lds_bytes(int R, int C, int n_emit, int path_words, int D, int waves,
                                                 int cone_guards = 0) {
   const int RC = R * C;
-  return 4 * (size_t)D + align16(RC) + align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) +
+  return 5 * (size_t)D + align16(RC) + align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) +
          align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1)) +
          sizeof(int) * 64 * (size_t)waves + 32 + 68 * (size_t)cone_guards;
 }
@@ -96,7 +97,7 @@ __device__ __forceinline__ EnvLds carve(unsigned char* smem, int R, int C, int n
   L.vis = smem + D;
   L.gvis = smem + 2 * (size_t)D;
   L.gvis_r = smem + 3 * (size_t)D;
-  size_t o = 4 * (size_t)D;
+  size_t o = 5 * (size_t)D;  // [4D, 5D): the fast path's sink for masked stores (never read)
   L.grid = smem + o; o += align16(RC);
   L.em = reinterpret_cast<Emit*>(smem + o); o += align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1));
   L.path = reinterpret_cast<uint16_t*>(smem + o); o += align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1));
@@ -302,29 +303,41 @@ __device__ __forceinline__ void lds_st(uint32_t a, uint8_t v) {
   *reinterpret_cast<__attribute__((address_space(3))) uint8_t*>(a) = v;
 }
 
-// Every sample k = 1 .. n_samp of a fast ray in one LDS round trip.  (dxs, dys) = (dx, dy)
-// * stride, (mx, my) = kMagic32 + the padded (col, row) of the emitter; kofs turns the two
-// rounded bit patterns into the absolute LDS address of the stop byte.  The ring is as
-// wide as the longest fast ray (kRing >= kTieMaxRange), so each sample address lies inside
-// the padded stop map whether or not the ray has already stopped: all NS wall reads are
-// issued before any is used, and a running stop flag masks the visibility stores (a masked
-// store goes to a ring byte of the vis plane that nobody reads).  NS = n_samp, or with
-// CLAMP NS >= n_samp and the samples past n_samp repeat sample n_samp (k clamped), which
-// changes nothing.  Only the first two samples can land on the emitter's own tile (see
-// cast_rays).  Returns the ray's sample count up to and including the sample that ends it
-// (n_samp if none does), when COUNT.  Scalar fp32 on purpose (and this file builds with
-// -fno-slp-vectorize): ROCm 7.2 clang miscompiles the float2 / v_pk_fma_f32 form of this
-// loop (a lane's negation is lost).
+// 32-bit OR as one v_or_b32: the compiler otherwise narrows the OR of byte loads to a
+// 16-bit op and re-extends it with a v_and before every mad_u24 that consumes it.
+__device__ __forceinline__ uint32_t or_b32(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_or_b32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// Every sample k = 1 .. n_samp of a fast ray in one LDS round trip.  Coordinates are
+// computed in units of the smallest fp32 denormal (2^-149; fp32 denormals are preserved):
+// k and the padded emitter (col, row) -- the LDS base folded into the column -- enter as
+// denormals whose bit patterns are those integers, so fl32(k * dxs + mx) =
+// 2^-149 * rint_even(col' + k * dx * stride), one rounding of the exact product-sum (the
+// same rint as fp64's), and its bit pattern IS that integer: one mad_u24 (row * PC + col)
+// gives the LDS address of the stop byte.  The ring is as wide as the longest fast ray
+// (kRing >= kTieMaxRange), so each sample address lies inside the padded stop map whether
+// or not the ray has already stopped: all NS wall reads are issued before any is used, and
+// a running stop flag sends the visibility store of a stopped sample (and of the emitter's
+// own tile) to the sink plane (address + 3D, i.e. 4D .. 5D, never read) with one more
+// mad_u24 instead of a compare and select.  NS = n_samp, or with CLAMP NS >= n_samp and the
+// samples past n_samp repeat sample n_samp (k clamped), which changes nothing.  Only the
+// first two samples can land on the emitter's own tile (see cast_rays).  Returns the ray's
+// sample count up to and including the sample that ends it (n_samp if none does), when
+// COUNT.  Scalar fp32 on purpose (and this file builds with -fno-slp-vectorize): ROCm 7.2
+// clang miscompiles the float2 / v_pk_fma_f32 form of this loop (a lane's negation is lost).
 template <int D, int NS, bool CLAMP, bool COUNT>
-__device__ __forceinline__ int march_fast(uint32_t PC, uint32_t own, uint32_t dummy, float dxs, float dys, float mx,
-                                          float my, uint32_t kofs, int n_samp) {
+__device__ __forceinline__ int march_fast(uint32_t PC, uint32_t own, float dxs, float dys, float mx, float my,
+                                          int n_samp) {
   uint32_t a[NS], w[NS];
-  const float kmax = (float)n_samp;
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
-    const float k = (CLAMP && u > 0) ? __builtin_fminf((float)(u + 1), kmax) : (float)(u + 1);  // n_samp >= 1
-    const float yx = __builtin_fmaf(k, dxs, mx), yy = __builtin_fmaf(k, dys, my);  // rint(k*d) + magic + origin
-    a[u] = __umul24(__builtin_bit_cast(uint32_t, yy), PC) + __builtin_bit_cast(uint32_t, yx) - kofs;
+    const uint32_t ki = (CLAMP && u > 0) ? (uint32_t)(u + 1 < n_samp ? u + 1 : n_samp) : (uint32_t)(u + 1);
+    const float k = __builtin_bit_cast(float, ki);  // ki * 2^-149 (wave-uniform)
+    const float yx = __builtin_fmaf(k, dxs, mx), yy = __builtin_fmaf(k, dys, my);
+    a[u] = __umul24(__builtin_bit_cast(uint32_t, yy), PC) + __builtin_bit_cast(uint32_t, yx);
     w[u] = lds_ld(a[u]);
   }
   uint32_t stop = 0;
@@ -332,9 +345,9 @@ __device__ __forceinline__ int march_fast(uint32_t PC, uint32_t own, uint32_t du
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
     if (COUNT) cnt = (stop == 0 && w[u] != 0 && u < n_samp) ? u + 1 : cnt;
-    stop |= w[u];
-    const bool skip = stop != 0 || (u < 2 && a[u] == own);
-    lds_st((skip ? dummy : a[u]) + D, 1);
+    stop = u == 0 ? w[0] : or_b32(stop, w[u]);
+    const uint32_t skip = u < 2 ? or_b32(stop, (uint32_t)(a[u] == own)) : stop;  // 0 or 1
+    lds_st(__umul24(skip, 3u * D) + a[u] + D, 1);
   }
   return cnt;
 }
@@ -434,12 +447,6 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
   const int wave = uni((int)(threadIdx.x >> 6));
   int* queue = L.queue + wave * 64;
   const uint32_t base = (uint32_t)(uintptr_t)smem;  // LDS address of the stop map
-  // bits(kMagic32 + v) = 0x4B400000 + v: the row's low 24 bits carry 0x400000 into the
-  // product, which kofs removes together with the column's exponent bits.
-  const uint32_t kofs = 0x400000u * (uint32_t)PC + 0x4B400000u - base;
-  // masked fast-path stores: one dword per lane of a 32-lane LDS group, in the vis plane's
-  // top ring rows (G * PC >= 78 bytes; wrapped below that)
-  const uint32_t dummy = base + (uint32_t)((4 * (threadIdx.x & 31)) % (kRing * PC));
   unsigned int n_eval = 0, n_exact = 0;
   int qn = 0;               // near-tie rays met by this wave (queued while <= 64)
   bool exact_em = false;    // this wave owns chunks of an exact-only emitter
@@ -474,18 +481,20 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
     if (active && !tie) {
       const uint32_t own = base + (uint32_t)((E.row + kRing) * PC + (E.col + kRing));
       const int n_samp = E.kind == 0 ? 2 * E.range : E.range;
-      const float mx = kMagic32 + (float)(E.col + kRing), my = kMagic32 + (float)(E.row + kRing);
+      // the padded emitter position as denormal bit patterns (march_fast), LDS base on the column
+      const float mx = __builtin_bit_cast(float, base + (uint32_t)(E.col + kRing));
+      const float my = __builtin_bit_cast(float, (uint32_t)(E.row + kRing));
       const float h = E.kind == 0 ? 0.5f : 1.0f;  // sample stride: camera half tiles, guard whole tiles
       const float dxs = below_one(cf) * h, dys = -below_one(sf) * h;  // exact scalings; dy = -sin (security.py:72-75)
       int done;
       if (n_samp == 2 * kTieMaxRange)  // the reference cameras (range 6)
-        done = march_fast<D, 2 * kTieMaxRange, false, COUNT>(PC, own, dummy, dxs, dys, mx, my, kofs, n_samp);
+        done = march_fast<D, 2 * kTieMaxRange, false, COUNT>(PC, own, dxs, dys, mx, my, n_samp);
       else if (n_samp == 4)  // the reference guards (range 4)
-        done = march_fast<D, 4, false, COUNT>(PC, own, dummy, dxs, dys, mx, my, kofs, n_samp);
+        done = march_fast<D, 4, false, COUNT>(PC, own, dxs, dys, mx, my, n_samp);
       else if (n_samp < 4)
-        done = march_fast<D, 4, true, COUNT>(PC, own, dummy, dxs, dys, mx, my, kofs, n_samp);
+        done = march_fast<D, 4, true, COUNT>(PC, own, dxs, dys, mx, my, n_samp);
       else
-        done = march_fast<D, 2 * kTieMaxRange, true, COUNT>(PC, own, dummy, dxs, dys, mx, my, kofs, n_samp);
+        done = march_fast<D, 2 * kTieMaxRange, true, COUNT>(PC, own, dxs, dys, mx, my, n_samp);
       n_eval += (unsigned int)done;
     }
   }

@@ -13,6 +13,8 @@
 //     [3][R][C] float32 observation (environment.py:347-374) leaves in 16-byte stores.
 // Arithmetic follows the reference's IEEE double semantics exactly: no FMA
 // contraction, half-to-even rint(), glibc-exact sin/cos (heist_trig.h).
+#include <utility>
+
 #include "heist_device.h"
 #include "heist_trig.h"
 
@@ -311,6 +313,34 @@ __device__ __forceinline__ uint32_t or_b32(uint32_t a, uint32_t b) {
   return r;
 }
 
+// (x, y) = K * 2^-149 * (dxs, dys) + (mx, my) as ONE v_pk_fma_f32 (two fp32 FMAs, each
+// rounded once, as v_fma_f32 does); K is an integer inline constant, i.e. the denormal
+// K * 2^-149, applied to both halves (op_sel_hi).  Inline asm: the compiler's own packed
+// form of this loop is miscompiled by ROCm 7.2 clang (see march_fast).
+template <int K>
+__device__ __forceinline__ uint64_t pk_fma_k(uint64_t d, uint64_t m) {
+  static_assert(K >= 1 && K <= 12, "inline constant");
+  uint64_t r;
+#define HEIST_PKC(n) \
+  if constexpr (K == n) asm("v_pk_fma_f32 %0, %1, " #n ", %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(d), "s"(m));
+  HEIST_PKC(1) HEIST_PKC(2) HEIST_PKC(3) HEIST_PKC(4) HEIST_PKC(5) HEIST_PKC(6)
+  HEIST_PKC(7) HEIST_PKC(8) HEIST_PKC(9) HEIST_PKC(10) HEIST_PKC(11) HEIST_PKC(12)
+#undef HEIST_PKC
+  return r;
+}
+
+template <int U>
+__device__ __forceinline__ uint32_t fast_addr(uint32_t PC, uint64_t d, uint64_t m) {
+  const uint64_t r = pk_fma_k<U + 1>(d, m);
+  return __umul24((uint32_t)(r >> 32), PC) + (uint32_t)r;
+}
+
+template <int NS, int... Us>
+__device__ __forceinline__ void fast_addrs(uint32_t (&a)[NS], uint32_t PC, uint64_t d, uint64_t m,
+                                           std::integer_sequence<int, Us...>) {
+  ((a[Us] = fast_addr<Us>(PC, d, m)), ...);
+}
+
 // Every sample k = 1 .. n_samp of a fast ray in one LDS round trip.  Coordinates are
 // computed in units of the smallest fp32 denormal (2^-149; fp32 denormals are preserved):
 // k and the padded emitter (col, row) -- the LDS base folded into the column -- enter as
@@ -332,12 +362,17 @@ template <int D, int NS, bool CLAMP, bool COUNT>
 __device__ __forceinline__ int march_fast(uint32_t PC, uint32_t own, float dxs, float dys, float mx, float my,
                                           int n_samp) {
   uint32_t a[NS], w[NS];
+  const uint64_t dv = ((uint64_t)__builtin_bit_cast(uint32_t, dys) << 32) | __builtin_bit_cast(uint32_t, dxs);
+  const uint64_t mv = ((uint64_t)__builtin_bit_cast(uint32_t, my) << 32) | __builtin_bit_cast(uint32_t, mx);
+  if constexpr (!CLAMP) fast_addrs(a, PC, dv, mv, std::make_integer_sequence<int, NS>{});
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
-    const uint32_t ki = (CLAMP && u > 0) ? (uint32_t)(u + 1 < n_samp ? u + 1 : n_samp) : (uint32_t)(u + 1);
-    const float k = __builtin_bit_cast(float, ki);  // ki * 2^-149 (wave-uniform)
-    const float yx = __builtin_fmaf(k, dxs, mx), yy = __builtin_fmaf(k, dys, my);
-    a[u] = __umul24(__builtin_bit_cast(uint32_t, yy), PC) + __builtin_bit_cast(uint32_t, yx);
+    if (CLAMP) {
+      const uint32_t ki = u > 0 ? (uint32_t)(u + 1 < n_samp ? u + 1 : n_samp) : 1u;
+      const float k = __builtin_bit_cast(float, ki);  // ki * 2^-149 (wave-uniform)
+      const float yx = __builtin_fmaf(k, dxs, mx), yy = __builtin_fmaf(k, dys, my);
+      a[u] = __umul24(__builtin_bit_cast(uint32_t, yy), PC) + __builtin_bit_cast(uint32_t, yx);
+    }
     w[u] = lds_ld(a[u]);
   }
   uint32_t stop = 0;

@@ -73,10 +73,13 @@ struct Emit {
   double fov;
   double step;    // fov / num_rays: the fast path's ray spacing (approximate angle)
   int32_t row, col, range, num_rays;
-  int32_t first;  // index of this emitter's ray 0 in the env's flattened ray list
+  int32_t first;  // index of this emitter's first 64-ray chunk in the env's chunk list
   int32_t kind;   // 0 camera (half-tile sub-steps), 1 guard (whole-tile steps), 2 guard with a cached cone (no rays)
+  int32_t members;  // direction group (publish_emitters): a leader's count of consecutive slots sharing its
+                    // ray directions (itself included); 0 for the other members (no chunks of their own)
+  int32_t pad_;
 };
-static_assert(sizeof(Emit) == 48, "Emit layout");
+static_assert(sizeof(Emit) == 56, "Emit layout");
 
 struct EnvParams {
   int R, C, RC, max_steps;

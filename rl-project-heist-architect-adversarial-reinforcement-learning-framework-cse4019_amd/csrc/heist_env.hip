@@ -430,7 +430,7 @@ __device__ __forceinline__ Emit uni(const Emit& e) {
   Emit u;
   u.hmh = uni(e.hmh); u.fov = uni(e.fov); u.step = uni(e.step);
   u.row = uni(e.row); u.col = uni(e.col); u.range = uni(e.range); u.num_rays = uni(e.num_rays);
-  u.first = uni(e.first); u.kind = uni(e.kind);
+  u.first = uni(e.first); u.kind = uni(e.kind); u.members = uni(e.members);
   return u;
 }
 
@@ -514,23 +514,31 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
     }
     qn += __popcll(b);
     if (active && !tie) {
-      const uint32_t own = base + (uint32_t)((E.row + kRing) * PC + (E.col + kRing));
-      const int n_samp = E.kind == 0 ? 2 * E.range : E.range;
-      // the padded emitter position as denormal bit patterns (march_fast), LDS base on the column
-      const float mx = __builtin_bit_cast(float, base + (uint32_t)(E.col + kRing));
-      const float my = __builtin_bit_cast(float, (uint32_t)(E.row + kRing));
+      const int n_samp = E.kind == 0 ? 2 * E.range : E.range;  // every member of a group: same range
       const float h = E.kind == 0 ? 0.5f : 1.0f;  // sample stride: camera half tiles, guard whole tiles
       const float dxs = below_one(cf) * h, dys = -below_one(sf) * h;  // exact scalings; dy = -sin (security.py:72-75)
-      int done;
+      // the ray of every member of the direction group: same direction, each from its own tile
+      auto group = [&](auto ns, auto clamp) {
+        constexpr int NS = decltype(ns)::value;
+        constexpr bool CL = decltype(clamp)::value;
+        for (int m = 0; m < E.members; ++m) {
+          const int row = m == 0 ? E.row : uni(L.em[k + m].row);
+          const int col = m == 0 ? E.col : uni(L.em[k + m].col);
+          const uint32_t own = base + (uint32_t)((row + kRing) * PC + (col + kRing));
+          // the padded emitter position as denormal bit patterns (march_fast), LDS base on the column
+          const float mx = __builtin_bit_cast(float, base + (uint32_t)(col + kRing));
+          const float my = __builtin_bit_cast(float, (uint32_t)(row + kRing));
+          n_eval += (unsigned int)march_fast<D, NS, CL, COUNT>(PC, own, dxs, dys, mx, my, n_samp);
+        }
+      };
       if (n_samp == 2 * kTieMaxRange)  // the reference cameras (range 6)
-        done = march_fast<D, 2 * kTieMaxRange, false, COUNT>(PC, own, dxs, dys, mx, my, n_samp);
+        group(std::integral_constant<int, 2 * kTieMaxRange>{}, std::false_type{});
       else if (n_samp == 4)  // the reference guards (range 4)
-        done = march_fast<D, 4, false, COUNT>(PC, own, dxs, dys, mx, my, n_samp);
+        group(std::integral_constant<int, 4>{}, std::false_type{});
       else if (n_samp < 4)
-        done = march_fast<D, 4, true, COUNT>(PC, own, dxs, dys, mx, my, n_samp);
+        group(std::integral_constant<int, 4>{}, std::true_type{});
       else
-        done = march_fast<D, 2 * kTieMaxRange, true, COUNT>(PC, own, dxs, dys, mx, my, n_samp);
-      n_eval += (unsigned int)done;
+        group(std::integral_constant<int, 2 * kTieMaxRange>{}, std::true_type{});
     }
   }
   if (probe == 2) return;
@@ -539,9 +547,11 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
   if (qn <= 64) {
     if (lane < qn) {
       const int v = queue[lane];
-      const Emit E = L.em[v >> 16];
-      ++n_exact;
-      n_eval += (unsigned int)exact_ray<U, D>(smem, E, v & 0xffff, PC, probe, hd);
+      const int kq = v >> 16;
+      for (int m = 0; m < L.em[kq].members; ++m) {
+        ++n_exact;
+        n_eval += (unsigned int)exact_ray<U, D>(smem, L.em[kq + m], v & 0xffff, PC, probe, hd);
+      }
     }
   } else {
     k = 0;
@@ -552,10 +562,11 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
       const int i = (c - E.first) * 64 + lane;
       float cf, sf, xr;
       fast_dir(__builtin_fma((double)i, E.step, E.hmh), &cf, &sf, &xr);
-      if (i <= E.num_rays && near_tie(cf, sf, xr, E.kind == 0)) {
-        ++n_exact;
-        n_eval += (unsigned int)exact_ray<U, D>(smem, E, i, PC, probe, hd);
-      }
+      if (i <= E.num_rays && near_tie(cf, sf, xr, E.kind == 0))
+        for (int m = 0; m < E.members; ++m) {
+          ++n_exact;
+          n_eval += (unsigned int)exact_ray<U, D>(smem, L.em[k + m], i, PC, probe, hd);
+        }
     }
   }
   if (exact_em) {
@@ -565,10 +576,11 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
       const Emit E = uni(L.em[k]);
       if (fast_emitter(E, mode)) continue;
       const int i = (c - E.first) * 64 + lane;
-      if (i <= E.num_rays) {
-        ++n_exact;
-        n_eval += (unsigned int)exact_ray<U, D>(smem, E, i, PC, probe, hd);
-      }
+      if (i <= E.num_rays)
+        for (int m = 0; m < E.members; ++m) {
+          ++n_exact;
+          n_eval += (unsigned int)exact_ray<U, D>(smem, L.em[k + m], i, PC, probe, hd);
+        }
     }
   }
   if (COUNT) {
@@ -582,11 +594,24 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
 // kind -1 and no rays).  Every slot lives in wave 0 (at most 64 of them), where an
 // exclusive lane scan of the emitters' chunk counts (ceil((num_rays + 1) / 64) chunks of
 // 64 rays) gives each emitter its first chunk index.
+// Direction groups: a camera whose (heading - fov/2, fov, num_rays, range) equal the
+// previous slot's casts its rays in the same directions (security.py:70), so it joins that
+// slot's group and gets no chunks of its own; the group leader's chunks compute each ray
+// direction (and its tie screen) once and march it from every member's tile.  Cameras an
+// Architect decodes share one fov/speed/heading per layout (networks.py:283-322), so all
+// of a layout's cameras form one group.
 static_assert(kMaxEmitters <= 64, "publish_emitters keeps every emitter in wave 0");
 __device__ __forceinline__ void publish_emitters(const EnvLds& L, Emit E, int n_em) {
   const int t = threadIdx.x;
   if (t < 64) {
-    const int cnt = (t < n_em && (E.kind == 0 || E.kind == 1)) ? (E.num_rays + 1 + 63) / 64 : 0;  // 2: cached cone
+    const double ph = __shfl_up(E.hmh, 1, 64), pf = __shfl_up(E.fov, 1, 64);
+    const int pn = __shfl_up(E.num_rays, 1, 64), pr = __shfl_up(E.range, 1, 64), pk = __shfl_up(E.kind, 1, 64);
+    const bool cont = t > 0 && t < n_em && E.kind == 0 && pk == 0 && ph == E.hmh && pf == E.fov &&
+                      pn == E.num_rays && pr == E.range;
+    const unsigned long long lead = __ballot(!cont) | (n_em < 64 ? 1ull << n_em : 0ull);  // + sentinel slot n_em
+    const unsigned long long above = t < 63 ? lead >> (t + 1) : 0ull;
+    E.members = cont ? 0 : (above ? (int)__builtin_ctzll(above) + 1 : 64 - t);
+    const int cnt = (t < n_em && !cont && (E.kind == 0 || E.kind == 1)) ? (E.num_rays + 1 + 63) / 64 : 0;  // 2: cached cone
     int incl = cnt;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -612,7 +637,7 @@ __device__ __forceinline__ Emit cam_emit(const Cam& cm) {
   E.fov = cm.fov;
   E.row = cm.row; E.col = cm.col; E.range = cm.range; E.num_rays = cm.num_rays;
   E.step = cm.fov * __builtin_amdgcn_rcp((double)cm.num_rays);  // fast-path angles only: approximate
-  E.first = 0; E.kind = 0;
+  E.first = 0; E.kind = 0; E.members = 1;
   return E;
 }
 
@@ -622,7 +647,7 @@ __device__ __forceinline__ Emit guard_emit(const Guard& gd) {
   E.fov = gd.fov;
   E.row = unpack_r(gd.pos); E.col = unpack_c(gd.pos); E.range = gd.range; E.num_rays = gd.num_rays;
   E.step = gd.fov * __builtin_amdgcn_rcp((double)gd.num_rays);
-  E.first = 0; E.kind = gd.hslot == kUncached ? 1 : 2;
+  E.first = 0; E.kind = gd.hslot == kUncached ? 1 : 2; E.members = 1;
   return E;
 }
 
@@ -907,6 +932,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   const bool act = !s.done;
   const int a_raw = (int)actions[e];
   clear_vis<NT>(p, L);
+  if (p.probe_mode == 8) return;  // profiling: prefetch issue + plane clears only
   HEIST_STEP_STAMP(1);
   // One barrier before the raycast: the emitter slots all live in wave 0, whose lanes
   // update them from their records alone (a guard's next patrol point and its cached
@@ -975,6 +1001,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     E = guard_emit(gd);
   }
   publish_emitters(L, E, n_slot);
+  if (p.probe_mode == 9) return;  // profiling: everything before the raycast barrier
   HEIST_STEP_STAMP(2);
   // 3. visibility (environment.py:257-258); an already-done env recomputes the same plane
   raycast_pass<NT, U, D>(p, e, smem, L, n_slot, mc);
@@ -1335,6 +1362,7 @@ __global__ __launch_bounds__(64) void guard_cone_kernel(EnvParams p, const uint8
     E.num_rays = gd.num_rays;
     E.first = 0;
     E.kind = 1;
+    E.members = 1;
     for (int ray = lane; ray <= E.num_rays; ray += 64) exact_ray<U, D>(smem, E, ray, L.PC, 0, p.half_deg);
     __syncthreads();
     if (lane < 16) {
@@ -1395,7 +1423,7 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
     E.fov = fov;
     E.row = row; E.col = col; E.range = range; E.num_rays = num_rays_for(fov);
     E.step = fov / (double)E.num_rays;
-    E.first = 0; E.kind = kind;
+    E.first = 0; E.kind = kind; E.members = 1;
     L.em[0] = E;
     L.meta[0] = 1;
     L.meta[1] = (E.num_rays + 1 + 63) / 64;  // 64-ray chunks (publish_emitters)

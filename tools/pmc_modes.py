@@ -1,6 +1,6 @@
 """Per-probe-mode PMC summary: rocprofv3 --pmc counter CSV of tools/probe_step_modes.py,
 whose step_kernel dispatches come in blocks of 55 (5 warm-up + 50 timed) cycling through
-the probe modes 0..7 for 5 rounds.  Prints, per mode, the median of each counter over its
+the probe modes 0..9 for 5 rounds.  Prints, per mode, the median of each counter over its
 dispatches, divided by SQ_WAVES where that makes a per-wave figure.
     python tools/pmc_modes.py <counter_collection.csv> [out.json]"""
 import collections
@@ -8,7 +8,7 @@ import csv
 import json
 import sys
 
-MODES = (0, 1, 2, 3, 4, 5, 6, 7)
+MODES = (0, 1, 2, 3, 4, 5, 6, 7, 8, 9)
 PER_MODE = 55
 
 

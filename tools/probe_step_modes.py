@@ -2,7 +2,8 @@
 with HEIST_PROBE_MODE = 0 (normal), 1 (no rays), 2 (ray angles + sin/cos only),
 3 (marching with a fixed direction, no sin/cos), 4 (no observation write), 5 (neither
 rays nor observation write), 6 (return at entry: launch + dispatch floor), 7 (return after
-the raycast).  Modes 1-7 give wrong results on
+the raycast), 8 (return after the prefetch issue and plane clears), 9 (return before the
+raycast barrier: + camera/guard update and emitter table).  Modes 1-7 give wrong results on
 purpose; they only bound the cost of each part.  One JSON line per mode."""
 import json
 import os
@@ -29,7 +30,7 @@ def bench_layouts(env, seed=1234):
 def main():
     n = int(os.environ.get("PROBE_N", "4096"))
     envs = {}
-    for mode in (0, 1, 2, 3, 4, 5, 6, 7):
+    for mode in (0, 1, 2, 3, 4, 5, 6, 7, 8, 9):
         os.environ["HEIST_PROBE_MODE"] = str(mode)
         env = HeistEnv(n, EnvironmentConfig(), max_cams=8, max_guards=4, max_path=16, device="cuda", auto_reset=True)
         bench_layouts(env)

@@ -54,17 +54,16 @@ __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(
 struct EnvLds {
   uint8_t* wall;   // LDS offset 0: [(R+2G)(C+2G)] ray stop map, 1 = wall or outside the grid (G = kRing)
   uint8_t* vis;    // LDS offset D: visibility with the same padded geometry (ring bytes unused): camera
-                   // rays and live-raycast guards
-  uint8_t* gvis;   // LDS offset 2D: the cached guard cones (same geometry); visibility = vis | gvis
-  uint8_t* gvis_r; // LDS offset 3D: the cached guard cones after an in-step auto-reset (guards at patrol point 0)
-                   // LDS offset 4D: sink plane, where march_fast sends the stores of stopped samples
+                   // rays and live-raycast guards; the cached guard cones are ORed in where read
+                   // (cone_vis4).  LDS offset 2D: sink plane, where march_fast sends the stores of
+                   // stopped samples (never read)
   uint8_t* grid;   // [RC]
   Emit* em;        // [n_emit]
   uint16_t* path;  // [max_guards][max_path]
   int* queue;      // [W][64] per-wave exact-path ray queues (cast_rays)
   int* meta;       // [0] emitters, [1] total rays
-  uint16_t* cone;  // [2][max_guards][16] cached guard cones (kind-2 emitters, heist_device.h): this tick's
-                   // pose, then the pose an auto-reset would give (patrol point 0, same heading)
+  uint16_t* cone;  // [2][max_guards][16] cached guard cones (kind-2 emitters, heist_device.h): set 0 this
+                   // tick's pose, set 1 the pose an auto-reset would give (patrol point 0, same heading)
   uint32_t* rpos;  // [max_guards] patrol point 0 of each guard (row | col << 8), for the reset cones
   int PC;          // padded row stride C + 2G
   int off0;        // padded index of tile (0, 0): G * PC + G
@@ -85,7 +84,7 @@ __host__ __device__ inline int padded_bytes(int R, int C) { return (R + 2 * kRin
 __host__ __device__ inline size_t env_lds_bytes(int R, int C, int n_emit, int path_words, int D, int waves,
                                                 int cone_guards = 0) {
   const int RC = R * C;
-  return 5 * (size_t)D + align16(RC) + align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) +
+  return 3 * (size_t)D + align16(RC) + align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1)) +
          align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1)) +
          sizeof(int) * 64 * (size_t)waves + 32 + 68 * (size_t)cone_guards;
 }
@@ -97,9 +96,7 @@ __device__ __forceinline__ EnvLds carve(unsigned char* smem, int R, int C, int n
   EnvLds L;
   L.wall = smem;
   L.vis = smem + D;
-  L.gvis = smem + 2 * (size_t)D;
-  L.gvis_r = smem + 3 * (size_t)D;
-  size_t o = 5 * (size_t)D;  // [4D, 5D): the fast path's sink for masked stores (never read)
+  size_t o = 3 * (size_t)D;  // [2D, 3D): the fast path's sink for masked stores (never read)
   L.grid = smem + o; o += align16(RC);
   L.em = reinterpret_cast<Emit*>(smem + o); o += align16(sizeof(Emit) * (n_emit > 0 ? n_emit : 1));
   L.path = reinterpret_cast<uint16_t*>(smem + o); o += align16(sizeof(uint16_t) * (path_words > 0 ? path_words : 1));
@@ -351,7 +348,7 @@ __device__ __forceinline__ void fast_addrs(uint32_t (&a)[NS], uint32_t PC, uint6
 // (kRing >= kTieMaxRange), so each sample address lies inside the padded stop map whether
 // or not the ray has already stopped: all NS wall reads are issued before any is used, and
 // a running stop flag sends the visibility store of a stopped sample (and of the emitter's
-// own tile) to the sink plane (address + 3D, i.e. 4D .. 5D, never read) with one more
+// own tile) to the sink plane (address + D, i.e. 2D .. 3D, never read) with one more
 // mad_u24 instead of a compare and select.  NS = n_samp, or with CLAMP NS >= n_samp and the
 // samples past n_samp repeat sample n_samp (k clamped), which changes nothing.  Only the
 // first two samples can land on the emitter's own tile (see cast_rays).  Returns the ray's
@@ -382,7 +379,7 @@ __device__ __forceinline__ int march_fast(uint32_t PC, uint32_t own, float dxs, 
     if (COUNT) cnt = (stop == 0 && w[u] != 0 && u < n_samp) ? u + 1 : cnt;
     stop = u == 0 ? w[0] : or_b32(stop, w[u]);
     const uint32_t skip = u < 2 ? or_b32(stop, (uint32_t)(a[u] == own)) : stop;  // 0 or 1
-    lds_st(__umul24(skip, 3u * D) + a[u] + D, 1);
+    lds_st(__umul24(skip, (uint32_t)D) + a[u] + D, 1);
   }
   return cnt;
 }
@@ -622,11 +619,14 @@ __device__ __forceinline__ void publish_emitters(const EnvLds& L, Emit E, int n_
       E.first = incl - cnt;
       L.em[t] = E;
     }
+    const unsigned long long cached = __ballot(t < n_em && E.kind == 2);  // guards with a cached cone
     if (t == 63) {
       L.meta[0] = n_em;
       L.meta[1] = incl;
       L.meta[2] = 0;
       L.meta[4] = 0;
+      L.meta[6] = (int)(uint32_t)cached;
+      L.meta[7] = (int)(uint32_t)(cached >> 32);
     }
   }
 }
@@ -677,32 +677,37 @@ __device__ __forceinline__ void stage_guard_cone(const EnvParams& p, int e, cons
   dst[1] = b;
 }
 
-// OR every cached guard cone staged in LDS into the visibility plane: thread q of the
-// 16 x 15 window sets tile (row + q/16 - 7, col + q%16 - 7) if its bit is set (bits only
-// ever name tiles inside the grid, so the address is always in the plane).
-// RESET: the cones an in-step auto-reset gives (staged after this tick's, guards at
-// patrol point 0) into the reset plane gvis_r instead.
-template <int NT, bool RESET = false>
-__device__ __forceinline__ void stamp_guard_cones(const EnvLds& L, int mc, int n_slot) {
-  const int mg = n_slot - mc;
-  for (int k = mc; k < n_slot; ++k) {
-    if (uni(L.em[k].kind) != 2) continue;
-    int r0, c0;
-    if (RESET) {
-      const int rp = uni((int)L.rpos[k - mc]);
-      r0 = unpack_r(rp) - kConeRange;
-      c0 = unpack_c(rp) - kConeRange;
+// Visibility of tiles (r, c0 .. c0 + 3) under the cached guard cones (the kind-2 slots,
+// mask in meta[6..7] from publish_emitters) as four 0/1 bytes (byte j = tile c0 + j), read
+// straight from the staged 32-byte cone entries instead of stamping them into a plane.
+// set 0: this tick's cones (rows L.cone[16 g], guard on its emitter slot's tile); set 1: the
+// cones an in-step auto-reset gives (rows L.cone[16 (mg + g)], guard at patrol point 0).
+// Bit dc + 7 of row dr + 7 is tile (gr + dr, gc + dc); a cone only names tiles inside the
+// grid (guard_cone_kernel), so no bounds test on (r, c) is needed.
+__device__ __forceinline__ uint32_t cone_vis4(const EnvLds& L, int mc, int mg, int set, int r, int c0) {
+  uint64_t m = ((uint64_t)(uint32_t)uni(L.meta[7]) << 32) | (uint32_t)uni(L.meta[6]);
+  uint32_t v = 0;
+  while (m) {
+    const int k = (int)__builtin_ctzll(m);
+    m &= m - 1;
+    const int g = k - mc;
+    int gr, gc;
+    if (set) {
+      const int rp = uni((int)L.rpos[g]);
+      gr = unpack_r(rp);
+      gc = unpack_c(rp);
     } else {
-      r0 = uni(L.em[k].row) - kConeRange;
-      c0 = uni(L.em[k].col) - kConeRange;
+      gr = uni(L.em[k].row);
+      gc = uni(L.em[k].col);
     }
-    const uint16_t* rows = L.cone + 16 * ((RESET ? mg : 0) + k - mc);
-    uint8_t* plane = RESET ? L.gvis_r : L.gvis;
-    for (int q = threadIdx.x; q < 16 * (2 * kConeRange + 1); q += NT) {
-      const int rr = q >> 4, cc = q & 15;
-      if ((rows[rr] >> cc) & 1u) plane[L.at(r0 + rr, c0 + cc)] = 1;
-    }
+    const int dr = r - gr + kConeRange;
+    const uint32_t row = (unsigned)dr <= 2u * kConeRange ? (uint32_t)L.cone[16 * (set * mg + g) + dr] : 0u;
+    // bits dc .. dc + 3 of the row, dc = c0 - gc + 7 in [-4, 28) after the shift by 4
+    const int sh = c0 - gc + kConeRange + 4;
+    const uint32_t b = __builtin_amdgcn_ubfe(row << 4, (uint32_t)(sh < 0 ? 0 : (sh > 31 ? 31 : sh)), 4u);
+    v |= (b * 0x204081u) & 0x01010101u;  // bit j -> byte j
   }
+  return v;
 }
 
 // Visibility (visibility.py:31-65) once the emitter table (n_slot slots, guards from slot
@@ -716,7 +721,6 @@ __device__ __forceinline__ void raycast_pass(const EnvParams& p, int e, unsigned
     const Emit E = L.em[t];
     if (E.kind == 1) L.vis[L.at(E.row, E.col)] = 1;
   }
-  stamp_guard_cones<NT>(L, mc, n_slot);
   if (p.probe_mode != 1 && p.probe_mode != 5) {
     if (p.sample_counter || p.redo_counter)
       cast_rays<NT, U, D, true>(smem, L, p.ray_mode, p.probe_mode, p.half_deg);
@@ -728,19 +732,11 @@ __device__ __forceinline__ void raycast_pass(const EnvParams& p, int e, unsigned
   if (p.redo_counter && t == 0) p.redo_counter[e] += (unsigned int)L.meta[4];
 }
 
-// Zero the ray plane (RAYS) and / or the cached-cone plane (CONES).
-template <int NT, bool RAYS = true, bool CONES = true>
+// Zero the ray plane.
+template <int NT>
 __device__ __forceinline__ void clear_vis(const EnvParams& p, const EnvLds& L) {
   uint32_t* v4 = reinterpret_cast<uint32_t*>(L.vis);
-  uint32_t* g4 = reinterpret_cast<uint32_t*>(L.gvis);
-  uint32_t* r4 = reinterpret_cast<uint32_t*>(L.gvis_r);
-  for (int i = threadIdx.x; i < (padded_bytes(p.R, p.C) + 3) / 4; i += NT) {
-    if (RAYS) v4[i] = 0u;
-    if (CONES) {
-      g4[i] = 0u;
-      r4[i] = 0u;
-    }
-  }
+  for (int i = threadIdx.x; i < (padded_bytes(p.R, p.C) + 3) / 4; i += NT) v4[i] = 0u;
 }
 
 // ---------------------------------------------------------------------------
@@ -812,14 +808,16 @@ __device__ __forceinline__ void patch4(float4& v, int m, float val) {
   else if (m == 3) v.w = val;
 }
 
-// Observation row [3][R][C] (environment.py:347-374): occupancy / 5, visibility, and the
-// position channel (static plane with the solver and vault cells patched; the vault
-// wins if the solver stands on it).
+// Observation row [3][R][C] (environment.py:347-374): occupancy / 5, visibility (ray
+// plane | cached guard cones of cone set `cset`, cone_vis4), and the position channel
+// (static plane with the solver and vault cells patched; the vault wins if the solver
+// stands on it).
 template <int NT>
-__device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvScalars& s, const EnvLds& L,
-                                          const uint8_t* cones, float* __restrict__ obs) {
+__device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvScalars& s, const EnvLds& L, int cset,
+                                          float* __restrict__ obs) {
   const int t = threadIdx.x;
   const int RC = p.RC, C = p.C;
+  const int mc = p.max_cams, mg = p.max_guards;
   float* o = obs + (size_t)e * 3 * RC;
   const int solver = s.pos_r * C + s.pos_c;
   const int vault = p.vr * C + p.vc;
@@ -830,36 +828,36 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
     float4* o0 = reinterpret_cast<float4*>(o);
     float4* o1 = o0 + n4;
     float4* o2 = o1 + n4;
-    // the first half of the block writes channels 0 and 1, the second half channel 2
+    // the first half of the block writes channels 0 and 2, the second half channel 1
     constexpr int H = NT / 2;
     if (t < H) {
-    for (int q = t; q < n4; q += H) {
-      const uint32_t b = *reinterpret_cast<const uint32_t*>(L.grid + 4 * q);
-      // float32(tile) / 5 == float32(tile) * 0.2f for every tile type 0..7 (checked), and the
-      // byte -> float conversion is one v_cvt_f32_ubyteN
-      o0[q] = make_float4((float)(b & 0xff) * 0.2f, (float)((b >> 8) & 0xff) * 0.2f,
-                          (float)((b >> 16) & 0xff) * 0.2f, (float)(b >> 24) * 0.2f);
-      const int r = q / c4;
-      const int a = L.at(r, 4 * (q - r * c4));
-      uint32_t v;
-      if ((kRing & 3) == 0) {
-        v = *reinterpret_cast<const uint32_t*>(L.vis + a) | *reinterpret_cast<const uint32_t*>(cones + a);
-      } else {
-        const uint16_t* vp2 = reinterpret_cast<const uint16_t*>(L.vis + a);
-        const uint16_t* gp2 = reinterpret_cast<const uint16_t*>(cones + a);
-        v = ((uint32_t)vp2[0] | ((uint32_t)vp2[1] << 16)) | ((uint32_t)gp2[0] | ((uint32_t)gp2[1] << 16));
+      const int qs = solver >> 2, qv = vault >> 2;
+      for (int q = t; q < n4; q += H) {
+        const uint32_t b = *reinterpret_cast<const uint32_t*>(L.grid + 4 * q);
+        // float32(tile) / 5 == float32(tile) * 0.2f for every tile type 0..7 (checked), and the
+        // byte -> float conversion is one v_cvt_f32_ubyteN
+        o0[q] = make_float4((float)(b & 0xff) * 0.2f, (float)((b >> 8) & 0xff) * 0.2f,
+                            (float)((b >> 16) & 0xff) * 0.2f, (float)(b >> 24) * 0.2f);
+        float4 v = reinterpret_cast<const float4*>(p.plane0)[q];  // the handle's static plane (L2-resident)
+        if (q == qs) patch4(v, solver & 3, sv);          // only the solver's and the vault's
+        if (q == qv) patch4(v, vault & 3, p.vault_val);  // float4 take these branches
+        o2[q] = v;
       }
-      // visibility bytes are 0 or 1 in both planes, so their OR converts directly
-      o1[q] = make_float4((float)(v & 0xff), (float)((v >> 8) & 0xff), (float)((v >> 16) & 0xff), (float)(v >> 24));
-    }
     } else {
-    const int qs = solver >> 2, qv = vault >> 2;
-    for (int q = t - H; q < n4; q += H) {
-      float4 v = reinterpret_cast<const float4*>(p.plane0)[q];  // the handle's static plane (L2-resident)
-      if (q == qs) patch4(v, solver & 3, sv);          // only the solver's and the vault's
-      if (q == qv) patch4(v, vault & 3, p.vault_val);  // float4 take these branches
-      o2[q] = v;
-    }
+      for (int q = t - H; q < n4; q += H) {
+        const int r = q / c4, c0 = 4 * (q - r * c4);
+        const int a = L.at(r, c0);
+        uint32_t v;
+        if ((kRing & 3) == 0) {
+          v = *reinterpret_cast<const uint32_t*>(L.vis + a);
+        } else {
+          const uint16_t* vp2 = reinterpret_cast<const uint16_t*>(L.vis + a);
+          v = (uint32_t)vp2[0] | ((uint32_t)vp2[1] << 16);
+        }
+        v |= cone_vis4(L, mc, mg, cset, r, c0);
+        // visibility bytes are 0 or 1, so they convert directly
+        o1[q] = make_float4((float)(v & 0xff), (float)((v >> 8) & 0xff), (float)((v >> 16) & 0xff), (float)(v >> 24));
+      }
     }
   } else {
     for (int q = t; q < 3 * RC; q += NT) {
@@ -869,8 +867,8 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
       if (ch == 0) {
         v = p.tile_lut[L.grid[cell] & 7];
       } else if (ch == 1) {
-        const int r = cell / C;
-        v = (L.vis[L.at(r, cell - r * C)] | cones[L.at(r, cell - r * C)]) ? 1.0f : 0.0f;
+        const int r = cell / C, c = cell - r * C;
+        v = (L.vis[L.at(r, c)] | (cone_vis4(L, mc, mg, cset, r, c) & 1u)) ? 1.0f : 0.0f;
       } else {
         v = cell == vault ? p.vault_val : (cell == solver ? sv : p.plane0[cell]);
       }
@@ -1028,7 +1026,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     reward += (double)(s.prev_dist - curr) * 0.1;
     s.prev_dist = curr;
     if (curr <= 3 && s.initial_dist > 3) reward += 0.05 * (double)(3 - curr);
-    if (L.vis[L.at(s.pos_r, s.pos_c)] | L.gvis[L.at(s.pos_r, s.pos_c)]) {
+    if (L.vis[L.at(s.pos_r, s.pos_c)] | (cone_vis4(L, p.max_cams, p.max_guards, 0, s.pos_r, s.pos_c) & 1u)) {
       s.detected = 1;
       reward += p.r_detect;
       s.done = 1;
@@ -1051,13 +1049,13 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   }
   const int done_now = s.done;
   HEIST_STEP_STAMP(4);
-  const uint8_t* cones_plane = L.gvis;
+  int cset = 0;  // cached guard cones: this tick's
   if (auto_reset && done_now) {  // block-uniform: the barriers inside are safe
     // The reset keeps every heading (environment.py:204-208) and moves only the guards
     // back to patrol point 0, so the camera visibility stays and so does a guard's that
     // stands at its start already.  Cached guards: their reset cones were staged with this
-    // tick's and go to the reset plane (no barrier, no load); a live-raycast guard off its
-    // start forces a full second raycast (rare: guards that do not fit the cone cache).
+    // tick's (cone set 1, read by write_obs: no barrier, no load); a live-raycast guard off
+    // its start forces a full second raycast (rare: guards that do not fit the cone cache).
     const int moved = L.meta[5];  // set by the guard lanes before the raycast barrier
     reset_solver(p, s);
     if (live_guard) {
@@ -1085,13 +1083,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
       clear_vis<NT>(p, L);
       raycast_pass<NT, U, D>(p, e, smem, L, n_slot, mc);
     } else if (moved & 2) {
-      stamp_guard_cones<NT, true>(L, mc, n_slot);
-      cones_plane = L.gvis_r;
-      __syncthreads();
+      cset = 1;
     }
   }
   HEIST_STEP_STAMP(5);
-  if (p.probe_mode < 4) write_obs<NT>(p, e, s, L, cones_plane, obs);
+  if (p.probe_mode < 4) write_obs<NT>(p, e, s, L, cset, obs);
   HEIST_STEP_STAMP(6);
   if (t == 0) {
     rew[e] = (float)reward;
@@ -1138,7 +1134,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   }
   publish_emitters(L, E, n_slot);
   raycast_pass<NT, U, D>(p, e, smem, L, n_slot, mc);
-  write_obs<NT>(p, e, s, L, L.gvis, obs);
+  write_obs<NT>(p, e, s, L, 0, obs);
   if (t == 0) p.scal[e] = s;
 }
 

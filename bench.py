@@ -23,6 +23,11 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "rl-project-heist-architect-adversarial-reinforcement-learning-framework-cse4019_amd")
 sys.path[:0] = [ROOT, PKG]
+# MIOpen's find results and compiled kernels for the full-train secondaries' convolutions
+# (miopen_cache/, recorded by a bench run on MI355X): without them a fresh box spends
+# ~2 min per precision searching solvers before the first PPO update
+for _k, _v in (("MIOPEN_USER_DB_PATH", "miopen_cache"), ("MIOPEN_CUSTOM_CACHE_DIR", "miopen_cache")):
+    os.environ.setdefault(_k, os.path.join(ROOT, _v))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -711,8 +711,9 @@ __device__ __forceinline__ uint32_t cone_vis4(const EnvLds& L, int mc, int mg, i
 }
 
 // Visibility (visibility.py:31-65) once the emitter table (n_slot slots, guards from slot
-// mc on) is in LDS and vis is zeroed.
-template <int NT, int U, int D>
+// mc on) is in LDS and vis is zeroed.  CNT: 1 ray-sample / exact-ray counting compiled in
+// (the step kernel's counting variant), 0 not, -1 chosen at run time (reset).
+template <int NT, int U, int D, int CNT = -1>
 __device__ __forceinline__ void raycast_pass(const EnvParams& p, int e, unsigned char* smem, const EnvLds& L, int n_slot,
                                              int mc) {
   __syncthreads();  // emitter table, stop map and cleared vis in place
@@ -722,14 +723,14 @@ __device__ __forceinline__ void raycast_pass(const EnvParams& p, int e, unsigned
     if (E.kind == 1) L.vis[L.at(E.row, E.col)] = 1;
   }
   if (p.probe_mode != 1 && p.probe_mode != 5) {
-    if (p.sample_counter || p.redo_counter)
+    if (CNT == 1 || (CNT < 0 && (p.sample_counter || p.redo_counter)))
       cast_rays<NT, U, D, true>(smem, L, p.ray_mode, p.probe_mode, p.half_deg);
     else
       cast_rays<NT, U, D, false>(smem, L, p.ray_mode, p.probe_mode, p.half_deg);
   }
   __syncthreads();
-  if (p.sample_counter && t == 0) p.sample_counter[e] += (unsigned int)L.meta[2];
-  if (p.redo_counter && t == 0) p.redo_counter[e] += (unsigned int)L.meta[4];
+  if (CNT != 0 && p.sample_counter && t == 0) p.sample_counter[e] += (unsigned int)L.meta[2];
+  if (CNT != 0 && p.redo_counter && t == 0) p.redo_counter[e] += (unsigned int)L.meta[4];
 }
 
 // Zero the ray plane.
@@ -904,7 +905,9 @@ __device__ __forceinline__ double guard_heading_after(const EnvParams& p, int dr
       p.stamps[((size_t)e * W + (threadIdx.x >> 6)) * 10 + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
-template <int W, int U, int O, int D, bool STAMP>
+// COUNT: the counting variant (heist_count_samples / heist_count_redo armed), a kernel of
+// its own so profiles of the plain step are not mixed with it.
+template <int W, int U, int O, int D, bool STAMP, bool COUNT>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) void step_kernel(EnvParams p, const int64_t* __restrict__ actions,
                                                        float* __restrict__ obs, float* __restrict__ rew,
                                                        double* __restrict__ rew64, uint8_t* __restrict__ done_out,
@@ -1002,7 +1005,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   if (p.probe_mode == 9) return;  // profiling: everything before the raycast barrier
   HEIST_STEP_STAMP(2);
   // 3. visibility (environment.py:257-258); an already-done env recomputes the same plane
-  raycast_pass<NT, U, D>(p, e, smem, L, n_slot, mc);
+  raycast_pass<NT, U, D, COUNT ? 1 : 0>(p, e, smem, L, n_slot, mc);
   if (p.probe_mode == 7) return;  // profiling: everything up to the raycast
   HEIST_STEP_STAMP(3);
 
@@ -1081,7 +1084,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
       }
       publish_emitters(L, E2, n_slot);
       clear_vis<NT>(p, L);
-      raycast_pass<NT, U, D>(p, e, smem, L, n_slot, mc);
+      raycast_pass<NT, U, D, COUNT ? 1 : 0>(p, e, smem, L, n_slot, mc);
     } else if (moved & 2) {
       cset = 1;
     }
@@ -1564,10 +1567,9 @@ hipError_t launch_set_layout(const EnvParams& p, int max_walls, const int32_t* w
 }
 
 // (waves per env W, samples per ray chunk U, min waves per SIMD O, stop-map -> vis gap D)
-// variants; (4, 4, 1, D) is the default for either D.
+// variants; (2, 4, 8, D) is the default for either D.
 #define HEIST_ENV_VARIANTS(X) \
-  X(4, 4, 1, 1024) X(4, 4, 1, 6144) X(1, 4, 1, 1024) X(2, 4, 1, 1024) X(4, 2, 1, 1024) X(4, 4, 8, 1024) \
-  X(4, 4, 8, 6144) X(2, 4, 8, 1024) X(1, 4, 8, 1024) X(2, 4, 8, 6144)
+  X(2, 4, 8, 1024) X(2, 4, 8, 6144) X(4, 4, 8, 1024) X(4, 4, 8, 6144) X(1, 4, 8, 1024)
 
 int vis_gap_for(int R, int C) { return padded_bytes(R, C) <= 1024 ? 1024 : 6144; }
 
@@ -1597,11 +1599,14 @@ hipError_t launch_step(const EnvParams& p, const int64_t* actions, float* obs, f
 #define HEIST_STEP_CASE(W, U, O, D)                                                                       \
   if (p.step_waves == W && p.ray_chunk == U && p.step_occ == O && p.vis_gap == D) {                      \
     if (p.stamps)                                                                                        \
-      hipLaunchKernelGGL((step_kernel<W, U, O, D, true>), dim3(p.n_envs), dim3(64 * W), lds, st, p, actions, \
-                         obs, rew, rew64, done_out, status_out, auto_reset);                             \
+      hipLaunchKernelGGL((step_kernel<W, U, O, D, true, false>), dim3(p.n_envs), dim3(64 * W), lds, st, p, \
+                         actions, obs, rew, rew64, done_out, status_out, auto_reset);                    \
+    else if (p.sample_counter || p.redo_counter)                                                         \
+      hipLaunchKernelGGL((step_kernel<W, U, O, D, false, true>), dim3(p.n_envs), dim3(64 * W), lds, st, p, \
+                         actions, obs, rew, rew64, done_out, status_out, auto_reset);                    \
     else                                                                                                 \
-      hipLaunchKernelGGL((step_kernel<W, U, O, D, false>), dim3(p.n_envs), dim3(64 * W), lds, st, p, actions, \
-                         obs, rew, rew64, done_out, status_out, auto_reset);                             \
+      hipLaunchKernelGGL((step_kernel<W, U, O, D, false, false>), dim3(p.n_envs), dim3(64 * W), lds, st, p, \
+                         actions, obs, rew, rew64, done_out, status_out, auto_reset);                    \
     return hipGetLastError();                                                                            \
   }
   HEIST_ENV_VARIANTS(HEIST_STEP_CASE)

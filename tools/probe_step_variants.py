@@ -12,15 +12,11 @@ import torch  # noqa: E402
 from heist_amd import EnvironmentConfig, HeistEnv  # noqa: E402
 from heist_amd.layouts import valid_synthetic_layouts  # noqa: E402
 
-VARIANTS = {
-    "w4_u4_o1": {"HEIST_STEP_OCC": "1"},
-    "w4_u4_o8_exact": {"HEIST_EXACT_RAYS": "1"},
-    "w4_u4_o8": {"HEIST_STEP_OCC": "8"},
+VARIANTS = {  # the compiled variants (HEIST_ENV_VARIANTS in heist_env.hip)
     "w2_u4_o8": {"HEIST_STEP_WAVES": "2", "HEIST_STEP_OCC": "8"},
+    "w2_u4_o8_exact": {"HEIST_STEP_WAVES": "2", "HEIST_EXACT_RAYS": "1"},
+    "w4_u4_o8": {"HEIST_STEP_WAVES": "4", "HEIST_STEP_OCC": "8"},
     "w1_u4_o8": {"HEIST_STEP_WAVES": "1", "HEIST_STEP_OCC": "8"},
-    "w1_u4_o1": {"HEIST_STEP_WAVES": "1", "HEIST_STEP_OCC": "1"},
-    "w2_u4_o1": {"HEIST_STEP_WAVES": "2", "HEIST_STEP_OCC": "1"},
-    "w4_u2_o1": {"HEIST_RAY_CHUNK": "2", "HEIST_STEP_OCC": "1"},
 }
 
 

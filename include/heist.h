@@ -140,6 +140,13 @@ int heist_bfs_valid(const int32_t* grid, int n, int rows, int cols, int start_r,
 int heist_cones(int n, int rows, int cols, const uint8_t* walls, const int32_t* meta, const double* params,
                 uint8_t* tiles_out, heist_stream_t stream);
 
+/* The reference's LIST ORDER of the same cones (get_vision_cone_tiles / get_visible_tiles
+ * append a tile when a ray first reaches it, rays in index order, samples in distance
+ * order): keys_out [n][R][C] uint32 = (ray << 12 | sample) of the first visit on the exact
+ * fp64 path, 0xFFFFFFFF where no ray reaches the tile.  Same inputs as heist_cones. */
+int heist_cone_order(int n, int rows, int cols, const uint8_t* walls, const int32_t* meta, const double* params,
+                     uint32_t* keys_out, heist_stream_t stream);
+
 /* heist_cones with an explicit ray_mode (0 fast + exact re-cast, 1 exact only; see
  * heist_set_ray_mode).  heist_cones is ray_mode 0. */
 int heist_cones_mode(int n, int rows, int cols, const uint8_t* walls, const int32_t* meta, const double* params,

@@ -29,6 +29,8 @@ hipError_t launch_bfs(const int32_t* grid, int n, int R, int C, int sr, int sc, 
 int vis_gap_for(int R, int C);
 int stop_map_bytes(int R, int C);
 bool env_variant_exists(int W, int U, int O, int D);
+hipError_t launch_cone_order(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
+                             uint32_t* keys_out, hipStream_t st);
 hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
                         uint8_t* out, int ray_mode, hipStream_t st);
 hipError_t launch_fast_dir(const double* deg, int64_t n, float* co, float* so, hipStream_t st);
@@ -176,8 +178,17 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   }
   // 2 waves per env: 16 blocks resident per CU (LDS ~5 KB each) and half the redundant
   // block-uniform work of 4 waves; 23.0 us per 4096-env step vs 26.8 at 4 waves and 24.1
-  // at 1 (C2 Architect layouts with the guard cone cache, gpurun_out r02j)
-  p.step_waves = 2;
+  // at 1 (C2 Architect layouts with the guard cone cache, gpurun_out r02j).  A batch too
+  // small to give every SIMD 8 waves at 2 per env takes 4 per env instead (BASELINE C5:
+  // 2048 envs of 32 x 32, 22.7 -> 21.0 us per step; C4's 8192 envs: 2 waves, 44.5 vs
+  // 52.1 us; profiles/r02ae_configs.log)
+  {
+    int dev = 0, n_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n_cu = 256;
+    p.step_waves = 2 * (size_t)n_envs < 32 * (size_t)n_cu ? 4 : 2;
+  }
   p.ray_chunk = 4;  // tuning knobs; a combination without a compiled variant falls back to (2, 4, 8)
   // 8 waves per SIMD (64 VGPRs): 4096 envs are two full rounds of 8 workgroups per CU
   // (41.4 us per step vs 46.6 at the unbounded 85 VGPRs / 5 waves, profiles/r01m_*)
@@ -383,6 +394,16 @@ int heist_cones_mode(int n, int rows, int cols, const uint8_t* walls, const int3
   if (n <= 0) return 0;
   return check_hip(heist::launch_cones(n, rows, cols, walls, meta, params, tiles_out, ray_mode, (hipStream_t)stream),
                    "heist_cones_mode");
+}
+
+int heist_cone_order(int n, int rows, int cols, const uint8_t* walls, const int32_t* meta, const double* params,
+                     uint32_t* keys_out, heist_stream_t stream) {
+  HEIST_REQUIRE(walls && meta && params && keys_out, "heist_cone_order: null pointer");
+  HEIST_REQUIRE(rows >= 1 && cols >= 1 && rows <= heist::kMaxDim && cols <= heist::kMaxDim,
+                "heist_cone_order: need 1 <= rows, cols <= 64");
+  if (n <= 0) return 0;
+  return check_hip(heist::launch_cone_order(n, rows, cols, walls, meta, params, keys_out, (hipStream_t)stream),
+                   "heist_cone_order");
 }
 
 int heist_fast_dir(const double* angle_deg, int64_t n, float* cos_out, float* sin_out, heist_stream_t stream) {

@@ -104,7 +104,7 @@ struct EnvParams {
   int step_waves;             // wavefronts per env in step/reset (1, 2 or 4)
   int ray_chunk;              // samples per ray computed together (2, 4)
   int step_occ;               // min waves per SIMD the step kernel is compiled for (1, 8)
-  int vis_gap;                // LDS distance stop map -> vis plane (1024 or 6144), see heist_env.hip
+  int vis_gap;                // LDS distance stop map -> vis plane (1024, 2048 or 6144), see heist_env.hip
   unsigned long long* sample_counter;  // optional [n_envs]: ray samples evaluated per env, else null
   unsigned long long* redo_counter;    // optional [n_envs]: rays re-cast on the exact fp64 path, else null
   const double* half_deg;      // [2][kHalfDegN] glibc-exact sin, cos of m/2 degrees (m = -1440 .. 1439)

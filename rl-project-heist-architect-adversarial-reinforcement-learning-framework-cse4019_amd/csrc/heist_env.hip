@@ -67,7 +67,8 @@ struct EnvLds {
   uint32_t* rpos;  // [max_guards] patrol point 0 of each guard (row | col << 8), for the reset cones
   int PC;          // padded row stride C + 2G
   int off0;        // padded index of tile (0, 0): G * PC + G
-  __device__ __forceinline__ int at(int r, int c) const { return off0 + r * PC + c; }
+  // r >= 0 and PC < 2^24: one full-rate v_mad_u32_u24 (a 32-bit multiply is quarter rate)
+  __device__ __forceinline__ int at(int r, int c) const { return off0 + (int)__umul24((uint32_t)r, (uint32_t)PC) + c; }
 };
 
 // Width G of the stop ring around the grid: the longest fp32 fast-path ray (range
@@ -78,7 +79,7 @@ constexpr int kRing = 6;
 
 // The padded planes hold (R + 2G) x (C + 2G) bytes; D is the compile-time distance from
 // the stop map to the visibility plane (so one address serves both), 1024 for grids up to
-// 20 x 20 and 6144 for the 64 x 64 maximum.
+// 20 x 20, 2048 up to 33 x 33 and 6144 for the 64 x 64 maximum.
 __host__ __device__ inline int padded_bytes(int R, int C) { return (R + 2 * kRing) * (C + 2 * kRing); }
 
 __host__ __device__ inline size_t env_lds_bytes(int R, int C, int n_emit, int path_words, int D, int waves,
@@ -144,9 +145,12 @@ __device__ __forceinline__ int round_plus(double x) {
 // number of leading samples that may land on the emitter's own tile (see cast_rays).
 // Returns the index of the chunk's first sample that ends the ray (a wall or the grid
 // edge; with TAIL also sample `left`), U if none does.
-template <int U, int D, bool TAIL, int OWN>
+// KEY (heist_cone_order): instead of marking the tile, lower its u32 first-visit key
+// keys[address] to kbase + the 1-based sample index (LDS atomic min).
+template <int U, int D, bool TAIL, int OWN, bool KEY = false>
 __device__ __forceinline__ int sample_chunk(unsigned char* smem, int PC, int own, double col, double row,
-                                            double dxs, double dys, double kd, int left) {
+                                            double dxs, double dys, double kd, int left, uint32_t* keys = nullptr,
+                                            uint32_t kbase = 0) {
   int a[U], w[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -164,7 +168,11 @@ __device__ __forceinline__ int sample_chunk(unsigned char* smem, int PC, int own
     first = (!stop && st) ? u : first;
     stop |= st;
     const bool skip = stop || (u < OWN && a[u] == own);
-    smem[D + (skip ? 0 : a[u])] = 1;
+    if (KEY) {
+      if (!skip) atomicMin(&keys[a[u]], kbase + (uint32_t)kd + (uint32_t)u);
+    } else {
+      smem[D + (skip ? 0 : a[u])] = 1;
+    }
   }
   return first;
 }
@@ -173,24 +181,24 @@ __device__ __forceinline__ int sample_chunk(unsigned char* smem, int PC, int own
 // carries the own-tile test.  Returns the ray's sample count up to and including the
 // sample that ends it (n_samp if none does): the raycast's work figure, the same on the
 // fast path.
-template <int U, int D, int OWN>
+template <int U, int D, int OWN, bool KEY = false>
 __device__ __forceinline__ int march(unsigned char* smem, int PC, int own, double col, double row, double dxs,
-                                     double dys, int n_samp) {
+                                     double dys, int n_samp, uint32_t* keys = nullptr, uint32_t kbase = 0) {
   if (n_samp < U) {
-    const int f = sample_chunk<U, D, true, OWN>(smem, PC, own, col, row, dxs, dys, 1.0, n_samp);
+    const int f = sample_chunk<U, D, true, OWN, KEY>(smem, PC, own, col, row, dxs, dys, 1.0, n_samp, keys, kbase);
     return f + 1 < n_samp ? f + 1 : n_samp;
   }
-  int f = sample_chunk<U, D, false, OWN>(smem, PC, own, col, row, dxs, dys, 1.0, U);
+  int f = sample_chunk<U, D, false, OWN, KEY>(smem, PC, own, col, row, dxs, dys, 1.0, U, keys, kbase);
   if (f < U) return f + 1;
   double kd = 1.0 + U;
   int s0 = 1 + U;
   for (; s0 + U - 1 <= n_samp; s0 += U, kd += (double)U) {
-    f = sample_chunk<U, D, false, 0>(smem, PC, own, col, row, dxs, dys, kd, U);
+    f = sample_chunk<U, D, false, 0, KEY>(smem, PC, own, col, row, dxs, dys, kd, U, keys, kbase);
     if (f < U) return s0 + f;
   }
   if (s0 > n_samp) return n_samp;
   const int left = n_samp - s0 + 1;
-  f = sample_chunk<U, D, true, 0>(smem, PC, own, col, row, dxs, dys, kd, left);
+  f = sample_chunk<U, D, true, 0, KEY>(smem, PC, own, col, row, dxs, dys, kd, left, keys, kbase);
   return s0 - 1 + (f + 1 < left ? f + 1 : left);
 }
 
@@ -389,9 +397,9 @@ __device__ __forceinline__ int march_fast(uint32_t PC, uint32_t own, float dxs, 
 // A ray angle that is a whole number of half degrees (guards after an axis move; the
 // reference's default cameras: heading 0, fov 60, speed 15) reads the same glibc-exact
 // sin/cos from hd (computed by heist_trig::sincos at heist_create) instead of evaluating it.
-template <int U, int D>
+template <int U, int D, bool KEY = false>
 __device__ __forceinline__ int exact_ray(unsigned char* smem, const Emit& E, int i, int PC, int probe,
-                                         const double* hd) {
+                                         const double* hd, uint32_t* keys = nullptr) {
   const double angle = E.hmh + (E.fov * (double)i) / (double)E.num_rays;  // security.py:70
   double sn, cs;
   const double a2 = angle * 2.0;  // exact
@@ -411,8 +419,9 @@ __device__ __forceinline__ int exact_ray(unsigned char* smem, const Emit& E, int
   // dist = stride * s with stride a power of two, so dx * dist == (dx * stride) * s
   // bit for bit; dy = -sin (security.py:72-75).
   const double col = (double)E.col, row = (double)E.row;
-  if (E.kind == 0) return march<U, D, 2>(smem, PC, own, col, row, cs * 0.5, -sn * 0.5, n_samp);
-  return march<U, D, 0>(smem, PC, own, col, row, cs, -sn, n_samp);
+  const uint32_t kbase = (uint32_t)i << 12;  // first-visit key: (ray, sample) in ray-major order
+  if (E.kind == 0) return march<U, D, 2, KEY>(smem, PC, own, col, row, cs * 0.5, -sn * 0.5, n_samp, keys, kbase);
+  return march<U, D, 0, KEY>(smem, PC, own, col, row, cs, -sn, n_samp, keys, kbase);
 }
 
 // Wave-uniform values into scalar registers (every lane holds the same copy).
@@ -658,6 +667,27 @@ __device__ __forceinline__ size_t cone_entry(const EnvParams& p, int e, int g, i
   return ((((size_t)e * p.max_guards + g) * kConePath + idx) * kConeSlots + slot) * 16;
 }
 
+// One env's records as wave-uniform (SGPR) base pointers, so that per-lane accesses are a
+// 32-bit offset from a scalar base (saddr addressing) instead of 64-bit vector index math.
+struct EnvBase {
+  Cam* cams;
+  Guard* guards;
+  const uint16_t* paths;
+  const uint16_t* cones;
+};
+__device__ __forceinline__ EnvBase env_base(const EnvParams& p, int e) {
+  EnvBase b;
+  b.cams = p.cams + (size_t)e * p.max_cams;
+  b.guards = p.guards + (size_t)e * p.max_guards;
+  b.paths = p.paths + (size_t)e * p.max_guards * p.max_path;
+  b.cones = p.cones + (size_t)e * p.max_guards * (kConePath * kConeSlots * 16);
+  return b;
+}
+// u16 offset of guard g's cone entry (patrol index, slot) from EnvBase::cones
+__device__ __forceinline__ uint32_t cone_off(uint32_t g, uint32_t idx, uint32_t slot) {
+  return ((g * kConePath + idx) * kConeSlots + slot) * 16u;  // constant multipliers: shifts
+}
+
 // A cached guard's cone for its pose after this tick's move (move: the env acts and the
 // patrol has >= 2 points, security.py:147) into LDS cone[g]: the record's nslot names the
 // heading slot of the next patrol point, so the entry is known before the barrier.
@@ -705,7 +735,7 @@ __device__ __forceinline__ uint32_t cone_vis4(const EnvLds& L, int mc, int mg, i
     // bits dc .. dc + 3 of the row, dc = c0 - gc + 7 in [-4, 28) after the shift by 4
     const int sh = c0 - gc + kConeRange + 4;
     const uint32_t b = __builtin_amdgcn_ubfe(row << 4, (uint32_t)(sh < 0 ? 0 : (sh > 31 ? 31 : sh)), 4u);
-    v |= (b * 0x204081u) & 0x01010101u;  // bit j -> byte j
+    v |= __umul24(b, 0x204081u) & 0x01010101u;  // bit j -> byte j (24-bit multiply: full rate)
   }
   return v;
 }
@@ -762,7 +792,8 @@ __device__ __forceinline__ Guard as_guard(const EmitterRaw& r) { return __builti
 // max_cams + max_guards loads emitter slot t (camera t, then guard t - max_cams) whether or
 // not the env fills it, so no load waits for the EnvScalars (scalar loads) to arrive.
 template <int NT>
-__device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds& L, EmitterRaw& raw) {
+__device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvBase& eb, const EnvLds& L,
+                                         EmitterRaw& raw) {
   const int t = threadIdx.x;
   const int RC = p.RC;
   const uint8_t* src = p.grid + (size_t)e * RC;
@@ -782,8 +813,8 @@ __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvLds
   raw.a = make_uint4(0u, 0u, 0u, 0u);
   raw.b = raw.a;
   if (t < p.max_cams + p.max_guards) {
-    const uint4* rs = t < p.max_cams ? reinterpret_cast<const uint4*>(p.cams + (size_t)e * p.max_cams + t)
-                                     : reinterpret_cast<const uint4*>(p.guards + (size_t)e * p.max_guards + (t - p.max_cams));
+    const uint4* rs = t < p.max_cams ? reinterpret_cast<const uint4*>(eb.cams + (uint32_t)t)
+                                     : reinterpret_cast<const uint4*>(eb.guards + (uint32_t)(t - p.max_cams));
     raw.a = rs[0];
     raw.b = rs[1];
   }
@@ -924,8 +955,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     q[9] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
   }
   const EnvLds L = carve<D>(smem, p.R, p.C, p.max_cams + p.max_guards, 0, W, p.max_guards);
+  const EnvBase eb = env_base(p, e);
   EmitterRaw raw;
-  prefetch<NT>(p, e, L, raw);
+  prefetch<NT>(p, e, eb, L, raw);
   if (t == 0) L.meta[5] = 0;  // guards off their patrol start after this tick: bit 0 live, bit 1 cached
   EnvScalars s = p.scal[e];
   const int mc = p.max_cams, n_slot = p.max_cams + p.max_guards;  // emitter slots: cameras, then guards
@@ -949,7 +981,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     Cam cm = as_cam(raw);
     if (act) {
       cm.heading = py_mod360(cm.heading + cm.speed * 1.0);
-      p.cams[(size_t)e * p.max_cams + t].heading = cm.heading;
+      eb.cams[(uint32_t)t].heading = cm.heading;
     }
     E = cam_emit(cm);
   } else if (live_guard) {
@@ -964,11 +996,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     }
     // the next patrol point, the cone of the pose after the move and the cone an
     // auto-reset would give (patrol point 0, the same heading), loaded together
-    const uint16_t np = moves ? p.paths[((size_t)e * p.max_guards + g) * p.max_path + nidx] : gd.pos;
+    const uint16_t np = moves ? eb.paths[__umul24((uint32_t)g, (uint32_t)p.max_path) + (uint32_t)nidx] : gd.pos;
     if (gd.hslot != kUncached) {
       const int slot = moves ? gd.nslot : gd.hslot;
-      const uint4* src = reinterpret_cast<const uint4*>(p.cones + cone_entry(p, e, g, nidx, slot));
-      const uint4* rsrc = reinterpret_cast<const uint4*>(p.cones + cone_entry(p, e, g, 0, slot));
+      const uint4* src = reinterpret_cast<const uint4*>(eb.cones + cone_off(g, nidx, slot));
+      const uint4* rsrc = reinterpret_cast<const uint4*>(eb.cones + cone_off(g, 0, slot));
       const uint4 ca = src[0], cb = src[1], ra = rsrc[0], rb = rsrc[1];
       uint4* dst = reinterpret_cast<uint4*>(L.cone + 16 * g);
       uint4* rdst = reinterpret_cast<uint4*>(L.cone + 16 * (p.max_guards + g));
@@ -987,7 +1019,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
                                        gd.heading);
       gd.idx = (int16_t)nidx;
       gd.pos = np;
-      Guard* gp = p.guards + (size_t)e * p.max_guards + g;
+      Guard* gp = eb.guards + (uint32_t)g;
       gp->heading = gd.heading;
       gp->idx = gd.idx;
       gp->pos = gd.pos;
@@ -1022,22 +1054,28 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     }
   }
   if (act) {
-    // 4-5. shaping, detection, vault, timeout (environment.py:235, :261-297)
-    reward = p.r_step;
+    // 4-5. shaping, detection, vault, timeout (environment.py:235, :261-297).  The float64
+    // reward is only stored by thread 0, so only wave 0 evaluates it (a wave-uniform branch
+    // around each term); every wave needs the integer outcome (done, status) for the
+    // auto-reset and the observation.
+    const bool rw = (threadIdx.x >> 6) == 0;
     status = kRunning;
     const int curr = iabs_(s.pos_r - p.vr) + iabs_(s.pos_c - p.vc);
-    reward += (double)(s.prev_dist - curr) * 0.1;
+    if (rw) {
+      reward = p.r_step;
+      reward += (double)(s.prev_dist - curr) * 0.1;
+      if (curr <= 3 && s.initial_dist > 3) reward += 0.05 * (double)(3 - curr);
+    }
     s.prev_dist = curr;
-    if (curr <= 3 && s.initial_dist > 3) reward += 0.05 * (double)(3 - curr);
     if (L.vis[L.at(s.pos_r, s.pos_c)] | (cone_vis4(L, p.max_cams, p.max_guards, 0, s.pos_r, s.pos_c) & 1u)) {
       s.detected = 1;
-      reward += p.r_detect;
+      if (rw) reward += p.r_detect;
       s.done = 1;
       status = kDetected;
     }
     if (s.pos_r == p.vr && s.pos_c == p.vc) {
       s.vault_reached = 1;
-      reward += p.r_vault;
+      if (rw) reward += p.r_vault;
       s.done = 1;
       status = kVaultReached;
     }
@@ -1045,9 +1083,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     if (s.tick >= p.max_steps) {
       s.done = 1;
       status = kTimeout;
-      double frac = 1.0 - (double)curr / (double)(s.initial_dist > 1 ? s.initial_dist : 1);
-      if (frac < 0.0) frac = 0.0;
-      reward += frac * 2.0;
+      if (rw) {
+        double frac = 1.0 - (double)curr / (double)(s.initial_dist > 1 ? s.initial_dist : 1);
+        if (frac < 0.0) frac = 0.0;
+        reward += frac * 2.0;
+      }
     }
   }
   const int done_now = s.done;
@@ -1063,7 +1103,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     reset_solver(p, s);
     if (live_guard) {
       const int g = t - mc;
-      Guard* gp = p.guards + (size_t)e * p.max_guards + g;
+      Guard* gp = eb.guards + (uint32_t)g;
       gp->idx = 0;
       gp->pos = pos0;
       if (gslot != kUncached) gp->nslot = (uint8_t)L.cone[16 * (p.max_guards + g) + 15];  // succ of (0, slot)
@@ -1111,8 +1151,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   const int t = threadIdx.x;
   if (mask && !mask[e]) return;
   const EnvLds L = carve<D>(smem, p.R, p.C, p.max_cams + p.max_guards, 0, W, p.max_guards);
+  const EnvBase eb = env_base(p, e);
   EmitterRaw raw;
-  prefetch<NT>(p, e, L, raw);
+  prefetch<NT>(p, e, eb, L, raw);
   EnvScalars s = p.scal[e];
   const int mc = p.max_cams, n_slot = p.max_cams + p.max_guards;
   clear_vis<NT>(p, L);
@@ -1126,7 +1167,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     Guard gd = as_guard(raw);
     gd.idx = 0;
     gd.pos = gd.pos0;
-    Guard* gp = p.guards + (size_t)e * p.max_guards + (t - mc);
+    Guard* gp = eb.guards + (uint32_t)(t - mc);
     gp->idx = 0;
     gp->pos = gd.pos0;
     if (gd.hslot != kUncached) {  // heading kept (environment.py:204-208): cone of (0, hslot)
@@ -1438,6 +1479,47 @@ __global__ __launch_bounds__(64) void cones_kernel(int R, int C, const uint8_t* 
   }
 }
 
+// heist_cone_order: the reference's LIST order of a cone (security.py:53-101 appends a tile
+// when a ray first reaches it: rays in index order, samples in distance order).  One
+// emitter per block on the exact fp64 path; every reached tile keeps the smallest
+// (ray << 12 | sample) key (LDS atomic min), 0xFFFFFFFF where no ray reached it.  Sorting
+// the reached tiles by key gives get_vision_cone_tiles' order.
+template <int D>
+__global__ __launch_bounds__(64) void cone_order_kernel(int R, int C, const uint8_t* __restrict__ walls,
+                                                         const int32_t* __restrict__ meta,
+                                                         const double* __restrict__ params,
+                                                         uint32_t* __restrict__ keys_out) {
+  constexpr int U = 4;
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int e = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int RC = R * C;
+  const EnvLds L = carve<D>(smem, R, C, 1, 0, 1);
+  uint32_t* keys = reinterpret_cast<uint32_t*>(smem + env_lds_bytes(R, C, 1, 0, D, 1));  // [padded] u32
+  for (int i = lane; i < RC; i += 64) L.grid[i] = walls[(size_t)e * RC + i] ? kWall : kEmpty;
+  for (int i = lane; i < padded_bytes(R, C); i += 64) keys[i] = 0xFFFFFFFFu;
+  __syncthreads();
+  build_wall_map<64>(L.grid, L, R, C);
+  __syncthreads();
+  Emit E;
+  E.kind = meta[e * 4];
+  E.row = meta[e * 4 + 1];
+  E.col = meta[e * 4 + 2];
+  E.range = meta[e * 4 + 3];
+  E.fov = params[e * 2];
+  E.hmh = params[e * 2 + 1] - E.fov / 2.0;
+  E.num_rays = num_rays_for(E.fov);
+  E.step = E.fov / (double)E.num_rays;
+  E.first = 0;
+  E.members = 1;
+  for (int ray = lane; ray <= E.num_rays; ray += 64) exact_ray<U, D, true>(smem, E, ray, L.PC, 0, nullptr, keys);
+  __syncthreads();
+  for (int i = lane; i < RC; i += 64) {
+    const int r = i / C;
+    keys_out[(size_t)e * RC + i] = keys[L.at(r, i - r * C)];
+  }
+}
+
 __global__ void init_kernel(EnvParams p) {  // one thread per env
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= p.n_envs) return;
@@ -1552,6 +1634,8 @@ hipError_t launch_guard_cones(const EnvParams& p, const uint8_t* mask, hipStream
   const size_t lds = env_lds_bytes(p.R, p.C, 1, kConePath, p.vis_gap, 1);
   if (p.vis_gap == 1024)
     hipLaunchKernelGGL(guard_cone_kernel<1024>, dim3(p.n_envs, p.max_guards), dim3(64), lds, st, p, mask);
+  else if (p.vis_gap == 2048)
+    hipLaunchKernelGGL(guard_cone_kernel<2048>, dim3(p.n_envs, p.max_guards), dim3(64), lds, st, p, mask);
   else
     hipLaunchKernelGGL(guard_cone_kernel<6144>, dim3(p.n_envs, p.max_guards), dim3(64), lds, st, p, mask);
   return hipGetLastError();
@@ -1569,9 +1653,14 @@ hipError_t launch_set_layout(const EnvParams& p, int max_walls, const int32_t* w
 // (waves per env W, samples per ray chunk U, min waves per SIMD O, stop-map -> vis gap D)
 // variants; (2, 4, 8, D) is the default for either D.
 #define HEIST_ENV_VARIANTS(X) \
-  X(2, 4, 8, 1024) X(2, 4, 8, 6144) X(4, 4, 8, 1024) X(4, 4, 8, 6144) X(1, 4, 8, 1024)
+  X(2, 4, 8, 1024) X(2, 4, 8, 2048) X(2, 4, 8, 6144) X(4, 4, 8, 1024) X(4, 4, 8, 2048) X(4, 4, 8, 6144) \
+  X(1, 4, 8, 1024)
 
-int vis_gap_for(int R, int C) { return padded_bytes(R, C) <= 1024 ? 1024 : 6144; }
+// the plane gap D: 1024 up to 20 x 20, 2048 up to 33 x 33 (BASELINE C5's 32 x 32), 6144 up to 64 x 64
+int vis_gap_for(int R, int C) {
+  const int b = padded_bytes(R, C);
+  return b <= 1024 ? 1024 : (b <= 2048 ? 2048 : 6144);
+}
 
 bool env_variant_exists(int W, int U, int O, int D) {
 #define HEIST_HAS_CASE(W_, U_, O_, D_) \
@@ -1633,8 +1722,23 @@ hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t
   const size_t lds = env_lds_bytes(R, C, 1, 0, D, 1);
   if (D == 1024)
     hipLaunchKernelGGL(cones_kernel<1024>, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, out, ray_mode);
+  else if (D == 2048)
+    hipLaunchKernelGGL(cones_kernel<2048>, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, out, ray_mode);
   else
     hipLaunchKernelGGL(cones_kernel<6144>, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, out, ray_mode);
+  return hipGetLastError();
+}
+
+hipError_t launch_cone_order(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
+                             uint32_t* keys_out, hipStream_t st) {
+  const int D = vis_gap_for(R, C);
+  const size_t lds = env_lds_bytes(R, C, 1, 0, D, 1) + 4 * (size_t)padded_bytes(R, C);
+  if (D == 1024)
+    hipLaunchKernelGGL(cone_order_kernel<1024>, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, keys_out);
+  else if (D == 2048)
+    hipLaunchKernelGGL(cone_order_kernel<2048>, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, keys_out);
+  else
+    hipLaunchKernelGGL(cone_order_kernel<6144>, dim3(n), dim3(64), lds, st, R, C, walls, meta, params, keys_out);
   return hipGetLastError();
 }
 

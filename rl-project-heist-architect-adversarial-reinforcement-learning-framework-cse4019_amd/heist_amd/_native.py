@@ -40,6 +40,7 @@ SIGNATURES = {
     "heist_bfs_valid": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "heist_cones": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     "heist_cones_mode": (_i, [_i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp]),
+    "heist_cone_order": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     "heist_fast_dir": (_i, [_vp, _i64, _vp, _vp, _vp]),
     "heist_architect_decode": (_i, [_vp, _i, _i, _i, _vp, _i, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _vp]),

@@ -22,17 +22,21 @@ class Wall:  # security.py:16-23
 
 
 def _cone_tiles(kind, row, col, fov, heading, rng, grid_rows, grid_cols, walls) -> List[Tuple[int, int]]:
+    """The visible tiles in the reference's list order (first visit by ray index, then by
+    distance along the ray), from heist_cone_order's first-visit keys."""
     import torch
     from .. import _native as nat
     dev = nat.require_gpu()
     w = torch.as_tensor(np.ascontiguousarray(np.asarray(walls, dtype=np.uint8).reshape(1, grid_rows, grid_cols)), device=dev)
     meta = torch.tensor([[kind, row, col, rng]], dtype=torch.int32, device=dev)
     par = torch.tensor([[float(fov), float(heading)]], dtype=torch.float64, device=dev)
-    out = torch.empty((1, grid_rows, grid_cols), dtype=torch.uint8, device=dev)
-    nat.check(nat.lib().heist_cones(1, grid_rows, grid_cols, nat.ptr(w), nat.ptr(meta), nat.ptr(par), nat.ptr(out),
-                                    nat.stream(dev)), "heist_cones")
-    rr, cc = np.nonzero(out[0].cpu().numpy())
-    return [(int(r), int(c)) for r, c in zip(rr, cc)]
+    keys = torch.empty((1, grid_rows, grid_cols), dtype=torch.int32, device=dev)  # uint32 bits
+    nat.check(nat.lib().heist_cone_order(1, grid_rows, grid_cols, nat.ptr(w), nat.ptr(meta), nat.ptr(par),
+                                         nat.ptr(keys), nat.stream(dev)), "heist_cone_order")
+    k = keys[0].cpu().numpy().view(np.uint32).reshape(-1)
+    hit = np.nonzero(k != 0xFFFFFFFF)[0]
+    hit = hit[np.argsort(k[hit], kind="stable")]
+    return [(int(i // grid_cols), int(i % grid_cols)) for i in hit]
 
 
 @dataclass
@@ -48,7 +52,7 @@ class Camera:  # security.py:30-106
         self.heading = (self.heading + self.rotation_speed * tick) % 360.0
 
     def get_vision_cone_tiles(self, grid_rows: int, grid_cols: int, walls: np.ndarray) -> List[Tuple[int, int]]:
-        """Visible tiles (as a set; the reference returns them in ray order)."""
+        """Visible tiles in the reference's order (security.py:53-101)."""
         return _cone_tiles(0, self.row, self.col, self.fov_angle, self.heading, self.vision_range, grid_rows,
                            grid_cols, walls)
 

@@ -14,6 +14,8 @@ Fixture files (all numpy .npz, loaded with allow_pickle=False):
                   visibility bits, state tensors for the first ops.
   cones.npz       Camera.get_vision_cone_tiles / Guard.get_visible_tiles
                   sweeps (security.py:53-101, :161-192).
+  cone_order.npz  the same methods' LIST order (first visit by ray index, then
+                  distance) on 600 more cases: ordered flat tile indices.
   bfs.npz         bfs_path_exists on random grids (utils.py:52-85).
   ppo.npz         SolverAgent._compute_gae (agents/solver.py:228-244) and the
                   clipped-PPO loss + d(loss)/d(logits, values) of
@@ -322,6 +324,44 @@ def make_cones():
                         walls=np.concatenate([w for w, _ in walls_all]), tiles=np.concatenate([t for _, t in walls_all]))
 
 
+def make_cone_order():
+    """The LIST order of get_vision_cone_tiles / get_visible_tiles (first visit by ray, then
+    by distance): per case the ordered flat tile indices r * C + c."""
+    rng = np.random.default_rng(17)
+    rows, vis, walls, order, lens = [], [], [], [], []
+    for i in range(600):
+        R, C = [(20, 20), (32, 32), (10, 10), (13, 21)][i % 4]
+        dens = [0.0, 0.1, 0.25][i % 3]
+        wm = rng.random((R, C)) < dens
+        wm[0, :] = wm[-1, :] = wm[:, 0] = wm[:, -1] = True
+        r, c = int(rng.integers(1, R - 1)), int(rng.integers(1, C - 1))
+        wm[r, c] = False
+        kind = i % 3  # 0 camera f32 params, 1 camera integer params, 2 guard
+        if kind == 0:
+            fov, head = f32(rng.uniform(30, 120)), f32(rng.uniform(0, 360))
+            rngv = int(rng.choice([4, 6, 8]))
+        elif kind == 1:
+            fov = float(rng.choice([30, 45, 60, 75, 90, 120]))
+            head = float(rng.integers(0, 72) * 5)
+            rngv = int(rng.choice([4, 6]))
+        else:
+            fov = float(rng.choice([90.0, 60.0, 120.0]))
+            head = float(rng.choice([0.0, 90.0, 180.0, 270.0, 135.0]))
+            rngv = int(rng.choice([3, 4, 5]))
+        if kind < 2:
+            tiles = Camera(row=r, col=c, fov_angle=fov, heading=head, vision_range=rngv).get_vision_cone_tiles(R, C, wm)
+        else:
+            tiles = Guard(patrol_path=[(r, c)], vision_range=rngv, fov_angle=fov, heading=head).get_visible_tiles(R, C, wm)
+        rows.append((1 if kind == 2 else 0, R, C, r, c, rngv))
+        vis.append((fov, head))
+        walls.append(np.packbits(wm.reshape(-1)))
+        order.extend(tr * C + tc for tr, tc in tiles)
+        lens.append(len(tiles))
+    np.savez_compressed(os.path.join(OUT, "cone_order.npz"), meta=np.array(rows, np.int64),
+                        params=np.array(vis, np.float64), walls=np.concatenate(walls),
+                        order=np.array(order, np.int32), lens=np.array(lens, np.int32))
+
+
 def make_bfs():
     rng = np.random.default_rng(11)
     meta, grids, res = [], [], []
@@ -585,8 +625,8 @@ def make_arch_update():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["kat", "bfs", "cones", "ppo", "nets", "env", "arch"]
+    which = sys.argv[1:] or ["kat", "bfs", "cones", "ppo", "nets", "env", "arch", "order"]
     for w in which:
         print("==", w, flush=True)
         {"kat": make_kat, "bfs": make_bfs, "cones": make_cones, "ppo": make_ppo,
-         "nets": make_nets, "env": make_env_traces, "arch": make_arch_update}[w]()
+         "nets": make_nets, "env": make_env_traces, "arch": make_arch_update, "order": make_cone_order}[w]()

@@ -80,6 +80,20 @@ def cones():
                    heading=float(head), walls=walls, tiles=tiles)
 
 
+def cone_orders():
+    """cone_order.npz: per case the emitter, walls and the reference's ordered tile list."""
+    z = load("cone_order.npz")
+    wcur = ocur = 0
+    for (kind, R, C, r, c, rng), (fov, head), n in zip(z["meta"], z["params"], z["lens"]):
+        nb = (int(R) * int(C) + 7) // 8
+        walls = np.unpackbits(z["walls"][wcur:wcur + nb])[:R * C].reshape(R, C).astype(bool)
+        wcur += nb
+        order = [(int(i) // int(C), int(i) % int(C)) for i in z["order"][ocur:ocur + int(n)]]
+        ocur += int(n)
+        yield dict(kind=int(kind), R=int(R), C=int(C), row=int(r), col=int(c), range=int(rng), fov=float(fov),
+                   heading=float(head), walls=walls, order=order)
+
+
 def bfs_cases():
     z = load("bfs.npz")
     cur = 0

@@ -83,6 +83,41 @@ def test_cones_bit_exact(gpu_device):
     assert n >= 1000
 
 
+def test_cone_order_matches_reference_list(gpu_device):
+    """heist_cone_order first-visit keys give get_vision_cone_tiles / get_visible_tiles'
+    list order (security.py:53-101, :161-192) on 600 reference-generated cases, through
+    the component classes (batched ABI call for each grid size, then the class methods)."""
+    from heist_amd import _native as nat
+    from heist_amd.components.security import Camera, Guard
+    groups = {}
+    for c in gd.cone_orders():
+        groups.setdefault((c["R"], c["C"]), []).append(c)
+    n = 0
+    for (R, C), cs in groups.items():
+        walls = torch.tensor(np.stack([c["walls"] for c in cs]).astype(np.uint8), device=gpu_device)
+        meta = torch.tensor([[c["kind"], c["row"], c["col"], c["range"]] for c in cs], dtype=torch.int32,
+                            device=gpu_device)
+        par = torch.tensor([[c["fov"], c["heading"]] for c in cs], dtype=torch.float64, device=gpu_device)
+        keys = torch.empty((len(cs), R, C), dtype=torch.int32, device=gpu_device)
+        nat.check(nat.lib().heist_cone_order(len(cs), R, C, nat.ptr(walls), nat.ptr(meta), nat.ptr(par),
+                                             nat.ptr(keys), nat.stream(gpu_device)), "heist_cone_order")
+        k = keys.cpu().numpy().view(np.uint32).reshape(len(cs), -1)
+        for i, c in enumerate(cs):
+            hit = np.nonzero(k[i] != 0xFFFFFFFF)[0]
+            got = [(int(j) // C, int(j) % C) for j in hit[np.argsort(k[i][hit], kind="stable")]]
+            assert got == c["order"], (c["kind"], c["fov"], c["heading"])
+            n += 1
+    assert n == 600
+    for c in list(gd.cone_orders())[:30]:  # the class methods return the same lists
+        if c["kind"] == 0:
+            got = Camera(row=c["row"], col=c["col"], fov_angle=c["fov"], heading=c["heading"],
+                         vision_range=c["range"]).get_vision_cone_tiles(c["R"], c["C"], c["walls"])
+        else:
+            got = Guard(patrol_path=[(c["row"], c["col"])], vision_range=c["range"], fov_angle=c["fov"],
+                        heading=c["heading"]).get_visible_tiles(c["R"], c["C"], c["walls"])
+        assert got == c["order"]
+
+
 def test_bfs_bit_exact(gpu_device):
     from heist_amd.utils import bfs_valid_batch
     groups = {}

@@ -59,6 +59,21 @@ def test_cones_bit_exact():
     assert n >= 1000
 
 
+def test_cone_order_fixture_sets_match_oracle():
+    """cone_order.npz's ordered lists hold exactly the oracle's visible tiles, each once
+    (the order itself is pinned on the GPU by test_cone_order_matches_reference_list)."""
+    n = 0
+    for c in gd.cone_orders():
+        got = po.cone(c["kind"], c["walls"], c["row"], c["col"], c["fov"], c["heading"], c["range"])
+        assert len(set(c["order"])) == len(c["order"])
+        want = np.zeros((c["R"], c["C"]), bool)
+        for r, cc in c["order"]:
+            want[r, cc] = True
+        np.testing.assert_array_equal(got, want)
+        n += 1
+    assert n == 600
+
+
 def test_bfs_matches_reference():
     n = 0
     for c in gd.bfs_cases():

@@ -223,8 +223,8 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
       sizeof(int32_t) * n,
       sizeof(double) * 3 * heist::kHalfDegN,  // [sin | cos | staging radians]
       (size_t)heist::stop_map_bytes(R, C) * n,
-      // guard cone cache: 32 B per (guard, patrol index, heading slot)
-      (size_t)32 * n * (max_guards > 0 ? max_guards : 1) * heist::kConePath * heist::kConeSlots,
+      // guard cone cache: 64 B per (guard, patrol index, heading slot)
+      sizeof(uint16_t) * heist::kConeEntry * n * (max_guards > 0 ? max_guards : 1) * heist::kConePath * heist::kConeSlots,
   };
   h->n_allocs = 0;
   for (size_t k = 0; k < sizeof(sizes) / sizeof(sizes[0]); ++k) {

@@ -8,7 +8,7 @@
 //   Cam        [N][max_cams]       32 B  fov, heading, speed (f64), row, col, range, num_rays
 //   Guard      [N][max_guards]     32 B  fov, heading (f64), idx, speed, len, range, num_rays
 //   paths      [N][max_guards][max_path] u16 (row | col << 8)
-//   cones      [N][max_guards][kConePath][kConeSlots] 32 B  each guard's vision cone at
+//   cones      [N][max_guards][kConePath][kConeSlots] 64 B  each guard's vision cone at
 //              every (patrol index, heading slot), built once per layout (guard_cone_kernel)
 // Per-handle constant tables: guard heading by (dr, dc) (host libm atan2), the two
 // static position-channel planes, the tile->float LUT.
@@ -32,9 +32,12 @@ constexpr int kHalfDegN = 2880;      // half-degree sin/cos table: angles -720 .
 // most len x (len + 1) cones.  Guards with a patrol of at most kConePath points, at most
 // kConeSlots distinct headings and a vision range of at most kConeRange get every cone
 // precomputed at set_layout; the tick ORs a 32-byte window instead of casting 181 rays.
-// Cone entry: 16 rows of u16, rows 0..14 = tiles (dr, dc) in [-7, 7]^2 around the guard
-// (bit dc + 7 of row dr + 7, the guard's own tile included), row 15 = the heading slot
-// after the next move from this state.
+// Cone entry (64 B, kConeEntry u16): 16 rows of u16, rows 0..14 = tiles (dr, dc) in
+// [-7, 7]^2 around the guard (bit dc + 7 of row dr + 7, the guard's own tile included), row
+// 15 = the heading slot after the next move from this state; then the pose the entry
+// describes, so a tick that moves a cached guard reads its new pose with its cone in one
+// load: u16 16..19 = the slot's heading (fp64 bits), u16 20 = the patrol point (r | c << 8).
+constexpr int kConeEntry = 32;
 constexpr int kConePath = 16;
 constexpr int kConeSlots = 8;
 constexpr int kConeRange = 7;
@@ -93,7 +96,7 @@ struct EnvParams {
   Cam* cams;
   Guard* guards;
   uint16_t* paths;
-  uint16_t* cones;            // [n_envs][max_guards][kConePath][kConeSlots][16] guard cone cache
+  uint16_t* cones;            // [n_envs][max_guards][kConePath][kConeSlots][kConeEntry] guard cone cache
   int guard_cones;            // 1: heist_set_layout builds the cone cache (default); 0: guards raycast live
   const double* heading_tab;  // [(2R-1)*(2C-1)]
   const float* plane0;        // [RC] position channel without the solver

@@ -664,7 +664,7 @@ __device__ __forceinline__ Emit guard_emit(const Guard& gd) {
 
 // Element offset (in u16) of the cone entry of guard g of env e at (patrol index, slot).
 __device__ __forceinline__ size_t cone_entry(const EnvParams& p, int e, int g, int idx, int slot) {
-  return ((((size_t)e * p.max_guards + g) * kConePath + idx) * kConeSlots + slot) * 16;
+  return ((((size_t)e * p.max_guards + g) * kConePath + idx) * kConeSlots + slot) * kConeEntry;
 }
 
 // One env's records as wave-uniform (SGPR) base pointers, so that per-lane accesses are a
@@ -680,12 +680,12 @@ __device__ __forceinline__ EnvBase env_base(const EnvParams& p, int e) {
   b.cams = p.cams + (size_t)e * p.max_cams;
   b.guards = p.guards + (size_t)e * p.max_guards;
   b.paths = p.paths + (size_t)e * p.max_guards * p.max_path;
-  b.cones = p.cones + (size_t)e * p.max_guards * (kConePath * kConeSlots * 16);
+  b.cones = p.cones + (size_t)e * p.max_guards * (kConePath * kConeSlots * kConeEntry);
   return b;
 }
 // u16 offset of guard g's cone entry (patrol index, slot) from EnvBase::cones
 __device__ __forceinline__ uint32_t cone_off(uint32_t g, uint32_t idx, uint32_t slot) {
-  return ((g * kConePath + idx) * kConeSlots + slot) * 16u;  // constant multipliers: shifts
+  return ((g * kConePath + idx) * kConeSlots + slot) * (uint32_t)kConeEntry;  // constant multipliers: shifts
 }
 
 // A cached guard's cone for its pose after this tick's move (move: the env acts and the
@@ -994,14 +994,21 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
       nidx += gd.step;
       if (nidx >= gd.len) nidx -= gd.len;
     }
-    // the next patrol point, the cone of the pose after the move and the cone an
-    // auto-reset would give (patrol point 0, the same heading), loaded together
-    const uint16_t np = moves ? eb.paths[__umul24((uint32_t)g, (uint32_t)p.max_path) + (uint32_t)nidx] : gd.pos;
-    if (gd.hslot != kUncached) {
+    // a cached guard: the cone entry of the pose after the move (which names that pose: patrol
+    // point and heading) and the cone an auto-reset would give (patrol point 0, the same
+    // heading), loaded together straight from the record; a live-raycast guard: the next
+    // patrol point, then its heading from the (dr, dc) table
+    const bool cached = gd.hslot != kUncached;
+    uint16_t np = gd.pos;
+    if (moves && !cached) np = eb.paths[__umul24((uint32_t)g, (uint32_t)p.max_path) + (uint32_t)nidx];
+    uint4 cm = make_uint4(0u, 0u, 0u, 0u);
+    if (cached) {
       const int slot = moves ? gd.nslot : gd.hslot;
       const uint4* src = reinterpret_cast<const uint4*>(eb.cones + cone_off(g, nidx, slot));
       const uint4* rsrc = reinterpret_cast<const uint4*>(eb.cones + cone_off(g, 0, slot));
       const uint4 ca = src[0], cb = src[1], ra = rsrc[0], rb = rsrc[1];
+      cm = src[2];
+      if (moves) np = (uint16_t)(cm.z & 0xffffu);
       uint4* dst = reinterpret_cast<uint4*>(L.cone + 16 * g);
       uint4* rdst = reinterpret_cast<uint4*>(L.cone + 16 * (p.max_guards + g));
       dst[0] = ca;
@@ -1015,8 +1022,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
       }
     }
     if (moves) {
-      gd.heading = guard_heading_after(p, unpack_r(np) - unpack_r(gd.pos), unpack_c(np) - unpack_c(gd.pos),
-                                       gd.heading);
+      gd.heading = cached ? __builtin_bit_cast(double, ((uint64_t)cm.y << 32) | cm.x)
+                          : guard_heading_after(p, unpack_r(np) - unpack_r(gd.pos), unpack_c(np) - unpack_c(gd.pos),
+                                                gd.heading);
       gd.idx = (int16_t)nidx;
       gd.pos = np;
       Guard* gp = eb.guards + (uint32_t)g;
@@ -1405,9 +1413,12 @@ __global__ __launch_bounds__(64) void guard_cone_kernel(EnvParams p, const uint8
     E.members = 1;
     for (int ray = lane; ray <= E.num_rays; ray += 64) exact_ray<U, D>(smem, E, ray, L.PC, 0, p.half_deg);
     __syncthreads();
-    if (lane < 16) {
+    if (lane < kConeEntry) {
       uint32_t bits = 0;
-      if (lane < 2 * kConeRange + 1) {
+      if (lane >= 16) {  // the pose the entry names: heading of slot h, patrol point i
+        const uint64_t hb = __builtin_bit_cast(uint64_t, heads[h]);
+        bits = lane < 20 ? (uint32_t)(hb >> (16 * (lane - 16))) & 0xffffu : (lane == 20 ? (uint32_t)L.path[i] : 0u);
+      } else if (lane < 2 * kConeRange + 1) {
         const int rr = E.row + lane - kConeRange;
         if ((unsigned)rr < (unsigned)R)
           for (int j = 0; j < 2 * kConeRange + 1; ++j) {

@@ -3,8 +3,8 @@
 // HBM layout (all [env]-major, one env is handled by one 64-lane wavefront):
 //   EnvScalars [N]                 48 B  solver state + layout counters
 //   grid       [N][R*C]            u8    tile types (utils.py:31-37), static per layout
-//   stop       [N][stop_bytes]     u8    the raycast's padded stop map (1 = wall or outside),
-//                                        static per layout, copied to LDS by step/reset
+//   stop       [N][stop_bytes]     u8    the raycast's padded stop map, 1 bit per cell (1 = wall or outside),
+//                                        static per layout, expanded into LDS by step/reset
 //   Cam        [N][max_cams]       32 B  fov, heading, speed (f64), row, col, range, num_rays
 //   Guard      [N][max_guards]     32 B  fov, heading (f64), idx, speed, len, range, num_rays
 //   paths      [N][max_guards][max_path] u16 (row | col << 8)
@@ -92,7 +92,7 @@ struct EnvParams {
   EnvScalars* scal;
   uint8_t* grid;
   uint8_t* stop;              // [n_envs][stop_bytes] padded stop maps (set_layout_kernel)
-  int stop_bytes;             // per env: (R + 2*kRing)(C + 2*kRing) rounded up to 16
+  int stop_bytes;             // per env: (R + 2*kRing)(C + 2*kRing) / 8 rounded up to 16 (bit-packed)
   Cam* cams;
   Guard* guards;
   uint16_t* paths;

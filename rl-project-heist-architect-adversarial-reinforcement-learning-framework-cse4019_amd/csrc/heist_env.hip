@@ -791,6 +791,15 @@ __device__ __forceinline__ Guard as_guard(const EmitterRaw& r) { return __builti
 // pass of NT threads cannot (W < 4, grids above 32 x 32, long patrol paths).  Thread t <
 // max_cams + max_guards loads emitter slot t (camera t, then guard t - max_cams) whether or
 // not the env fills it, so no load waits for the EnvScalars (scalar loads) to arrive.
+// Packed stop-map byte j (bits = padded cells 8 j .. 8 j + 7) -> 8 bytes of the LDS wall
+// plane: (x * 0x204081) & 0x01010101 spreads 4 bits to bit 0 of 4 bytes (no carries).
+__device__ __forceinline__ void expand_stop(uint8_t* wall, int j, uint32_t b) {
+  uint2 v;
+  v.x = __umul24(b & 15u, 0x204081u) & 0x01010101u;
+  v.y = __umul24((b >> 4) & 15u, 0x204081u) & 0x01010101u;
+  *reinterpret_cast<uint2*>(wall + 8 * j) = v;
+}
+
 template <int NT>
 __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvBase& eb, const EnvLds& L,
                                          EmitterRaw& raw) {
@@ -804,11 +813,10 @@ __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvBas
 
   uint32_t gv = 0u;
   if (t < n4) gv = s4[t];
-  // the layout's padded stop map, built once by set_layout_kernel
-  const float4* ss = reinterpret_cast<const float4*>(p.stop + (size_t)e * p.stop_bytes);
-  float4* sd = reinterpret_cast<float4*>(L.wall);
-  const int n_stop = p.stop_bytes / 16;
-  float4 sv = make_float4(0.f, 0.f, 0.f, 0.f);
+  // the layout's padded stop map, built once by set_layout_kernel (bit-packed)
+  const uint8_t* ss = p.stop + (size_t)e * p.stop_bytes;
+  const int n_stop = p.stop_bytes;
+  uint32_t sv = 0u;
   if (t < n_stop) sv = ss[t];
   raw.a = make_uint4(0u, 0u, 0u, 0u);
   raw.b = raw.a;
@@ -819,8 +827,8 @@ __device__ __forceinline__ void prefetch(const EnvParams& p, int e, const EnvBas
     raw.b = rs[1];
   }
   if (t < n4) d4[t] = gv;
-  if (t < n_stop) sd[t] = sv;
-  for (int i = t + NT; i < n_stop; i += NT) sd[i] = ss[i];
+  if (t < n_stop) expand_stop(L.wall, t, sv);
+  for (int i = t + NT; i < n_stop; i += NT) expand_stop(L.wall, i, ss[i]);
   for (int i = t + NT; i < n4; i += NT) {
     d4[i] = s4[i];
   }
@@ -1195,20 +1203,28 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
 // ---------------------------------------------------------------------------
 
 // The padded stop map of tile grid g (1 = wall or outside the grid; the layout of
-// EnvLds::wall) into p.stop for env e, by threads lane, lane + stride, ...  Built once per
-// layout; step and reset copy it into LDS with the rest of the prefetch.
+// EnvLds::wall) into p.stop for env e, bit-packed (bit k of byte j = padded cell 8 j + k),
+// by threads lane, lane + stride, ...  Built once per layout; step and reset expand it into
+// the LDS byte plane with the rest of the prefetch (expand_stop), 1 bit of HBM per cell.
 __device__ __forceinline__ void write_stop_map(const EnvParams& p, int e, const uint8_t* g, int lane, int stride) {
   const int R = p.R, C = p.C, PC = C + 2 * kRing, nb = (R + 2 * kRing) * PC;
   uint8_t* stp = p.stop + (size_t)e * p.stop_bytes;
-  for (int i = lane; i < p.stop_bytes; i += stride) {
-    const int pr = i / PC;
-    const int r = pr - kRing, c = i - pr * PC - kRing;
-    const bool out = i >= nb || (unsigned)r >= (unsigned)R || (unsigned)c >= (unsigned)C;
-    stp[i] = out ? 1 : (g[r * C + c] == kWall ? 1 : 0);
+  for (int j = lane; j < p.stop_bytes; j += stride) {
+    uint32_t bits = 0;
+    for (int k = 0; k < 8; ++k) {
+      const int i = 8 * j + k;
+      const int pr = i / PC;
+      const int r = pr - kRing, c = i - pr * PC - kRing;
+      const bool out = i >= nb || (unsigned)r >= (unsigned)R || (unsigned)c >= (unsigned)C;
+      if (out || g[r * C + c] == kWall) bits |= 1u << k;
+    }
+    stp[j] = (uint8_t)bits;
   }
 }
 
-int stop_map_bytes(int R, int C) { return (int)align16((size_t)padded_bytes(R, C)); }
+// Packed stop map bytes per env: 16-aligned, so its expansion (8 x) ends inside the LDS
+// wall plane for every D (a multiple of 128 >= padded_bytes).
+int stop_map_bytes(int R, int C) { return (int)align16((size_t)(padded_bytes(R, C) + 7) / 8); }
 
 // 4-neighbour reachability start -> goal over non-wall tiles (utils.py:52-85) as a
 // wave-level bitboard flood fill: lane r holds row r as a 64-bit mask.
@@ -1362,9 +1378,8 @@ __global__ __launch_bounds__(64) void guard_cone_kernel(EnvParams p, const uint8
   if (!p.guard_cones || len < 1 || len > kConePath || gd.range < 0 || gd.range > kConeRange) return;
   const int R = p.R, C = p.C;
   const EnvLds L = carve<D>(smem, R, C, 1, kConePath, 1);
-  const uint4* ss = reinterpret_cast<const uint4*>(p.stop + (size_t)e * p.stop_bytes);
-  uint4* sd = reinterpret_cast<uint4*>(L.wall);
-  for (int i = lane; i < p.stop_bytes / 16; i += 64) sd[i] = ss[i];
+  const uint8_t* ss = p.stop + (size_t)e * p.stop_bytes;
+  for (int i = lane; i < p.stop_bytes; i += 64) expand_stop(L.wall, i, ss[i]);
   if (lane < len) L.path[lane] = p.paths[((size_t)e * p.max_guards + g) * p.max_path + lane];
   __syncthreads();
   if (lane == 0) {

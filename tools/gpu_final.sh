@@ -1,5 +1,6 @@
 #!/bin/bash
-# Final round-1 GPU session: GPU parity suite, smoke, default bench, rocprof kernel stats, PMC traffic passes.
+# Final GPU session of a round: GPU parity suite, smoke, default bench, rocprof kernel stats,
+# PMC traffic passes, per-probe-mode SQ instruction mix, phase stamps.
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
 OUT=gpurun_out/${TAG:-r01z}
 mkdir -p $OUT
@@ -12,5 +13,7 @@ run prof 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o heist --output-for
 run pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary
 run pmc_write 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary
 run sstamp 300 python tools/probe_step_stamps.py
+run pmc_modes 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS -d $OUT/pmc_modes -o modes --output-format csv -- python3 tools/probe_step_modes.py
+python tools/pmc_modes.py $OUT/pmc_modes/modes_counter_collection.csv $OUT/pmc_modes.json > /dev/null
 run bench 900 python bench.py
 echo "== all done"

@@ -113,6 +113,7 @@ struct EnvParams {
   const double* half_deg;      // [2][kHalfDegN] glibc-exact sin, cos of m/2 degrees (m = -1440 .. 1439)
   int32_t* order;              // [n_envs] env of step/reset block b: heaviest raycast first (order_kernel)
   unsigned long long* stamps;          // optional [n_envs][waves][8]: step-kernel phase stamps (s_memtime), else null
+  int obs_store;              // observation stores: 0 plain, 1 write-through (sc1), 2 nt, 3 sc1 nt (HEIST_OBS_STORE)
   int ray_mode;               // 0: fp32 fast path with exact fp64 re-cast of near-tie rays; 1: exact fp64 only
   int probe_mode;             // profiling only (HEIST_PROBE_MODE): 0 normal, 1 no rays, 2 angles+sin/cos only,
                               // 3 marches with a fixed direction (no sin/cos), 4 no observation write,

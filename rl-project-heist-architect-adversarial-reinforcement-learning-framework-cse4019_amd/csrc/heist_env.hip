@@ -848,6 +848,21 @@ __device__ __forceinline__ void patch4(float4& v, int m, float val) {
   else if (m == 3) v.w = val;
 }
 
+// One 16-byte observation store at byte offset `off` of the env's row (buffer descriptor rs)
+// with the handle's cache policy (EnvParams::obs_store, default 2 = nt).  The 20 MB of
+// observations per 4096-env step are the launch's largest write; plain stores leave them
+// dirty in L2 for the kernel boundary to write back (MI355X_MICROARCH.md, boundary row:
+// + dirty bytes / 6 TB/s per dependent launch).  Measured per 4096-env step (C2 layouts,
+// profiles/r02ba_probe_obs_store.log): plain 16.66 us, sc1 16.22, nt 15.44, sc1 nt 16.10.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void obs_put(__amdgpu_buffer_rsrc_t rs, int pol, int off, float4 v) {
+  const u32x4_t u = __builtin_bit_cast(u32x4_t, v);
+  if (pol == 1) __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, 16);       // sc1
+  else if (pol == 2) __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, 2);   // nt
+  else if (pol == 3) __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, 18);  // sc1 nt
+  else __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, 0);
+}
+
 // Observation row [3][R][C] (environment.py:347-374): occupancy / 5, visibility (ray
 // plane | cached guard cones of cone set `cset`, cone_vis4), and the position channel
 // (static plane with the solver and vault cells patched; the vault wins if the solver
@@ -865,9 +880,8 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
   static_assert((kRing & 1) == 0, "padded vis rows of a C % 4 == 0 grid are 2-byte aligned");
   if ((C & 3) == 0) {  // a float4 never crosses a row; 4 vis bytes in two aligned u16 reads
     const int n4 = RC / 4, c4 = C / 4;
-    float4* o0 = reinterpret_cast<float4*>(o);
-    float4* o1 = o0 + n4;
-    float4* o2 = o1 + n4;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(o, (short)0, 12 * RC, 0x00020000);
+    const int pol = p.obs_store;
     // the first half of the block writes channels 0 and 2, the second half channel 1
     constexpr int H = NT / 2;
     if (t < H) {
@@ -876,12 +890,13 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
         const uint32_t b = *reinterpret_cast<const uint32_t*>(L.grid + 4 * q);
         // float32(tile) / 5 == float32(tile) * 0.2f for every tile type 0..7 (checked), and the
         // byte -> float conversion is one v_cvt_f32_ubyteN
-        o0[q] = make_float4((float)(b & 0xff) * 0.2f, (float)((b >> 8) & 0xff) * 0.2f,
-                            (float)((b >> 16) & 0xff) * 0.2f, (float)(b >> 24) * 0.2f);
+        obs_put(rs, pol, 16 * q,
+                make_float4((float)(b & 0xff) * 0.2f, (float)((b >> 8) & 0xff) * 0.2f,
+                            (float)((b >> 16) & 0xff) * 0.2f, (float)(b >> 24) * 0.2f));
         float4 v = reinterpret_cast<const float4*>(p.plane0)[q];  // the handle's static plane (L2-resident)
         if (q == qs) patch4(v, solver & 3, sv);          // only the solver's and the vault's
         if (q == qv) patch4(v, vault & 3, p.vault_val);  // float4 take these branches
-        o2[q] = v;
+        obs_put(rs, pol, 16 * (2 * n4 + q), v);
       }
     } else {
       for (int q = t - H; q < n4; q += H) {
@@ -896,7 +911,8 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
         }
         v |= cone_vis4(L, mc, mg, cset, r, c0);
         // visibility bytes are 0 or 1, so they convert directly
-        o1[q] = make_float4((float)(v & 0xff), (float)((v >> 8) & 0xff), (float)((v >> 16) & 0xff), (float)(v >> 24));
+        obs_put(rs, pol, 16 * (n4 + q),
+                make_float4((float)(v & 0xff), (float)((v >> 8) & 0xff), (float)((v >> 16) & 0xff), (float)(v >> 24)));
       }
     }
   } else {

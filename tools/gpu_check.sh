@@ -41,6 +41,7 @@ for s in ${STEPS:-pytest smoke bench prof}; do
     mprobesyn) PROBE_LAYOUTS=synthetic step probe_modes_syn 600 python tools/probe_step_modes.py ;;
     uprobe) step probe_update 600 python tools/probe_update.py ;;
     mprobe) step probe_modes 600 python tools/probe_step_modes.py ;;
+    oprobe) step probe_obs_store 300 python tools/probe_obs_store.py ;;
     vprobe) step probe_variants 600 python tools/probe_step_variants.py ;;
     envtest) step pytest_env 900 python -u -m pytest tests/test_gpu_env.py -x -q --timeout 200 --timeout-method thread ;;
     quick) step bench_quick 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary ;;

@@ -42,6 +42,7 @@ for s in ${STEPS:-pytest smoke bench prof}; do
     uprobe) step probe_update 600 python tools/probe_update.py ;;
     mprobe) step probe_modes 600 python tools/probe_step_modes.py ;;
     oprobe) step probe_obs_store 300 python tools/probe_obs_store.py ;;
+    dprobe) PROBE_VAR=HEIST_DISPATCH_ORDER PROBE_POLICIES=0,1 step probe_dispatch_order 300 python tools/probe_obs_store.py ;;
     vprobe) step probe_variants 600 python tools/probe_step_variants.py ;;
     envtest) step pytest_env 900 python -u -m pytest tests/test_gpu_env.py -x -q --timeout 200 --timeout-method thread ;;
     quick) step bench_quick 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary ;;
@@ -51,6 +52,7 @@ for s in ${STEPS:-pytest smoke bench prof}; do
             i=$((i+1)); PROBE_N=4096 step pmc_policy$i 600 rocprofv3 --pmc $grp --kernel-include-regex solver_conv -d "$OUT/pp$i" -o pol --output-format csv -- python3 tools/probe_policy.py
             python tools/pmc_summary.py "$OUT/pp$i/pol_counter_collection.csv" solver_conv "$OUT/pmc_policy$i.json" > /dev/null; rm -rf "$OUT/pp$i"
           done ;;
+    icache) step pmc_icache 120 rocprofv3 --pmc SQC_ICACHE_MISSES SQC_ICACHE_HITS SQ_IFETCH SQ_WAVES -d "$OUT/pmc_icache" -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary ;;
     list) step counters 120 rocprofv3 -L ;;
     pmcsq) step pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS -d "$OUT/pmc_sq" -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary
            step pmc_sq2 600 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU GRBM_GUI_ACTIVE -d "$OUT/pmc_sq2" -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary ;;

@@ -182,8 +182,9 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   // small to give every SIMD 8 waves at 2 per env takes 4 per env instead (BASELINE C5:
   // 2048 envs of 32 x 32, 22.7 -> 21.0 us per step; C4's 8192 envs: 2 waves, 44.5 vs
   // 52.1 us; profiles/r02ae_configs.log)
+  int n_cu = 0;
   {
-    int dev = 0, n_cu = 0;
+    int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       n_cu = 256;
@@ -212,6 +213,12 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
     p.step_occ = 8;
     p.vis_gap = heist::vis_gap_for(R, C);
   }
+  // Heaviest-raycast-first dispatch (order_kernel) also pays when the whole grid is
+  // resident at once: it deals every CU one env of each cost stratum.  Block b = env b
+  // (HEIST_DISPATCH_ORDER=0, no order[] load) measured 16.29 vs 15.37 us per 4096-env step
+  // (profiles/r02bd_probe_dispatch_order.log).
+  p.dispatch_order = 1;
+  if (const char* m = getenv("HEIST_DISPATCH_ORDER")) p.dispatch_order = atoi(m) ? 1 : 0;
   for (int k = 0; k < 8; ++k) p.tile_lut[k] = k <= 5 ? (float)k / 5.0f : 0.0f;  // environment.py:319
 
   const size_t sizes[] = {

@@ -969,7 +969,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
                                                        int8_t* __restrict__ status_out, int auto_reset) {
   constexpr int NT = 64 * W;
   extern __shared__ __align__(16) unsigned char smem[];
-  const int e = p.order[blockIdx.x];
+  const int e = p.dispatch_order ? p.order[blockIdx.x] : (int)blockIdx.x;
   const int t = threadIdx.x;
   if (p.probe_mode == 6) return;  // profiling: launch + dispatch floor
   HEIST_STEP_STAMP(0);
@@ -1179,7 +1179,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
                                                         float* __restrict__ obs) {
   constexpr int NT = 64 * W;
   extern __shared__ __align__(16) unsigned char smem[];
-  const int e = p.order[blockIdx.x];
+  const int e = p.dispatch_order ? p.order[blockIdx.x] : (int)blockIdx.x;
   const int t = threadIdx.x;
   if (mask && !mask[e]) return;
   const EnvLds L = carve<D>(smem, p.R, p.C, p.max_cams + p.max_guards, 0, W, p.max_guards);

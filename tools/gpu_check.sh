@@ -42,9 +42,13 @@ for s in ${STEPS:-pytest smoke bench prof}; do
     uprobe) step probe_update 600 python tools/probe_update.py ;;
     mprobe) step probe_modes 600 python tools/probe_step_modes.py ;;
     oprobe) step probe_obs_store 300 python tools/probe_obs_store.py ;;
+    prprobe) PROBE_VAR=HEIST_STEP_PRIO PROBE_POLICIES=0,1,2,3 step probe_step_prio 300 python tools/probe_obs_store.py ;;
     dprobe) PROBE_VAR=HEIST_DISPATCH_ORDER PROBE_POLICIES=0,1 step probe_dispatch_order 300 python tools/probe_obs_store.py ;;
     vprobe) step probe_variants 600 python tools/probe_step_variants.py ;;
     envtest) step pytest_env 900 python -u -m pytest tests/test_gpu_env.py -x -q --timeout 200 --timeout-method thread ;;
+    kprobe) HIP_FORCE_DEV_KERNARG=0 step bench_kernarg0 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary
+            HIP_FORCE_DEV_KERNARG=1 step bench_kernarg1 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary
+            step bench_kernargdef 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary ;;
     quick) step bench_quick 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary ;;
     quicksyn) step bench_quick_syn 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary --layouts synthetic ;;
     ppmc) for grp in "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS" \

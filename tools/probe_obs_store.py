@@ -1,6 +1,7 @@
-"""heist_step timing by observation-store cache policy (HEIST_OBS_STORE, read at
-heist_create: 0 plain, 1 write-through sc1, 2 nt, 3 sc1 nt) at 4096 envs on the bench's C2
-layouts (fixed Architect checkpoint, budget 15).  Rounds interleave the policies so clock
+"""heist_step timing by a handle knob read at heist_create (PROBE_VAR, default
+HEIST_OBS_STORE: 0 plain, 1 write-through sc1, 2 nt, 3 sc1 nt observation stores; or e.g.
+HEIST_DISPATCH_ORDER 0/1) at 4096 envs on the bench's C2 layouts (fixed Architect
+checkpoint, budget 15).  Rounds interleave the policies so clock
 and thermal drift hit all of them alike; every policy must give the same observations.
 One JSON line per policy."""
 import json
@@ -17,10 +18,11 @@ from heist_amd import EnvironmentConfig, HeistEnv  # noqa: E402
 
 def main():
     n = int(os.environ.get("PROBE_N", "4096"))
+    var = os.environ.get("PROBE_VAR", "HEIST_OBS_STORE")
     pols = [int(x) for x in os.environ.get("PROBE_POLICIES", "0,1,2,3").split(",")]
     envs = {}
     for pol in pols:
-        os.environ["HEIST_OBS_STORE"] = str(pol)
+        os.environ[var] = str(pol)
         env = HeistEnv(n, EnvironmentConfig(), max_cams=8, max_guards=4, max_path=16, device="cuda", auto_reset=True)
         bench.architect_layouts(env, 15, seed=1234)
         env.reset()
@@ -45,7 +47,7 @@ def main():
         if ref is None:
             ref = o
         v = sorted(res[m])
-        print(json.dumps({"obs_store": m, "n": n, "us_per_step_median": round(v[len(v) // 2], 2),
+        print(json.dumps({"var": var, "value": m, "n": n, "us_per_step_median": round(v[len(v) // 2], 2),
                           "us_all": [round(x, 2) for x in res[m]], "obs_equal_to_first": bool(torch.equal(o, ref))}),
               flush=True)
 

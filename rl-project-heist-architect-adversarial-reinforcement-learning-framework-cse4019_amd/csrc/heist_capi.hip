@@ -219,6 +219,8 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   // (profiles/r02bd_probe_dispatch_order.log).
   p.dispatch_order = 1;
   if (const char* m = getenv("HEIST_DISPATCH_ORDER")) p.dispatch_order = atoi(m) ? 1 : 0;
+  p.split_obs = 1;
+  if (const char* m = getenv("HEIST_SPLIT_OBS")) p.split_obs = atoi(m) ? 1 : 0;
   for (int k = 0; k < 8; ++k) p.tile_lut[k] = k <= 5 ? (float)k / 5.0f : 0.0f;  // environment.py:319
 
   const size_t sizes[] = {

@@ -933,6 +933,71 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
   }
 }
 
+// Step kernel, C % 4 == 0 and two or more waves: the observation in two halves.
+// (1) write_obs_static: channel 0 and channel 2 without the solver cell depend on nothing
+// this tick computes, so the waves other than wave 0 store them while wave 0 updates the
+// emitters (they would otherwise idle at the raycast barrier).  Quad q (4 cells) belongs
+// to thread 64 + q % (NT - 64), which reads its grid dword from global memory (L2: the
+// prefetch just loaded it; L.grid is not yet visible across waves).
+template <int NT>
+__device__ __forceinline__ void write_obs_static(const EnvParams& p, int e, float* __restrict__ obs) {
+  constexpr int PW = NT - 64;
+  const int t = (int)threadIdx.x - 64;
+  if (t < 0) return;
+  const int RC = p.RC, n4 = RC / 4;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(obs + (size_t)e * 3 * RC, (short)0, 12 * RC, 0x00020000);
+  const uint32_t* s4 = reinterpret_cast<const uint32_t*>(p.grid + (size_t)e * RC);
+  const int vault = p.vr * p.C + p.vc, qv = vault >> 2;
+  const int pol = p.obs_store;
+  for (int q = t; q < n4; q += PW) {
+    const uint32_t b = s4[q];
+    float4 v = reinterpret_cast<const float4*>(p.plane0)[q];
+    obs_put(rs, pol, 16 * q,
+            make_float4((float)(b & 0xff) * 0.2f, (float)((b >> 8) & 0xff) * 0.2f, (float)((b >> 16) & 0xff) * 0.2f,
+                        (float)(b >> 24) * 0.2f));
+    if (q == qv) patch4(v, vault & 3, p.vault_val);
+    obs_put(rs, pol, 16 * (2 * n4 + q), v);
+  }
+}
+
+// (2) write_obs_dynamic, after the raycast: channel 1 over all NT threads, and the solver's
+// quad of channel 2 stored again by its owner from (1) -- the same thread, so its second
+// store lands after its first (program order to one address).
+template <int NT>
+__device__ __forceinline__ void write_obs_dynamic(const EnvParams& p, int e, const EnvScalars& s, const EnvLds& L,
+                                                  int cset, float* __restrict__ obs) {
+  constexpr int PW = NT - 64;
+  const int t = threadIdx.x;
+  const int RC = p.RC, C = p.C, n4 = RC / 4, c4 = C / 4;
+  const int mc = p.max_cams, mg = p.max_guards;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(obs + (size_t)e * 3 * RC, (short)0, 12 * RC, 0x00020000);
+  const int pol = p.obs_store;
+  for (int q = t; q < n4; q += NT) {
+    const int r = q / c4, c0 = 4 * (q - r * c4);
+    const int a = L.at(r, c0);
+    uint32_t v;
+    if ((kRing & 3) == 0) {
+      v = *reinterpret_cast<const uint32_t*>(L.vis + a);
+    } else {
+      const uint16_t* vp2 = reinterpret_cast<const uint16_t*>(L.vis + a);
+      v = (uint32_t)vp2[0] | ((uint32_t)vp2[1] << 16);
+    }
+    v |= cone_vis4(L, mc, mg, cset, r, c0);
+    obs_put(rs, pol, 16 * (n4 + q),
+            make_float4((float)(v & 0xff), (float)((v >> 8) & 0xff), (float)((v >> 16) & 0xff), (float)(v >> 24)));
+  }
+  const int solver = s.pos_r * C + s.pos_c, qs = solver >> 2;
+  if (t >= 64 && qs % PW == t - 64) {
+    const int vault = p.vr * C + p.vc;
+    float4 v = reinterpret_cast<const float4*>(p.plane0)[qs];
+    patch4(v, solver & 3, p.plane1[solver]);
+    if (qs == (vault >> 2)) patch4(v, vault & 3, p.vault_val);
+    obs_put(rs, pol, 16 * (2 * n4 + qs), v);
+  }
+}
+
 __device__ __forceinline__ void reset_solver(const EnvParams& p, EnvScalars& s) {  // environment.py:191-202
   s.pos_r = p.sr; s.pos_c = p.sc; s.tick = 0;
   s.done = 0; s.detected = 0; s.vault_reached = 0;
@@ -1065,6 +1130,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     if (off_start) atomicOr(reinterpret_cast<unsigned int*>(&L.meta[5]), gslot == kUncached ? 1u : 2u);
     E = guard_emit(gd);
   }
+  constexpr bool kSplitObs = NT >= 128;  // the observation in two halves (write_obs_static)
+  const bool split_obs = kSplitObs && p.split_obs && (p.C & 3) == 0 && p.probe_mode < 4;
+  if (split_obs) write_obs_static<NT>(p, e, obs);
   publish_emitters(L, E, n_slot);
   if (p.probe_mode == 9) return;  // profiling: everything before the raycast barrier
   HEIST_STEP_STAMP(2);
@@ -1162,7 +1230,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     }
   }
   HEIST_STEP_STAMP(5);
-  if (p.probe_mode < 4) write_obs<NT>(p, e, s, L, cset, obs);
+  if (split_obs) write_obs_dynamic<NT>(p, e, s, L, cset, obs);
+  else if (p.probe_mode < 4) write_obs<NT>(p, e, s, L, cset, obs);
   HEIST_STEP_STAMP(6);
   if (t == 0) {
     rew[e] = (float)reward;

@@ -495,7 +495,7 @@ def test_observation_store_forms_agree(R, n, gpu_device, monkeypatch):
     for store, split in ((2, 1), (0, 0), (1, 1), (3, 0), (0, 1)):
         monkeypatch.setenv("HEIST_OBS_STORE", str(store))
         monkeypatch.setenv("HEIST_SPLIT_OBS", str(split))
-        e = HeistEnv(n, cfg, max_cams=8, max_guards=4, max_path=16, device=gpu_device)
+        e = HeistEnv(n, cfg, max_cams=16, max_guards=8, max_path=16, device=gpu_device)
         e.set_layouts(lays, budget=15 if R == 20 else 40)
         envs.append(e)
     o = [e.reset() for e in envs]

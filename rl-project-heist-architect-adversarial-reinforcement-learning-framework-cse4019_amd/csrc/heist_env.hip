@@ -941,7 +941,7 @@ __device__ __forceinline__ void write_obs(const EnvParams& p, int e, const EnvSc
 // prefetch just loaded it; L.grid is not yet visible across waves).
 template <int NT>
 __device__ __forceinline__ void write_obs_static(const EnvParams& p, int e, float* __restrict__ obs) {
-  constexpr int PW = NT - 64;
+  constexpr int PW = NT > 64 ? NT - 64 : 1;  // NT = 64: never called (split needs two waves)
   const int t = (int)threadIdx.x - 64;
   if (t < 0) return;
   const int RC = p.RC, n4 = RC / 4;
@@ -967,7 +967,7 @@ __device__ __forceinline__ void write_obs_static(const EnvParams& p, int e, floa
 template <int NT>
 __device__ __forceinline__ void write_obs_dynamic(const EnvParams& p, int e, const EnvScalars& s, const EnvLds& L,
                                                   int cset, float* __restrict__ obs) {
-  constexpr int PW = NT - 64;
+  constexpr int PW = NT > 64 ? NT - 64 : 1;  // NT = 64: never called (split needs two waves)
   const int t = threadIdx.x;
   const int RC = p.RC, C = p.C, n4 = RC / 4, c4 = C / 4;
   const int mc = p.max_cams, mg = p.max_guards;

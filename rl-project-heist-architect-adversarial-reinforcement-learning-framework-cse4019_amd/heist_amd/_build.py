@@ -13,7 +13,8 @@ PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO_ROOT = os.path.dirname(PKG_ROOT)
 CSRC = os.path.join(PKG_ROOT, "csrc")
 INCLUDE = os.path.join(REPO_ROOT, "include")
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libheist_hip.so")
+# HEIST_LIB: load another build of the library (A/B measurements of compile-time variants)
+LIB_PATH = os.environ.get("HEIST_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libheist_hip.so")
 BUILD_DIR = os.path.join(PKG_ROOT, "build")
 ARCH = os.environ.get("HEIST_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["heist_env.hip", "heist_arch.hip", "heist_ppo.hip", "heist_policy.hip", "heist_capi.hip"]

@@ -43,7 +43,7 @@ for s in ${STEPS:-pytest smoke bench prof}; do
     mprobe) step probe_modes 600 python tools/probe_step_modes.py ;;
     oprobe) step probe_obs_store 300 python tools/probe_obs_store.py ;;
     prprobe) PROBE_VAR=HEIST_STEP_PRIO PROBE_POLICIES=0,1,2,3 step probe_step_prio 300 python tools/probe_obs_store.py ;;
-    sprobe) PROBE_VAR=HEIST_SPLIT_OBS PROBE_POLICIES=0,1 step probe_split_obs 300 python tools/probe_obs_store.py ;;
+    sprobe) PROBE_VAR=HEIST_SPLIT_OBS PROBE_POLICIES=${PROBE_POLICIES:-0,1} step probe_split_obs 300 python tools/probe_obs_store.py ;;
     dprobe) PROBE_VAR=HEIST_DISPATCH_ORDER PROBE_POLICIES=0,1 step probe_dispatch_order 300 python tools/probe_obs_store.py ;;
     vprobe) step probe_variants 600 python tools/probe_step_variants.py ;;
     envtest) step pytest_env 900 python -u -m pytest tests/test_gpu_env.py -x -q --timeout 200 --timeout-method thread ;;

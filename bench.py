@@ -13,6 +13,7 @@ scaling); the only RCCL calls are the barrier and the max-over-ranks of the elap
 under torchrun WORLD_SIZE must equal N.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 4096] [--no-cpu-baseline]
+                    [--no-secondary] [--backend nccl|gloo] [--train-envs 8192]
 """
 import argparse
 import json
@@ -98,37 +99,16 @@ def cpu_baseline(layouts, cfg, budget, target_s=10.0, threads=1):
     return out
 
 
-def architect_layouts(env, budget, seed, ckpt=None, max_rounds=20):
-    """BASELINE config 2's layouts: the fixed Architect checkpoint sampled at T = 1.0 with
-    the given budget (cameras and guards allowed), every env resampled until its layout is
-    BFS-valid.  Returns the accepted layouts as reference-format lists."""
-    from heist_amd.agents import ArchitectAgent
+def architect_layouts(env, budget, seed, ckpt=None):
+    """BASELINE config 2's layouts (heist_amd.layouts.architect_checkpoint_layouts): the
+    fixed Architect checkpoint sampled at T = 1.0, every env resampled until BFS-valid."""
+    from heist_amd.layouts import architect_checkpoint_layouts
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     import mint_architect_checkpoint as mint
     path = ckpt or mint.DEFAULT
     if not os.path.exists(path):
         mint.mint(path)
-    ag = ArchitectAgent(grid_rows=env.rows, grid_cols=env.cols, budget=budget, device=env.device)
-    ag.load(path)
-    gen = torch.Generator(device=env.device)
-    gen.manual_seed(seed)
-    n = env.n_envs
-    from heist_amd.training import _lb_rows, _scatter_layout
-    lb, _, _ = ag.generate_layouts(n, 1.0, True, True, env=env, generator=gen, record=False)
-    valid = env.set_layout_batch(lb).clone()
-    for _ in range(max_rounds):
-        bad = (~valid).nonzero().reshape(-1).cpu().numpy()
-        if len(bad) == 0:
-            break
-        lbk, _, _ = ag.generate_layouts(len(bad), 1.0, True, True, env=env, generator=gen, record=False)
-        full = _scatter_layout(lbk, bad, env)
-        m = torch.zeros(n, dtype=torch.uint8, device=env.device)
-        m[torch.as_tensor(bad, device=env.device)] = 1
-        v = env.set_layout_batch(full, m)
-        for k in lb.__dataclass_fields__:
-            getattr(lb, k)[torch.as_tensor(bad, device=env.device)] = getattr(lbk, k)
-        valid[torch.as_tensor(bad, device=env.device)] = v[torch.as_tensor(bad, device=env.device)]
-    return lb, bool(valid.all())
+    return architect_checkpoint_layouts(env, budget, seed, path)
 
 
 def measure_rollout(env, dev, steps=20, warmup=3, precision="bf16"):
@@ -232,31 +212,51 @@ def measure_policy(dev, n, iters=50, warmup=5, R=20):
 
 
 def measure_train(cfg, dev, n_envs, rollout_len=32, minibatch=16384, update_precision="fp32",
-                  rollout_precision="fp32"):
-    """Batched AdversarialTrainer iteration (C3-style self-play at the Full Security phase):
-    rollout + heist_gae (V(s_T) bootstrap) + adv-norm + 3 PPO epochs (heist_ppo_loss,
-    Adam) + Architect scoring/update/re-layout."""
+                  rollout_precision="fp32", curriculum=None, episode0=200, iters=1):
+    """Batched AdversarialTrainer iterations (self-play at the curriculum phase of episode0):
+    rollout + heist_gae (V(s_T) bootstrap) + adv-norm + 3 PPO epochs (heist_ppo_loss, Adam;
+    inside a process group every optimizer step averages the Solver's gradients with one
+    flat all-reduce) + Architect scoring/update/re-layout.  Collective at N > 1: every rank
+    runs it; the time is the max over ranks between two barriers and the value counts the
+    env-steps of all ranks."""
     from heist_amd.training import AdversarialTrainer
     import tempfile
+    dist = torch.distributed
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    world = dist.get_world_size() if multi else 1
     d = tempfile.mkdtemp()
     tr = AdversarialTrainer(cfg, solver_episodes_per_layout=4, total_episodes=10 ** 9, save_dir=d, log_dir=d,
                             n_envs=n_envs, rollout_len=rollout_len, minibatch=minibatch, device=dev, seed=0,
-                            update_precision=update_precision, rollout_precision=rollout_precision)
-    tr.global_episode = 200
+                            update_precision=update_precision, rollout_precision=rollout_precision,
+                            curriculum=curriculum)
+    tr.global_episode = episode0
     tr._assign_layouts(np.arange(n_envs))
     log("  warm-up iteration")
     tr.train_iteration()
     torch.cuda.synchronize(dev)
+    if multi:
+        dist.barrier()
     t0 = time.perf_counter()
-    tr.train_iteration()
+    outs = [tr.train_iteration() for _ in range(iters)]
     torch.cuda.synchronize(dev)
+    if multi:
+        dist.barrier()
     dt = time.perf_counter() - t0
-    return {"value": rollout_len * n_envs / dt, "unit": "env-steps/s", "s_per_iteration": dt,
+    if multi:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    _, budget, _, _, phase = tr.get_curriculum_phase(episode0 + 1)
+    return {"value": iters * rollout_len * n_envs * world / dt, "unit": "env-steps/s", "n_gpus": world,
+            "s_per_iteration": dt / iters, "iterations": iters,
             "dtype": "rollout %s, update %s" % (rollout_precision, update_precision),
-            "config": "T=%d x %d envs, 3 epochs, minibatch %d; rollout policy %s, PPO update %s "
-                      "(NHWC MIOpen convs)" % (rollout_len, n_envs, minibatch,
-                                               "bf16 fused kernels" if rollout_precision == "bf16" else "fp32",
-                                               update_precision)}
+            "solver_optimizer_steps_per_iteration": outs[-1].get("solver_updates"),
+            "config": "T=%d x %d envs/GPU x %d GPU%s, %s phase (budget %d), 3 epochs, minibatch %d per rank; rollout "
+                      "policy %s, PPO update %s (NHWC MIOpen convs)%s"
+                      % (rollout_len, n_envs, world, "s" if world > 1 else "", phase, budget, minibatch,
+                         "bf16 fused kernels" if rollout_precision == "bf16" else "fp32", update_precision,
+                         "; one flat RCCL/gloo all-reduce of the Solver gradients per optimizer step" if multi
+                         else "")}
 
 
 def _spawned_rank(rank, world, port, argv):
@@ -279,6 +279,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-secondary", action="store_true", help="skip the rollout / full-train numbers")
+    ap.add_argument("--train-envs", type=int, default=8192, help="envs per GPU of the N > 1 full-train line (C4)")
+    ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                    help="torch.distributed backend at N > 1 (nccl = RCCL over xGMI; gloo lets several ranks share "
+                         "one GPU, for tests)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -302,8 +306,12 @@ def main():
     dist = torch.distributed
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        local %= max(1, torch.cuda.device_count())  # gloo: several ranks may share one GPU
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -322,6 +330,12 @@ def main():
     else:
         layouts = valid_synthetic_layouts(env, args.budget, seed=1234 + rank)
     env.reset()
+    kcfg = env.kernel_config()
+    if kcfg["probe_mode"] != 0:  # the profiling kernel skips phases: its numbers are not the step's
+        print("bench.py: HEIST_PROBE_MODE=%d selects the profiling step kernel (phases skipped, results wrong); "
+              "refusing to time it" % kcfg["probe_mode"], file=sys.stderr)
+        sys.exit(2)
+    knobs = {k: v for k, v in os.environ.items() if k.startswith("HEIST_")}
     gen = torch.Generator(device=dev)
     gen.manual_seed(4321 + rank)
     actions = torch.randint(0, 5, (args.warmup + args.steps, N), device=dev, generator=gen, dtype=torch.int64)
@@ -360,8 +374,9 @@ def main():
     env.count_samples(cnt)
     env.count_exact_rays(cnt_x)
     n_count = 40  # Architect cameras share their parameters, so the work per tick cycles with the headings
+    count_actions = torch.randint(0, 5, (n_count, N), device=dev, generator=gen, dtype=torch.int64)
     for k in range(n_count):
-        env.step(actions[k])
+        env.step(count_actions[k])
     env.count_samples(None)
     env.count_exact_rays(None)
     samples_per_step = float(cnt.sum().item()) / (n_count * N)
@@ -393,7 +408,8 @@ def main():
                                    % (N, "BASELINE C2: fixed Architect checkpoint (T=1.0)" if args.layouts == "architect"
                                       else "synthetic (SURVEY 8d generator ii)", args.budget, ncam, ngu),
                        "envs_per_gpu": N, "grid": "20x20", "layouts": args.layouts,
-                       "parallelism": "env-sharded x%d" % world},
+                       "parallelism": "env-sharded x%d" % world, "kernel_config": kcfg, "env_knobs": knobs,
+                       "backend": args.backend if world > 1 else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "heist::step_kernel", "kernel_ms": kern_ms,
@@ -435,6 +451,17 @@ def main():
             line["cpu_baseline"] = cpu_baseline(layouts, cfg, args.budget, target_s=args.cpu_seconds, threads=cores)
             line["cpu_baseline_1core"] = cpu_baseline(layouts, cfg, args.budget, target_s=args.cpu_seconds / 2,
                                                       threads=1)
+    if world > 1 and not args.no_secondary:
+        # BASELINE config 4 at N > 1: 8192 envs/GPU, the c4 curriculum at its top (budget 40),
+        # every optimizer step averaging gradients with one all-reduce (collective: all ranks)
+        if rank == 0:
+            log("multi-GPU full train (C4: 8192 envs/GPU, budget 40, fp32 rollout + update)")
+        cfg4 = EnvironmentConfig(grid_rows=20, grid_cols=20, max_steps=200, architect_budget=40)
+        train = measure_train(cfg4, dev, args.train_envs, curriculum="c4", episode0=400,
+                              minibatch=min(16384, 4 * args.train_envs))
+        if rank == 0:
+            line["full_train_c4_multi_gpu"] = train
+    if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

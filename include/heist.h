@@ -112,6 +112,14 @@ int heist_step_stamps(heist_t h, uint64_t* buf);
  * at heist_create); no reference counterpart. */
 int heist_step_waves(heist_t h);
 
+/* The handle's effective kernel configuration, no reference counterpart (what a benchmark
+ * records next to its numbers): out[0..n) with n <= 10 receives step_waves, ray_chunk,
+ * step_occ, vis_gap, obs_store, ray_mode, probe_mode, dispatch_order, split_obs,
+ * guard_cones (the HEIST_* environment knobs as heist_create resolved them, then any
+ * heist_set_* calls).  probe_mode != 0 selects the profiling step kernel, whose results are
+ * wrong by design (phases skipped). */
+int heist_get_config(heist_t h, int32_t* out, int n);
+
 /* Raycast arithmetic of later heist_step / heist_reset calls on h: 0 (default) = fp32 fast
  * path with exact fp64 re-cast of every ray that comes within a bounded error of a .5 tie,
  * 1 = exact fp64 path for every ray.  Both give bit-identical visibility; 1 exists for

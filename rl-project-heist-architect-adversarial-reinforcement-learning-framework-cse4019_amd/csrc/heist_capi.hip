@@ -360,6 +360,16 @@ int heist_step_waves(heist_t h) {
   return h->p.step_waves;
 }
 
+int heist_get_config(heist_t h, int32_t* out, int n) {
+  if (int rc = check_handle(h)) return rc;
+  HEIST_REQUIRE(out != nullptr && n >= 0 && n <= 10, "heist_get_config: need out != NULL and 0 <= n <= 10");
+  const EnvParams& p = h->p;
+  const int32_t v[10] = {p.step_waves, p.ray_chunk,  p.step_occ,       p.vis_gap,   p.obs_store,
+                         p.ray_mode,   p.probe_mode, p.dispatch_order, p.split_obs, p.guard_cones};
+  for (int k = 0; k < n; ++k) out[k] = v[k];
+  return 0;
+}
+
 int heist_set_ray_mode(heist_t h, int ray_mode) {
   if (int rc = check_handle(h)) return rc;
   HEIST_REQUIRE(ray_mode == 0 || ray_mode == 1, "heist_set_ray_mode: ray_mode must be 0 or 1");

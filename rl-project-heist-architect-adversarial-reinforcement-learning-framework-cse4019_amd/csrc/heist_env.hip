@@ -745,18 +745,18 @@ __device__ __forceinline__ uint32_t cone_vis4(const EnvLds& L, int mc, int mg, i
 // (the step kernel's counting variant), 0 not, -1 chosen at run time (reset).
 template <int NT, int U, int D, int CNT = -1>
 __device__ __forceinline__ void raycast_pass(const EnvParams& p, int e, unsigned char* smem, const EnvLds& L, int n_slot,
-                                             int mc) {
+                                             int mc, int probe = 0) {
   __syncthreads();  // emitter table, stop map and cleared vis in place
   const int t = threadIdx.x;
   if (t >= mc && t < n_slot) {  // a live guard's own tile (visibility.py:59; a cached cone holds it)
     const Emit E = L.em[t];
     if (E.kind == 1) L.vis[L.at(E.row, E.col)] = 1;
   }
-  if (p.probe_mode != 1 && p.probe_mode != 5) {
+  if (probe != 1 && probe != 5) {
     if (CNT == 1 || (CNT < 0 && (p.sample_counter || p.redo_counter)))
-      cast_rays<NT, U, D, true>(smem, L, p.ray_mode, p.probe_mode, p.half_deg);
+      cast_rays<NT, U, D, true>(smem, L, p.ray_mode, probe, p.half_deg);
     else
-      cast_rays<NT, U, D, false>(smem, L, p.ray_mode, p.probe_mode, p.half_deg);
+      cast_rays<NT, U, D, false>(smem, L, p.ray_mode, probe, p.half_deg);
   }
   __syncthreads();
   if (CNT != 0 && p.sample_counter && t == 0) p.sample_counter[e] += (unsigned int)L.meta[2];
@@ -1026,8 +1026,11 @@ __device__ __forceinline__ double guard_heading_after(const EnvParams& p, int dr
   } while (0)
 
 // COUNT: the counting variant (heist_count_samples / heist_count_redo armed), a kernel of
-// its own so profiles of the plain step are not mixed with it.
-template <int W, int U, int O, int D, bool STAMP, bool COUNT>
+// its own so profiles of the plain step are not mixed with it.  PROBE: the profiling
+// variant that reads EnvParams::probe_mode (HEIST_PROBE_MODE: phases skipped, results
+// wrong); the product kernel is compiled with PROBE = false, where every probe test folds
+// away, and launch_step only selects the PROBE variant when probe_mode != 0.
+template <int W, int U, int O, int D, bool STAMP, bool COUNT, bool PROBE = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) void step_kernel(EnvParams p, const int64_t* __restrict__ actions,
                                                        float* __restrict__ obs, float* __restrict__ rew,
                                                        double* __restrict__ rew64, uint8_t* __restrict__ done_out,
@@ -1036,7 +1039,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   extern __shared__ __align__(16) unsigned char smem[];
   const int e = p.dispatch_order ? p.order[blockIdx.x] : (int)blockIdx.x;
   const int t = threadIdx.x;
-  if (p.probe_mode == 6) return;  // profiling: launch + dispatch floor
+  const int probe = PROBE ? p.probe_mode : 0;
+  if (probe == 6) return;  // profiling: launch + dispatch floor
   HEIST_STEP_STAMP(0);
   if (STAMP && (t & 63) == 0) {
     unsigned long long* q = p.stamps + ((size_t)e * W + (t >> 6)) * 10;
@@ -1054,7 +1058,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   const bool act = !s.done;
   const int a_raw = (int)actions[e];
   clear_vis<NT>(p, L);
-  if (p.probe_mode == 8) return;  // profiling: prefetch issue + plane clears only
+  if (probe == 8) return;  // profiling: prefetch issue + plane clears only
   HEIST_STEP_STAMP(1);
   // One barrier before the raycast: the emitter slots all live in wave 0, whose lanes
   // update them from their records alone (a guard's next patrol point and its cached
@@ -1131,14 +1135,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     E = guard_emit(gd);
   }
   constexpr bool kSplitObs = NT >= 128;  // the observation in two halves (write_obs_static)
-  const bool split_obs = kSplitObs && p.split_obs && (p.C & 3) == 0 && p.probe_mode < 4;
+  const bool split_obs = kSplitObs && p.split_obs && (p.C & 3) == 0 && probe < 4;
   if (split_obs) write_obs_static<NT>(p, e, obs);
   publish_emitters(L, E, n_slot);
-  if (p.probe_mode == 9) return;  // profiling: everything before the raycast barrier
+  if (probe == 9) return;  // profiling: everything before the raycast barrier
   HEIST_STEP_STAMP(2);
   // 3. visibility (environment.py:257-258); an already-done env recomputes the same plane
-  raycast_pass<NT, U, D, COUNT ? 1 : 0>(p, e, smem, L, n_slot, mc);
-  if (p.probe_mode == 7) return;  // profiling: everything up to the raycast
+  raycast_pass<NT, U, D, COUNT ? 1 : 0>(p, e, smem, L, n_slot, mc, probe);
+  if (probe == 7) return;  // profiling: everything up to the raycast
   HEIST_STEP_STAMP(3);
 
   double reward = 0.0;
@@ -1224,14 +1228,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
       }
       publish_emitters(L, E2, n_slot);
       clear_vis<NT>(p, L);
-      raycast_pass<NT, U, D, COUNT ? 1 : 0>(p, e, smem, L, n_slot, mc);
+      raycast_pass<NT, U, D, COUNT ? 1 : 0>(p, e, smem, L, n_slot, mc, probe);
     } else if (moved & 2) {
       cset = 1;
     }
   }
   HEIST_STEP_STAMP(5);
   if (split_obs) write_obs_dynamic<NT>(p, e, s, L, cset, obs);
-  else if (p.probe_mode < 4) write_obs<NT>(p, e, s, L, cset, obs);
+  else if (probe < 4) write_obs<NT>(p, e, s, L, cset, obs);
   HEIST_STEP_STAMP(6);
   if (t == 0) {
     rew[e] = (float)reward;
@@ -1793,11 +1797,22 @@ hipError_t launch_reset(const EnvParams& p, const uint8_t* mask, float* obs, hip
   return hipErrorInvalidValue;
 }
 
+// The profiling variant (HEIST_PROBE_MODE != 0) exists for the default 20 x 20 geometry only.
+static hipError_t launch_step_probe(const EnvParams& p, const int64_t* actions, float* obs, float* rew, double* rew64,
+                                    uint8_t* done_out, int8_t* status_out, int auto_reset, size_t lds, hipStream_t st) {
+  if (p.step_waves != 2 || p.ray_chunk != 4 || p.step_occ != 8 || p.vis_gap != 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((step_kernel<2, 4, 8, 1024, false, false, true>), dim3(p.n_envs), dim3(128), lds, st, p, actions,
+                     obs, rew, rew64, done_out, status_out, auto_reset);
+  return hipGetLastError();
+}
+
 hipError_t launch_step(const EnvParams& p, const int64_t* actions, float* obs, float* rew, double* rew64,
                        uint8_t* done_out, int8_t* status_out, int auto_reset, hipStream_t st) {
   const size_t lds = env_lds(p);
 #define HEIST_STEP_CASE(W, U, O, D)                                                                       \
   if (p.step_waves == W && p.ray_chunk == U && p.step_occ == O && p.vis_gap == D) {                      \
+    if (p.probe_mode)                                                                                    \
+      return launch_step_probe(p, actions, obs, rew, rew64, done_out, status_out, auto_reset, lds, st);  \
     if (p.stamps)                                                                                        \
       hipLaunchKernelGGL((step_kernel<W, U, O, D, true, false>), dim3(p.n_envs), dim3(64 * W), lds, st, p, \
                          actions, obs, rew, rew64, done_out, status_out, auto_reset);                    \

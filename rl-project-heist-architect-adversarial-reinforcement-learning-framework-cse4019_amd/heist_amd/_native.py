@@ -36,6 +36,7 @@ SIGNATURES = {
     "heist_set_ray_mode": (_i, [_vp, _i]),
     "heist_set_guard_cones": (_i, [_vp, _i]),
     "heist_step_waves": (_i, [_vp]),
+    "heist_get_config": (_i, [_vp, _vp, _i]),
     "heist_step_stamps": (_i, [_vp, _vp]),
     "heist_bfs_valid": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "heist_cones": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp]),

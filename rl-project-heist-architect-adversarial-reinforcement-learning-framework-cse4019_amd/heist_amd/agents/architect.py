@@ -141,8 +141,7 @@ class ArchitectAgent:  # agents/architect.py:16-170
         # policy_loss = -mean(lp * (r_norm - v)), no gradient path (as in the reference)
         s_lp_rn = (slpr - mean * slp) * scale if scale is not None else slpr
         policy_loss = -(s_lp_rn - slpv) / k
-        _, new_values, _ = self.network(self.grid_state())
-        new_value = new_values.squeeze()
+        new_value = self.network.value(self.grid_state()).squeeze()
         value_loss = F.mse_loss(new_value, torch.tensor(target, dtype=new_value.dtype, device=d))
         total = policy_loss + self.value_coeff * value_loss
         self._step(total, collective=True)
@@ -161,8 +160,7 @@ class ArchitectAgent:  # agents/architect.py:16-170
         if len(rewards) > 1:
             rewards = (rewards - rewards.mean()) / (rewards.std() + 1e-8)
         advantages = rewards - old_values
-        _, new_values, _ = self.network(self.grid_state())
-        new_value = new_values.squeeze()
+        new_value = self.network.value(self.grid_state()).squeeze()  # = forward()'s state_value
         value_loss = F.mse_loss(new_value, rewards.mean())
         policy_loss = -(old_log_probs * advantages.detach()).mean()  # no gradient path, as in the reference
         total_loss = policy_loss + self.value_coeff * value_loss

@@ -60,3 +60,34 @@ def valid_synthetic_layouts(env, budget: int, seed: int, max_rounds: int = 20, *
             lays[i] = synthetic_layout(rng, R, C, budget, **kw)
     env.set_layouts(lays, budget=budget)
     return lays
+
+
+def architect_checkpoint_layouts(env, budget: int, seed: int, ckpt: str, max_rounds: int = 20):
+    """BASELINE config 2's layouts for every env of a HeistEnv: the fixed Architect
+    checkpoint `ckpt` (reference dict format, agents/architect.py:157-170) sampled at T = 1.0
+    with `budget`, cameras and guards allowed (networks.py:241-335 decoded on the GPU), every
+    env resampled until its layout is BFS-valid.  Returns (LayoutBatch, all_valid); the
+    layouts are set on env."""
+    import torch
+    from .agents import ArchitectAgent
+    from .training import _scatter_layout
+    ag = ArchitectAgent(grid_rows=env.rows, grid_cols=env.cols, budget=budget, device=env.device)
+    ag.load(ckpt)
+    gen = torch.Generator(device=env.device)
+    gen.manual_seed(seed)
+    n = env.n_envs
+    lb, _, _ = ag.generate_layouts(n, 1.0, True, True, env=env, generator=gen, record=False)
+    valid = env.set_layout_batch(lb).clone()
+    for _ in range(max_rounds):
+        bad = (~valid).nonzero().reshape(-1)
+        if bad.numel() == 0:
+            break
+        lbk, _, _ = ag.generate_layouts(int(bad.numel()), 1.0, True, True, env=env, generator=gen, record=False)
+        full = _scatter_layout(lbk, bad.cpu().numpy(), env)
+        m = torch.zeros(n, dtype=torch.uint8, device=env.device)
+        m[bad] = 1
+        v = env.set_layout_batch(full, m)
+        for k in lb.__dataclass_fields__:
+            getattr(lb, k)[bad] = getattr(lbk, k)
+        valid[bad] = v[bad]
+    return lb, bool(valid.all())

@@ -223,6 +223,14 @@ class ArchitectNetwork(nn.Module):  # networks.py:134-335
         }
         return placement_logits, state_value, camera_params
 
+    def value(self, grid_state: torch.Tensor) -> torch.Tensor:
+        """state_value of forward() alone (encoder -> pool -> fc_global -> value_head): the only
+        output the Architect update's loss depends on (its policy term carries no gradient), so
+        the gradients equal those of the full forward (the decoder and camera heads get none)."""
+        features = self.encoder(grid_state)
+        g = self.global_pool(features).reshape(features.shape[0], -1)
+        return self.value_head(F.relu(self.fc_global(g)))
+
     @staticmethod
     def _generate_patrol(row: int, col: int, grid_h: int, grid_w: int) -> list:  # networks.py:324-335
         offsets = [(0, 0), (0, 1), (0, 2), (1, 2), (2, 2), (2, 1), (2, 0), (1, 0)]

@@ -14,9 +14,12 @@ GPU (and N per rank across GPUs):
     the [T, N] rollout: heist_gae per env column, bootstrapping V(s_T) where the rollout
     cuts an attempt (the reference's buffer always ends on done, so its 0 bootstrap is
     this with no cut), global advantage normalisation, heist_ppo_loss;
-  * the Architect updates once per rollout on the (log_prob, value, reward) of the
-    layouts scored during it (or, architect_update="per_layout", one reference-style
-    single-reward step per layout in episode order).
+  * the Architect takes one reference-style single-reward step per layout scored during
+    the rollout, in episode order (architect_update="per_layout", the default: the
+    reference calls update() after every layout, training.py:479-480, :558-559, so its
+    value target is the raw reward); architect_update="batched" instead runs the
+    reference's update formula once over all of them, which normalises k > 1 rewards and so
+    trains the value towards 0 -- faster, but not the reference's Architect learning.
 Data parallel (one process per GPU, torch.distributed): every collective is called the
 same number of times on every rank -- the Solver's minibatch count is agreed by a max
 all-reduce, the Architect's statistics are all-reduced, episode numbers are handed out
@@ -137,7 +140,7 @@ class AdversarialTrainer:  # training.py:115-790
                  architect_lr: float = 3e-4, solver_lr: float = 1e-3, n_envs: int = 256,
                  rollout_len: Optional[int] = None, minibatch: int = 4096, device=None, max_budget: Optional[int] = None,
                  seed: Optional[int] = None, update_precision: str = "fp32", rollout_precision: str = "fp32",
-                 curriculum: Union[str, Sequence[Tuple], None] = None, architect_update: str = "batched"):
+                 curriculum: Union[str, Sequence[Tuple], None] = None, architect_update: str = "per_layout"):
         self.config = config or EnvironmentConfig()
         self.solver_episodes = solver_episodes_per_layout
         self.total_episodes = total_episodes
@@ -156,9 +159,9 @@ class AdversarialTrainer:  # training.py:115-790
         if architect_update not in ("batched", "per_layout"):
             raise ValueError("architect_update must be 'batched' or 'per_layout'")
         self.architect_update = architect_update
-        if seed is not None:
-            torch.manual_seed(seed)
-            np.random.seed(seed)
+        if seed is not None:  # one stream per rank: ranks must not replay each other's layouts and actions
+            torch.manual_seed(seed + dist_utils.rank())
+            np.random.seed(seed + dist_utils.rank())
         mb = max_budget or max(b for _, b, _, _, _ in self.CURRICULUM)
         mb = max(mb, self.config.architect_budget)
         self.env = HeistEnv(n_envs, self.config, max_cams=max(1, mb // 3), max_guards=max(1, mb // 5), max_path=8,
@@ -446,9 +449,9 @@ class AdversarialTrainer:  # training.py:115-790
             next_ckpt = start_episode + 50
             while self.global_episode < start_episode + self.total_episodes:  # a global count: same on every rank
                 self.train_iteration()
-                if self.global_episode >= next_ckpt:
+                if self.global_episode >= next_ckpt:  # every 50 episodes at most (training.py:397-399)
                     self._save_checkpoint(self.global_episode)
-                    next_ckpt += 50
+                    next_ckpt = (self.global_episode // 50 + 1) * 50
             self._save_checkpoint(self.global_episode)
         finally:
             self._callback = None
@@ -466,24 +469,31 @@ class AdversarialTrainer:  # training.py:115-790
                   temperature=temperature, allow_cameras=allow_cameras, allow_guards=allow_guards, interactive=True,
                   phase="Interactive (budget=%d)" % budget)
         w, rk = dist_utils.world_size(), dist_utils.rank()
-        mine = min(num_episodes // w + (1 if rk < num_episodes % w else 0), self.n_envs)
         saved_a = self.solver_episodes
         saved_valid = self.b_valid.clone()
         self.solver_episodes = solver_attempts
-        ids = np.arange(mine)
+        # blocks of at most n_envs layouts per rank, so that any num_episodes is played
+        first = min(num_episodes, self.n_envs * w)
+        ids = np.arange(first // w + (1 if rk < first % w else 0))
         others = torch.ones(self.n_envs, dtype=torch.bool, device=self.device)
         others[torch.as_tensor(ids, device=self.device)] = False
-        self.b_valid &= ~others
         n0 = len(self.game_log)
         self._callback = callback
         try:
-            self._assign_layouts(ids, ov)
-            for _ in range(1000):
-                cnt = dist_utils.allreduce_(torch.tensor([len(self.game_log) - n0], device=self.device))
-                if int(cnt.item()) >= num_episodes:
-                    break
-                self.train_iteration(ov, reassign=False)
-                self.b_valid &= ~self.b_scored  # a scored interactive layout sits out until the block ends
+            done_eps = 0
+            while done_eps < num_episodes:
+                block = min(num_episodes - done_eps, self.n_envs * w)
+                bids = np.arange(block // w + (1 if rk < block % w else 0))
+                self.b_valid &= ~others
+                self._assign_layouts(bids, ov)
+                for _ in range(1000):
+                    cnt = dist_utils.allreduce_(torch.tensor([len(self.game_log) - n0], device=self.device))
+                    if int(cnt.item()) >= done_eps + block:
+                        break
+                    self.train_iteration(ov, reassign=False)
+                    self.b_valid &= ~self.b_scored  # a scored interactive layout sits out until its block ends
+                done_eps = int(dist_utils.allreduce_(torch.tensor([len(self.game_log) - n0],
+                                                                  device=self.device)).item())
         finally:
             self._callback = None
             self.solver_episodes = saved_a

@@ -291,6 +291,18 @@ class HeistEnv:
         bit-identical; takes effect at the next set_layout."""
         nat.check(nat.lib().heist_set_guard_cones(self._h, 1 if on else 0), "heist_set_guard_cones")
 
+    CONFIG_KEYS = ("step_waves", "ray_chunk", "step_occ", "vis_gap", "obs_store", "ray_mode", "probe_mode",
+                   "dispatch_order", "split_obs", "guard_cones")
+
+    def kernel_config(self) -> dict:
+        """The handle's effective kernel configuration (heist_get_config): the HEIST_* knobs as
+        heist_create resolved them plus later set_* calls.  probe_mode != 0 means the
+        profiling step kernel, whose results are wrong by design."""
+        out = (ctypes.c_int32 * len(self.CONFIG_KEYS))()
+        nat.check(nat.lib().heist_get_config(self._h, ctypes.cast(out, ctypes.c_void_p), len(self.CONFIG_KEYS)),
+                  "heist_get_config")
+        return dict(zip(self.CONFIG_KEYS, (int(v) for v in out)))
+
     @property
     def visibility(self) -> torch.Tensor:
         """Current visibility plane [N, R, C] (obs channel 1)."""

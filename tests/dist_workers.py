@@ -50,14 +50,17 @@ def trainer_worker(rank, world, port, out_dir):
     import numpy as np
     from heist_amd import EnvironmentConfig
     from heist_amd.training import AdversarialTrainer
-    torch.manual_seed(100 + rank)  # different sampling streams per rank; weights come from rank 0
     cfg = EnvironmentConfig(grid_rows=12, grid_cols=12, max_steps=40)
     n = 32
+    # the same seed on every rank: the trainer derives one sampling stream per rank from it
+    # (weights still come from rank 0's broadcast)
     tr = AdversarialTrainer(cfg, solver_episodes_per_layout=1 + rank, total_episodes=10 ** 6,
                             save_dir=os.path.join(out_dir, "ck"), log_dir=os.path.join(out_dir, "logs"),
-                            n_envs=n, rollout_len=24 + 8 * rank, minibatch=96, device="cuda:0")
+                            n_envs=n, rollout_len=24 + 8 * rank, minibatch=96, device="cuda:0", seed=5)
     tr.global_episode = 200
     tr._assign_layouts(np.arange(n))
+    first_grids = tr.env.export(grid=True)["grid"].cpu().clone()
+    tr._trace = []
     scored = []
     for it in range(3):
         if rank == 1:
@@ -67,11 +70,15 @@ def trainer_worker(rank, world, port, out_dir):
             tr.b_valid &= keep
         out = tr.train_iteration()
         scored.append(int(out["layouts_scored"]))
+        if it == 0:
+            first_actions = torch.stack([x[0] for x in tr._trace[:8]]).cpu()
+            tr._trace = None
     tr._save_checkpoint(tr.global_episode)
     eps = [e.to_dict()["episode"] for e in tr.game_log]
     torch.save({"solver": [p.detach().cpu() for p in tr.solver.network.parameters()],
                 "architect": [p.detach().cpu() for p in tr.architect.network.parameters()],
-                "global_episode": tr.global_episode, "episodes": eps, "scored": scored},
+                "global_episode": tr.global_episode, "episodes": eps, "scored": scored,
+                "first_grids": first_grids, "first_actions": first_actions},
                os.path.join(out_dir, "t%d.pt" % rank))
     dist.barrier()
     dist.destroy_process_group()

@@ -47,5 +47,8 @@ def test_trainer_two_ranks_unequal_shards(tmp_path, monkeypatch, gpu_device):
     assert a["global_episode"] == b["global_episode"]
     assert not set(a["episodes"]) & set(b["episodes"])  # episode numbers are global
     assert a["scored"] != b["scored"] or sum(a["scored"]) > 0
+    # seed=5 on both ranks still gives each rank its own layouts and actions
+    assert not torch.equal(a["first_grids"], b["first_grids"])
+    assert not torch.equal(a["first_actions"], b["first_actions"])
     logs = json.load(open(tmp_path / "logs" / "game_log.json"))
     assert sorted(e["episode"] for e in logs) == sorted(a["episodes"] + b["episodes"])

@@ -197,6 +197,42 @@ def test_full_size_sampled_vs_oracle(gpu_device):
             assert o_np[j].tobytes() == oracles[j].state_tensor().tobytes()
 
 
+def test_full_size_c2_checkpoint_layouts_vs_oracle(gpu_device):
+    """The bench's headline workload (BASELINE config 2: 4096 envs, 20x20, layouts sampled
+    from checkpoints/architect_c2_fixed.pt at T = 1.0, budget 15): 48 envs replayed through
+    the oracle for 120 ticks with auto-reset, bit-exact, and batch-wide invariants for all."""
+    import os
+    from heist_amd.layouts import architect_checkpoint_layouts
+    from heist_amd.training import _lb_rows
+    ckpt = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "checkpoints",
+                        "architect_c2_fixed.pt")
+    n, budget = 4096, 15
+    cfg = EnvironmentConfig(architect_budget=budget)
+    env = HeistEnv(n, cfg, max_cams=5, max_guards=3, max_path=16, device=gpu_device)
+    lb, all_valid = architect_checkpoint_layouts(env, budget, seed=1234, ckpt=ckpt)
+    assert all_valid
+    env.reset()
+    st = env.export(grid=True)
+    assert float(st["n_cams"].double().mean()) > 1.0 and int(st["n_guards"].max()) >= 1
+    pick = np.random.default_rng(5).choice(n, 48, replace=False)
+    lays = _lb_rows(lb, pick).to_lists()
+    oracles = _oracle_envs(cfg, lays, budget)
+    grid = st["grid"].float() / 5.0
+    g = torch.Generator(device="cpu").manual_seed(12)
+    for t in range(120):
+        acts = torch.randint(0, 5, (n,), generator=g)
+        obs, rew, done, status = env.step(acts)
+        assert torch.equal(obs[:, 0], grid)
+        o_np = obs[torch.from_numpy(pick).to(gpu_device)].cpu().numpy()
+        r64, dn, stt = (x.cpu().numpy() for x in (env.reward64, done, status))
+        for j, i in enumerate(pick):
+            r, d, s = oracles[j].step(int(acts[i]))
+            if d:
+                oracles[j].reset()
+            assert (r64[i], bool(dn[i]), int(stt[i])) == (r, d, s), "env %d t %d" % (i, t)
+            assert o_np[j].tobytes() == oracles[j].state_tensor().tobytes(), "env %d t %d" % (i, t)
+
+
 def test_step_after_done_without_auto_reset(gpu_device):
     cfg = EnvironmentConfig(grid_rows=6, grid_cols=6, max_steps=3)
     env = HeistEnv(2, cfg, device=gpu_device, auto_reset=False)

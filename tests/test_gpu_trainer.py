@@ -101,10 +101,13 @@ def _roundtrip(tr, tmp_path):
     tr2.env.close()
 
 
-def test_c3_selfplay_4096_envs(gpu_device, tmp_path):
-    """BASELINE config 3: 4096 envs/GPU, 20x20, alternating Architect/Solver PPO."""
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_c3_selfplay_4096_envs(gpu_device, tmp_path, precision):
+    """BASELINE config 3: 4096 envs/GPU, 20x20, alternating Architect/Solver PPO, on the
+    parity-default fp32 rollout (the reference's forward) and on the opt-in bf16 kernels."""
     n = 4096
-    tr = _trainer(tmp_path, n, T=48, A=2, device=gpu_device, minibatch=16384, rollout_precision="bf16")
+    tr = _trainer(tmp_path, n, T=48, A=2, device=gpu_device, minibatch=16384, rollout_precision=precision)
+    assert tr.solver.rollout_precision == precision
     rng = np.random.default_rng(3)
     valid = np.nonzero(tr.b_valid.cpu().numpy())[0]
     sample = rng.choice(valid, 32, replace=False)
@@ -165,6 +168,18 @@ def test_interactive_episodes_mask_training_envs(gpu_device, tmp_path):
     assert set(st) == {"grid", "visibility", "solver_pos", "solver_path", "vault_pos", "start_pos", "tick", "done",
                        "cameras", "guards", "detection_events"}
     assert tr.b_valid.any()  # training resumes on every env afterwards
+
+
+def test_interactive_episodes_more_than_envs(gpu_device, tmp_path):
+    """num_episodes > n_envs: the layouts are played in blocks of n_envs, every one of them."""
+    tr = _trainer(tmp_path, 6, R=10, T=30, A=1, device=gpu_device, minibatch=256)
+    n_before = len(tr.game_log)
+    res = tr.run_interactive_episodes(num_episodes=14, budget=5, solver_attempts=1, allow_cameras=False,
+                                      allow_guards=False)
+    assert len(res) == 14
+    new = [e.to_dict() for e in tr.game_log[n_before:]]
+    assert len(new) >= 14 and all(e["is_interactive"] for e in new)
+    assert len({e["episode"] for e in new}) == len(new)
 
 
 def test_per_layout_architect_updates(gpu_device, tmp_path):

@@ -28,6 +28,7 @@ for s in ${STEPS:-pytest smoke bench prof}; do
     pytesto8) for w in 1 2 4; do HEIST_STEP_OCC=8 HEIST_STEP_WAVES=$w step pytest_env_w${w}_o8 900 python -m pytest tests/test_gpu_env.py -x -q; done ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
+    driver) step bench_driver 900 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o heist --output-format csv -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-secondary ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary
          step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary ;;

@@ -16,4 +16,6 @@ run sstamp 300 python tools/probe_step_stamps.py
 run pmc_modes 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS -d $OUT/pmc_modes -o modes --output-format csv -- python3 tools/probe_step_modes.py
 python tools/pmc_modes.py $OUT/pmc_modes/modes_counter_collection.csv $OUT/pmc_modes.json > /dev/null
 run bench 900 python bench.py
+# the driver's own command line, last (BENCH_rNN.json runs exactly this)
+run bench_driver 900 python3 bench.py --gpus 1 --steps 20 --warmup 5
 echo "== all done"

@@ -111,6 +111,57 @@ def architect_layouts(env, budget, seed, ckpt=None):
     return architect_checkpoint_layouts(env, budget, seed, path)
 
 
+def time_env(env, actions, warmup, steps, K, world):
+    """Time `steps` env ticks over all envs after `warmup` untimed ones: K = 1 one heist_step
+    launch per tick, K > 1 heist_step_multi launches of K ticks (the last one shorter), every
+    tick's observation rows going to an [K, N, 3, R, C] buffer.  HIP events bracket the
+    timed launches on the stream they run on, so their span / steps is the mean tick
+    duration (inter-launch gaps included); the wall clock runs between two barriers and at
+    N > 1 is the max over ranks.  Returns (elapsed_s, kernel_ms_per_tick, issue_s, launches)."""
+    dev, N = env.device, env.n_envs
+    dist = torch.distributed
+    stream = torch.cuda.current_stream(dev)
+    if K > 1:
+        shape = (K, N, 3, env.rows, env.cols)
+        bufs = (torch.empty(shape, dtype=torch.float32, device=dev), torch.empty((K, N), device=dev),
+                torch.empty((K, N), dtype=torch.uint8, device=dev), torch.empty((K, N), dtype=torch.int8, device=dev))
+
+        def run(k0, n):
+            launches = 0
+            for j in range(0, n, K):
+                kk = min(K, n - j)
+                env.step_multi_raw(kk, actions[k0 + j:k0 + j + kk], *bufs)
+                launches += 1
+            return launches
+    else:
+        def run(k0, n):
+            for k in range(n):
+                env.step(actions[k0 + k])
+            return n
+    run(0, warmup)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    launches = run(warmup, steps)
+    e1.record(stream)
+    issue_s = time.perf_counter() - t0
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = e0.elapsed_time(e1) / steps
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, kern_ms, issue_s, launches
+
+
 def measure_rollout(env, dev, steps=20, warmup=3, precision="bf16"):
     """env step + batched Solver select_action (carried LSTM state): "bf16" on the fused
     kernels (opt-in), "fp32" on the reference's fp32 forward (the parity default)."""
@@ -132,10 +183,10 @@ def measure_rollout(env, dev, steps=20, warmup=3, precision="bf16"):
                     ", carried LSTM state"}
 
 
-def measure_env_config(dev, R, n, budget, steps=100, warmup=10, **kw):
-    """env-only heist_step at another BASELINE config (C4: 8192 envs/GPU at the top of the
+def measure_env_config(dev, R, n, budget, steps=100, warmup=10, K=1, **kw):
+    """env-only throughput at another BASELINE config (C4: 8192 envs/GPU at the top of the
     budget schedule; C5: 2048 envs/GPU, 32x32, exactly 4 cameras + 3 guards), timed like
-    the headline number (HIP events around `steps` launches)."""
+    the headline (time_env: K ticks per launch)."""
     from heist_amd import EnvironmentConfig, HeistEnv
     from heist_amd.layouts import valid_synthetic_layouts
     cfg = EnvironmentConfig(grid_rows=R, grid_cols=R, max_steps=200, architect_budget=budget)
@@ -148,23 +199,16 @@ def measure_env_config(dev, R, n, budget, steps=100, warmup=10, **kw):
         valid_synthetic_layouts(env, budget, seed=99, **kw)
     env.reset()
     acts = torch.randint(0, 5, (warmup + steps, n), device=dev, dtype=torch.int64)
-    for k in range(warmup):
-        env.step(acts[k])
-    st = torch.cuda.current_stream(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize(dev)
-    e0.record(st)
-    for k in range(steps):
-        env.step(acts[warmup + k])
-    e1.record(st)
-    torch.cuda.synchronize(dev)
-    ms = e0.elapsed_time(e1) / steps
+    K = max(1, min(K, steps))
+    _, ms, _, _ = time_env(env, acts, warmup, steps, K, 1)
     st = env.export()
     ncam, ngu = float(st["n_cams"].double().mean()), float(st["n_guards"].double().mean())
     b = algorithmic_bytes_per_env_step(R, R, ncam, ngu)
     gbs = b * n / (ms * 1e-3) / 1e9
+    env.close()
     return {"value": n / (ms * 1e-3), "unit": "env-steps/s", "kernel_ms": ms, "envs": n, "grid": "%dx%d" % (R, R),
-            "budget": budget, "mean_cameras": ncam, "mean_guards": ngu,
+            "budget": budget, "mean_cameras": ncam, "mean_guards": ngu, "ticks_per_launch": K,
+            "kernel": "heist::step_multi_kernel" if K > 1 else "heist::step_kernel",
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_env_step": b}}
 
@@ -279,6 +323,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-secondary", action="store_true", help="skip the rollout / full-train numbers")
+    ap.add_argument("--ticks-per-launch", type=int, default=20,
+                    help="K: env ticks per heist_step_multi launch in the timed region (1: one heist_step per tick)")
     ap.add_argument("--train-envs", type=int, default=8192, help="envs per GPU of the N > 1 full-train line (C4)")
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                     help="torch.distributed backend at N > 1 (nccl = RCCL over xGMI; gloo lets several ranks share "
@@ -339,33 +385,8 @@ def main():
     gen = torch.Generator(device=dev)
     gen.manual_seed(4321 + rank)
     actions = torch.randint(0, 5, (args.warmup + args.steps, N), device=dev, generator=gen, dtype=torch.int64)
-    stream = torch.cuda.current_stream(dev)
-
-    for k in range(args.warmup):
-        env.step(actions[k])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    # HIP events bracket the timed launches on the stream they run on; their span / K is the
-    # mean launch duration (it includes the small inter-launch gaps, so it is conservative)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record(stream)
-    for k in range(args.steps):
-        env.step(actions[args.warmup + k])
-    e1.record(stream)
-    issue_s = time.perf_counter() - t0
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    kern_ms = e0.elapsed_time(e1) / args.steps
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    K = max(1, min(args.ticks_per_launch, args.steps))
+    elapsed, kern_ms, issue_s, launches = time_env(env, actions, args.warmup, args.steps, K, world)
 
     # ALU work figure: ray samples evaluated per env-step, counted by the
     # kernel on extra steps after the timed region
@@ -385,7 +406,7 @@ def main():
     st = env.export()  # accepted placements (set_layout's rules), not the requested lists
     ncam, ngu = float(st["n_cams"].double().mean()), float(st["n_guards"].double().mean())
     b_step = algorithmic_bytes_per_env_step(20, 20, ncam, ngu)
-    achieved = b_step * N / (kern_ms * 1e-3) / 1e9  # GB/s, per launch / launch duration
+    achieved = b_step * N / (kern_ms * 1e-3) / 1e9  # GB/s: algorithmic bytes per tick / mean tick duration
     total_steps = args.steps * N * world
     value = total_steps / elapsed
 
@@ -395,41 +416,58 @@ def main():
         if os.path.exists(tf) and N == 4096:
             with open(tf) as f:
                 tj = json.load(f)
-            if tj.get("workload") == args.layouts:
-                traffic = tj.get("hbm_bytes_per_launch")
+            if tj.get("workload") == args.layouts and tj.get("ticks_per_launch", 1) == K:
+                traffic = tj.get("hbm_bytes_per_tick", tj.get("hbm_bytes_per_launch"))
                 traffic_src = "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this command (%s), corrected per " \
                               "MI355X_MICROARCH.md: profiles/heist_step_traffic.json" % tj.get("profile", "?")
         line = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "env-only heist_step, 20x20 grid, %d envs/GPU, %s budget-%d layouts "
-                                   "(mean %.2f cameras, %.2f guards/env accepted), uniform random actions, auto-reset"
-                                   % (N, "BASELINE C2: fixed Architect checkpoint (T=1.0)" if args.layouts == "architect"
+            "config": {"workload": "env-only %s, 20x20 grid, %d envs/GPU, %s budget-%d layouts "
+                                   "(mean %.2f cameras, %.2f guards/env accepted), uniform random actions pre-generated "
+                                   "in HBM, auto-reset, every tick's [N,3,20,20] f32 observation, reward, done and "
+                                   "status written to HBM"
+                                   % ("heist_step_multi, K=%d ticks per launch (state on chip between ticks)" % K
+                                      if K > 1 else "heist_step, one tick per launch", N,
+                                      "BASELINE C2: fixed Architect checkpoint (T=1.0)" if args.layouts == "architect"
                                       else "synthetic (SURVEY 8d generator ii)", args.budget, ncam, ngu),
+                       "ticks_per_launch": K,
                        "envs_per_gpu": N, "grid": "20x20", "layouts": args.layouts,
                        "parallelism": "env-sharded x%d" % world, "kernel_config": kcfg, "env_knobs": knobs,
                        "backend": args.backend if world > 1 else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "heist::step_kernel", "kernel_ms": kern_ms,
+                         "kernel": "heist::step_multi_kernel" if K > 1 else "heist::step_kernel",
+                         "kernel_ms": kern_ms, "kernel_ms_per_launch": kern_ms * K, "launches": launches,
                          "algorithmic_bytes_per_env_step": b_step,
                          "ray_samples_per_env_step": samples_per_step,
                          "exact_path_rays_per_env_step": exact_rays_per_step,
-                         "host_issue_us_per_step": issue_s / args.steps * 1e6},
+                         "host_issue_us_per_step": issue_s / args.steps * 1e6,
+                         "note": "achieved = algorithmic bytes per env-step (SURVEY 8d) x envs / mean tick duration; "
+                                 "with K > 1 the per-env state stays on chip between ticks, so the kernel moves "
+                                 "fewer bytes than the formula counts (see traffic)"},
             "cpu_baseline": None,
         }
-        log("env-only: %.1f M env-steps/s, step kernel %.1f us" % (value / 1e6, kern_ms * 1e3))
+        log("env-only: %.1f M env-steps/s, %.2f us per tick (K=%d)" % (value / 1e6, kern_ms * 1e3, K))
         # single-GPU figures: the secondary numbers and the CPU baseline run on rank 0 at N=1
         # only (at N>1 the other ranks would idle at the closing barrier meanwhile)
         if not args.no_secondary and world == 1:
             sec = {}
+            if K > 1:  # the rollout's kernel: one tick per launch (the policy needs each observation)
+                log("env-only, one tick per launch (heist_step)")
+                e1, k1, i1, _ = time_env(env, actions, args.warmup, args.steps, 1, 1)
+                sec["env_only_single_tick"] = {
+                    "value": args.steps * N / e1, "unit": "env-steps/s", "kernel_ms": k1,
+                    "host_issue_us_per_step": i1 / args.steps * 1e6, "kernel": "heist::step_kernel",
+                    "roofline": {"bound": "hbm", "achieved": b_step * N / (k1 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                                 "unit": "GB/s", "frac": b_step * N / (k1 * 1e-3) / 1e9 / HBM_PEAK_GBS}}
             log("env-only at the other BASELINE configs / layout sources")
             other = "synthetic" if args.layouts == "architect" else "architect"
-            sec["env_only_%s_layouts" % other] = measure_env_config(dev, 20, N, args.budget,
+            sec["env_only_%s_layouts" % other] = measure_env_config(dev, 20, N, args.budget, K=K,
                                                                     architect=other == "architect")
-            sec["env_only_c4_8192envs_budget40"] = measure_env_config(dev, 20, 8192, 40, architect=True)
-            sec["env_only_c5_32x32_2048envs_4cams_3guards"] = measure_env_config(dev, 32, 2048, 40, n_cams=4,
+            sec["env_only_c4_8192envs_budget40"] = measure_env_config(dev, 20, 8192, 40, K=K, architect=True)
+            sec["env_only_c5_32x32_2048envs_4cams_3guards"] = measure_env_config(dev, 32, 2048, 40, K=K, n_cams=4,
                                                                                  n_guards=3)
             log("rollout")
             sec["rollout_bf16"] = measure_rollout(env, dev, precision="bf16")

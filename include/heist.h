@@ -82,6 +82,20 @@ int heist_reset(heist_t h, const uint8_t* mask, float* obs_out, heist_stream_t s
 int heist_step(heist_t h, const int64_t* actions, float* obs_out, float* reward_out, double* reward64_out,
                uint8_t* done_out, int8_t* status_out, int auto_reset, heist_stream_t stream);
 
+/* K consecutive heist_step calls in one launch, for actions known in advance (env-only
+ * throughput, action replay; no reference counterpart as an entry point -- it is
+ * environment.py:216-299 + :347-374 applied K times).  Equivalent, bit for bit, to
+ *   for k in 0..K-1: heist_step(h, actions + k*N, obs_out + k*N*3*R*C, reward_out + k*N,
+ *                               reward64_out ? reward64_out + k*N : NULL, done_out + k*N,
+ *                               status_out + k*N, auto_reset, stream)
+ * with every per-tick output written (tick-major: actions [K][N] int64, obs_out
+ * [K][N][3][R][C] float32, reward_out [K][N] float32, reward64_out [K][N] float64 or NULL,
+ * done_out [K][N] uint8, status_out [K][N] int8); the per-env state stays on chip between
+ * the ticks.  1 <= K <= 1024. */
+int heist_step_multi(heist_t h, int K, const int64_t* actions, float* obs_out, float* reward_out,
+                     double* reward64_out, uint8_t* done_out, int8_t* status_out, int auto_reset,
+                     heist_stream_t stream);
+
 /* Copies per-env state out for get_environment_state / the single-env compatibility
  * class (environment.py:388-417).  Any pointer may be NULL.
  *   scalars [N][12] int32: pos_r, pos_c, tick, done, detected, vault_reached, prev_dist,

@@ -22,6 +22,9 @@ hipError_t launch_set_layout(const EnvParams& p, int max_walls, const int32_t* w
 hipError_t launch_reset(const EnvParams& p, const uint8_t* mask, float* obs, hipStream_t st);
 hipError_t launch_step(const EnvParams& p, const int64_t* actions, float* obs, float* rew, double* rew64,
                        uint8_t* done_out, int8_t* status_out, int auto_reset, hipStream_t st);
+hipError_t launch_step_multi(const EnvParams& p, const EnvParams* pg, int K, const int64_t* actions, float* obs,
+                             float* rew, double* rew64, uint8_t* done_out, int8_t* status_out, int auto_reset,
+                             hipStream_t st);
 hipError_t launch_export(const EnvParams& p, int32_t* scalars, int8_t* grid, double* cam_heading, int32_t* guard_idx,
                          double* guard_heading, hipStream_t st);
 hipError_t launch_bfs(const int32_t* grid, int n, int R, int C, int sr, int sc, int gr, int gc, uint8_t* out,
@@ -68,6 +71,9 @@ struct heist_env {
   EnvParams p;
   void* allocs[12];
   int n_allocs;
+  EnvParams* dev_p;  // device copy of p for the K-tick kernel (read through a pointer, not as kernel arguments)
+  EnvParams dev_p_host;  // what dev_p holds
+  bool dev_p_valid;
 };
 
 namespace {
@@ -236,6 +242,7 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
       (size_t)heist::stop_map_bytes(R, C) * n,
       // guard cone cache: 64 B per (guard, patrol index, heading slot)
       sizeof(uint16_t) * heist::kConeEntry * n * (max_guards > 0 ? max_guards : 1) * heist::kConePath * heist::kConeSlots,
+      sizeof(EnvParams),
   };
   h->n_allocs = 0;
   for (size_t k = 0; k < sizeof(sizes) / sizeof(sizes[0]); ++k) {
@@ -261,6 +268,8 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   p.stop = (uint8_t*)h->allocs[9];
   p.stop_bytes = heist::stop_map_bytes(R, C);
   p.cones = (uint16_t*)h->allocs[10];
+  h->dev_p = (EnvParams*)h->allocs[11];
+  h->dev_p_valid = false;
   p.guard_cones = 1;
   if (const char* gc = getenv("HEIST_GUARD_CONES")) p.guard_cones = atoi(gc) ? 1 : 0;
   std::vector<double> hrad(heist::kHalfDegN);
@@ -328,6 +337,26 @@ int heist_step(heist_t h, const int64_t* actions, float* obs_out, float* reward_
   return check_hip(heist::launch_step(h->p, actions, obs_out, reward_out, reward64_out, done_out, status_out,
                                       auto_reset, (hipStream_t)stream),
                    "heist_step");
+}
+
+int heist_step_multi(heist_t h, int K, const int64_t* actions, float* obs_out, float* reward_out,
+                     double* reward64_out, uint8_t* done_out, int8_t* status_out, int auto_reset,
+                     heist_stream_t stream) {
+  if (int rc = check_handle(h)) return rc;
+  HEIST_REQUIRE(K >= 1 && K <= 1024, "heist_step_multi: need 1 <= K <= 1024");
+  HEIST_REQUIRE(actions && obs_out && reward_out && done_out && status_out, "heist_step_multi: null output/input");
+  hipStream_t st = (hipStream_t)stream;
+  if (!h->dev_p_valid || std::memcmp(&h->dev_p_host, &h->p, sizeof(EnvParams)) != 0) {  // set_* changed it
+    h->dev_p_host = h->p;
+    if (int rc = check_hip(hipMemcpyAsync(h->dev_p, &h->dev_p_host, sizeof(EnvParams), hipMemcpyHostToDevice, st),
+                           "heist_step_multi: params upload"))
+      return rc;
+    if (int rc = check_hip(hipStreamSynchronize(st), "heist_step_multi: params upload")) return rc;
+    h->dev_p_valid = true;
+  }
+  return check_hip(heist::launch_step_multi(h->p, h->dev_p, K, actions, obs_out, reward_out, reward64_out, done_out,
+                                            status_out, auto_reset, st),
+                   "heist_step_multi");
 }
 
 int heist_export(heist_t h, int32_t* scalars, int8_t* grid, double* cam_heading, int32_t* guard_idx,

@@ -1247,6 +1247,307 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   HEIST_STEP_STAMP(7);
 }
 
+// ---------------------------------------------------------------------------
+// K ticks per launch (heist_step_multi)
+// ---------------------------------------------------------------------------
+
+// Channels 0 and 2 of observation row `o` (the env's [3][R][C] floats of one tick) except
+// the solver's quad, from LDS (the tile grid and the handle's static position plane,
+// copied in at the start of the launch): waves 1.. store them while wave 0 updates the
+// emitters.  Quad q belongs to thread 64 + q % (NT - 64), which stores the solver's quad
+// again in write_obs_dynamic (program order to one address).
+template <int NT>
+__device__ __forceinline__ void write_obs_static_lds(const EnvParams& p, const EnvLds& L, const float* plane,
+                                                     float* __restrict__ o) {
+  constexpr int PW = NT - 64;
+  const int t = (int)threadIdx.x - 64;
+  if (t < 0) return;
+  const int RC = p.RC, n4 = RC / 4;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(o, (short)0, 12 * RC, 0x00020000);
+  const int vault = p.vr * p.C + p.vc, qv = vault >> 2;
+  const int pol = p.obs_store;
+  for (int q = t; q < n4; q += PW) {
+    const uint32_t b = *reinterpret_cast<const uint32_t*>(L.grid + 4 * q);
+    float4 v = reinterpret_cast<const float4*>(plane)[q];
+    obs_put(rs, pol, 16 * q,
+            make_float4((float)(b & 0xff) * 0.2f, (float)((b >> 8) & 0xff) * 0.2f, (float)((b >> 16) & 0xff) * 0.2f,
+                        (float)(b >> 24) * 0.2f));
+    if (q == qv) patch4(v, vault & 3, p.vault_val);
+    obs_put(rs, pol, 16 * (2 * n4 + q), v);
+  }
+}
+
+// K consecutive heist_step ticks of one env per workgroup (environment.py:216-299 and
+// :347-374 K times), with actions[k][env] known up front: what env-only throughput and
+// action replay need.  The per-env state stays on chip for the whole launch -- grid, stop
+// map, patrol paths, the static position plane and the K actions in LDS, camera and guard
+// records in the registers of wave 0's emitter lanes, the solver scalars in registers --
+// and is written back once at the end; every tick still writes its full observation row
+// (obs[k][env], non-temporal 16-byte stores), reward, done and status.  Per tick: wave 0
+// advances cameras and guards in registers and publishes the emitter table while waves
+// 1.. store the tick's static observation channels, barrier, raycast (all waves),
+// barrier, move / reward / detection / auto-reset / channel 1, and the next tick's cached
+// guard cone entries are loaded before channel 1 is stored (so that waiting for them does
+// not wait for those stores: vmcnt counts in issue order), to land during the barrier and
+// the next emitter update.  A finishing env loads its cached guards' reset cones (patrol
+// point 0, same heading) only then.  A cached guard's heading is the one its slot names;
+// it is read from the cone entry once, at the end.  Results are bit-identical to K
+// heist_step launches (tests/test_gpu_env.py).
+template <int W, int U, int O, int D>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) void step_multi_kernel(
+    EnvParams p, int K, const int64_t* __restrict__ actions, float* __restrict__ obs, float* __restrict__ rew,
+    double* __restrict__ rew64, uint8_t* __restrict__ done_out, int8_t* __restrict__ status_out, int auto_reset) {
+  constexpr int NT = 64 * W;
+  static_assert(W >= 2, "channels 0/2 are stored by the waves after wave 0");
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int e = p.dispatch_order ? p.order[blockIdx.x] : (int)blockIdx.x;
+  const int t = threadIdx.x;
+  const int RC = p.RC, N = p.n_envs;
+  const int mc = p.max_cams, mg = p.max_guards, n_slot = mc + mg;
+  const int path_words = mg * p.max_path;
+  const EnvLds L = carve<D>(smem, p.R, p.C, n_slot, path_words, W, mg);
+  float* plane = reinterpret_cast<float*>(smem + align16(env_lds_bytes(p.R, p.C, n_slot, path_words, D, W, mg)));
+  EmitterRaw* rec = reinterpret_cast<EmitterRaw*>(reinterpret_cast<unsigned char*>(plane) +
+                                                  align16(sizeof(float) * (size_t)RC));  // [n_slot] records
+  uint8_t* act = reinterpret_cast<uint8_t*>(rec + n_slot);
+  const EnvBase eb = env_base(p, e);
+
+  // prologue: the env's layout and state, once per launch
+  {
+    EmitterRaw raw;
+    prefetch<NT>(p, e, eb, L, raw);
+    if (t < n_slot) rec[t] = raw;  // the emitter records live in LDS between ticks
+  }
+  for (int i = t; i < path_words; i += NT) L.path[i] = eb.paths[i];
+  for (int i = t; i < RC; i += NT) plane[i] = p.plane0[i];
+  for (int k = t; k < K; k += NT) {
+    const int64_t a = actions[(size_t)k * N + e];
+    act[k] = (uint8_t)((a < 0 || a > 4) ? 0 : a);  // unknown actions do not move (environment.py:239)
+  }
+  EnvScalars s = p.scal[e];
+  const int g = t - mc;
+  const bool live_cam = t < s.n_cams, live_guard = g >= 0 && g < s.n_guards;
+  bool cached = false;
+  // a cached guard's cone entry for the coming tick, loaded one tick ahead: the pose after
+  // its move (idx + step, nslot) if the env acts and the patrol has >= 2 points
+  // (security.py:147), else the pose it holds
+  uint4 ca = make_uint4(0u, 0u, 0u, 0u), cb = ca;
+  auto next_entry = [&](const EnvBase& eb, const Guard& gd, bool acts) {
+    int idx = gd.idx, slot = gd.hslot;
+    if (acts && gd.len >= 2) {
+      idx += gd.step;
+      if (idx >= gd.len) idx -= gd.len;
+      slot = gd.nslot;
+    }
+    const uint4* src = reinterpret_cast<const uint4*>(eb.cones + cone_off(g, idx, slot));
+    ca = src[0];
+    cb = src[1];
+  };
+  __syncthreads();  // records in LDS
+  if (live_guard) {
+    const Guard gd = as_guard(rec[t]);
+    cached = gd.hslot != kUncached;
+    L.rpos[g] = gd.pos0;
+    if (cached) next_entry(eb, gd, !s.done);
+  }
+
+  // Tick k is one or two raycast passes: pass 0 the tick itself; pass 1 only when the env
+  // finishes, auto-resets and a live-raycast guard stood off its patrol start (the reset
+  // observation needs the cone from patrol point 0).  One raycast instance in the loop.
+  int k = 0;
+  bool reset_pass = false;
+  double reward = 0.0;
+  int status = kAlreadyDone, done_now = 0;
+  while (k < K) {
+    const int mc = p.max_cams, mg = p.max_guards, n_slot = mc + mg;
+    const EnvLds L = carve<D>(smem, p.R, p.C, n_slot, mg * p.max_path, W, mg);
+    float* plane = reinterpret_cast<float*>(smem + align16(env_lds_bytes(p.R, p.C, n_slot, mg * p.max_path, D, W, mg)));
+    EmitterRaw* rec = reinterpret_cast<EmitterRaw*>(reinterpret_cast<unsigned char*>(plane) +
+                                                    align16(sizeof(float) * (size_t)p.RC));
+    const uint8_t* act = reinterpret_cast<const uint8_t*>(rec + n_slot);
+    const EnvBase eb = env_base(p, e);
+    const int RC = p.RC, N = p.n_envs;
+    __syncthreads();  // the previous pass's readers of vis / em / meta / cones are done
+    Emit E;
+    E.kind = -1;
+    const bool act_now = !s.done;
+    if (!reset_pass) {
+      if (t == 0) L.meta[5] = 0;
+      // 2. cameras rotate, guards patrol (security.py:49-51, :145-159)
+      if (live_cam) {
+        Cam cm = as_cam(rec[t]);
+        if (act_now) {
+          cm.heading = py_mod360(cm.heading + cm.speed * 1.0);
+          rec[t] = __builtin_bit_cast(EmitterRaw, cm);
+        }
+        E = cam_emit(cm);
+      } else if (live_guard) {
+        Guard gd = as_guard(rec[t]);
+        const bool moves = act_now && gd.len >= 2;
+        int nidx = gd.idx;
+        if (moves) {
+          nidx += gd.step;
+          if (nidx >= gd.len) nidx -= gd.len;
+        }
+        const uint16_t np = moves ? L.path[__umul24((uint32_t)g, (uint32_t)p.max_path) + (uint32_t)nidx] : gd.pos;
+        if (cached) {
+          if (moves) gd.hslot = gd.nslot;
+          gd.nslot = (uint8_t)(cb.w >> 16);  // row 15: the slot after the next move
+          uint4* dst = reinterpret_cast<uint4*>(L.cone + 16 * g);
+          dst[0] = ca;
+          dst[1] = cb;
+        } else if (moves) {
+          gd.heading = guard_heading_after(p, unpack_r(np) - unpack_r(gd.pos), unpack_c(np) - unpack_c(gd.pos),
+                                           gd.heading);
+        }
+        gd.idx = (int16_t)nidx;
+        gd.pos = np;
+        if (gd.pos != gd.pos0) atomicOr(reinterpret_cast<unsigned int*>(&L.meta[5]), cached ? 2u : 1u);
+        rec[t] = __builtin_bit_cast(EmitterRaw, gd);
+        E = guard_emit(gd);
+      }
+      write_obs_static_lds<NT>(p, L, plane, obs + ((size_t)k * N + e) * 3 * RC);
+    } else {  // the emitters with every guard back at patrol point 0, headings kept
+      if (live_cam) E = cam_emit(as_cam(rec[t]));
+      if (live_guard) {
+        E = guard_emit(as_guard(rec[t]));
+        if (cached) {
+          uint4* dst = reinterpret_cast<uint4*>(L.cone + 16 * g);
+          const uint4* srcr = reinterpret_cast<const uint4*>(L.cone + 16 * (mg + g));
+          dst[0] = srcr[0];
+          dst[1] = srcr[1];
+        }
+      }
+    }
+    clear_vis<NT>(p, L);
+    publish_emitters(L, E, n_slot);
+    __syncthreads();  // emitter table, cone rows, cleared vis
+    // 3. visibility (environment.py:257-258)
+    if (live_guard && E.kind == 1) L.vis[L.at(E.row, E.col)] = 1;  // visibility.py:59
+    cast_rays<NT, U, D, false>(smem, L, p.ray_mode, 0, p.half_deg);
+    __syncthreads();  // vis complete
+
+    int cset = 0;
+    if (!reset_pass) {
+      reward = 0.0;
+      status = kAlreadyDone;
+      if (act_now) {
+        // 1. move (environment.py:239-246)
+        const int a = act[k];
+        const int nr = s.pos_r + (a == 1 ? -1 : (a == 2 ? 1 : 0)), nc = s.pos_c + (a == 3 ? -1 : (a == 4 ? 1 : 0));
+        if (nr >= 0 && nr < p.R && nc >= 0 && nc < p.C && L.grid[nr * p.C + nc] != kWall) {
+          s.pos_r = nr;
+          s.pos_c = nc;
+        }
+        // 4-5. shaping, detection, vault, timeout (environment.py:235, :261-297); the
+        // float64 reward on wave 0 only (thread 0 stores it)
+        const bool rw = (threadIdx.x >> 6) == 0;
+        status = kRunning;
+        const int curr = iabs_(s.pos_r - p.vr) + iabs_(s.pos_c - p.vc);
+        if (rw) {
+          reward = p.r_step;
+          reward += (double)(s.prev_dist - curr) * 0.1;
+          if (curr <= 3 && s.initial_dist > 3) reward += 0.05 * (double)(3 - curr);
+        }
+        s.prev_dist = curr;
+        if (L.vis[L.at(s.pos_r, s.pos_c)] | (cone_vis4(L, mc, mg, 0, s.pos_r, s.pos_c) & 1u)) {
+          s.detected = 1;
+          if (rw) reward += p.r_detect;
+          s.done = 1;
+          status = kDetected;
+        }
+        if (s.pos_r == p.vr && s.pos_c == p.vc) {
+          s.vault_reached = 1;
+          if (rw) reward += p.r_vault;
+          s.done = 1;
+          status = kVaultReached;
+        }
+        s.tick += 1;
+        if (s.tick >= p.max_steps) {
+          s.done = 1;
+          status = kTimeout;
+          if (rw) {
+            double frac = 1.0 - (double)curr / (double)(s.initial_dist > 1 ? s.initial_dist : 1);
+            if (frac < 0.0) frac = 0.0;
+            reward += frac * 2.0;
+          }
+        }
+      }
+      s.pos_r = uni(s.pos_r);  // block-uniform state in scalar registers
+      s.pos_c = uni(s.pos_c);
+      s.prev_dist = uni(s.prev_dist);
+      s.done = uni(s.done);
+      s.detected = uni(s.detected);
+      s.vault_reached = uni(s.vault_reached);
+      s.tick = uni(s.tick);
+      done_now = s.done;
+      if (auto_reset && done_now) {  // block-uniform: the barriers inside are safe
+        // environment.py:183-214: headings kept, guards back to patrol point 0.  A cached
+        // guard's reset cone (point 0, this slot) is loaded now -- only finishing envs pay
+        // for it -- for channel 1 (cone set 1) and the slot after its next move (row 15)
+        const int moved = L.meta[5];
+        reset_solver(p, s);
+        if (live_guard) {
+          Guard gd = as_guard(rec[t]);
+          gd.idx = 0;
+          gd.pos = gd.pos0;
+          if (cached) {
+            const uint4* rsrc = reinterpret_cast<const uint4*>(eb.cones + cone_off(g, 0, gd.hslot));
+            const uint4 ra = rsrc[0], rb = rsrc[1];
+            uint4* rdst = reinterpret_cast<uint4*>(L.cone + 16 * (mg + g));
+            rdst[0] = ra;
+            rdst[1] = rb;
+            gd.nslot = (uint8_t)(rb.w >> 16);
+          }
+          rec[t] = __builtin_bit_cast(EmitterRaw, gd);
+        }
+        if (moved & 1) {  // a live-raycast guard off its start: raycast again from the reset poses
+          reset_pass = true;
+          continue;
+        }
+        if (moved & 2) {
+          __syncthreads();  // the reset cones in LDS
+          cset = 1;
+        }
+      }
+    }
+    reset_pass = false;
+    if (live_guard && cached && k + 1 < K) next_entry(eb, as_guard(rec[t]), !s.done);  // lands during the next update
+    write_obs_dynamic<NT>(p, e, s, L, cset, obs + (size_t)k * N * 3 * RC);
+    if (t == 0) {
+      const size_t ko = (size_t)k * N + e;
+      rew[ko] = (float)reward;
+      if (rew64) rew64[ko] = reward;
+      done_out[ko] = (uint8_t)done_now;
+      status_out[ko] = (int8_t)status;
+    }
+    ++k;
+  }
+  // epilogue: the state the next launch (or heist_export) starts from
+  {
+  const int mc = p.max_cams, mg = p.max_guards, n_slot = mc + mg;
+  const EnvBase eb = env_base(p, e);
+  float* plane = reinterpret_cast<float*>(smem + align16(env_lds_bytes(p.R, p.C, n_slot, mg * p.max_path, D, W, mg)));
+  const EmitterRaw* rec = reinterpret_cast<const EmitterRaw*>(reinterpret_cast<unsigned char*>(plane) +
+                                                              align16(sizeof(float) * (size_t)p.RC));
+  if (t == 0) p.scal[e] = s;
+  if (live_cam) eb.cams[(uint32_t)t].heading = as_cam(rec[t]).heading;
+  if (live_guard) {
+    Guard gd = as_guard(rec[t]);
+    if (cached) {  // the heading its slot names (u16 16..19 of any entry with that slot)
+      const uint4 c2 = reinterpret_cast<const uint4*>(eb.cones + cone_off(g, gd.idx, gd.hslot))[2];
+      gd.heading = __builtin_bit_cast(double, ((uint64_t)c2.y << 32) | c2.x);
+    }
+    Guard* gp = eb.guards + (uint32_t)g;
+    gp->heading = gd.heading;
+    gp->idx = gd.idx;
+    gp->pos = gd.pos;
+    gp->hslot = gd.hslot;
+    gp->nslot = gd.nslot;
+  }
+  }
+}
+
 template <int W, int U, int O, int D>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) void reset_kernel(EnvParams p, const uint8_t* __restrict__ mask,
                                                         float* __restrict__ obs) {
@@ -1827,6 +2128,39 @@ hipError_t launch_step(const EnvParams& p, const int64_t* actions, float* obs, f
   HEIST_ENV_VARIANTS(HEIST_STEP_CASE)
 #undef HEIST_STEP_CASE
   return hipErrorInvalidValue;
+}
+
+// K ticks per launch: (W, U, O, D) variants with two or more waves per env; another
+// configuration (HEIST_STEP_WAVES=1) runs K single-tick launches instead (same results).
+#define HEIST_MULTI_VARIANTS(X) \
+  X(2, 4, 8, 1024) X(2, 4, 8, 2048) X(2, 4, 8, 6144) X(4, 4, 8, 1024) X(4, 4, 8, 2048) X(4, 4, 8, 6144)
+
+size_t step_multi_lds(const EnvParams& p, int K) {
+  const int n_slot = p.max_cams + p.max_guards;
+  return align16(env_lds_bytes(p.R, p.C, n_slot, p.max_guards * p.max_path, p.vis_gap, p.step_waves, p.max_guards)) +
+         align16(sizeof(float) * (size_t)p.RC) + 32 * (size_t)n_slot + align16((size_t)K);
+}
+
+hipError_t launch_step_multi(const EnvParams& p, const EnvParams* pg, int K, const int64_t* actions, float* obs,
+                             float* rew, double* rew64, uint8_t* done_out, int8_t* status_out, int auto_reset,
+                             hipStream_t st) {
+  const size_t lds = step_multi_lds(p, K);
+#define HEIST_MULTI_CASE(W, U, O, D)                                                                        \
+  if (p.step_waves == W && p.ray_chunk == U && p.step_occ == O && p.vis_gap == D && p.probe_mode == 0 &&   \
+      !p.stamps && !p.sample_counter && !p.redo_counter) {                                                   \
+    hipLaunchKernelGGL((step_multi_kernel<W, U, O, D>), dim3(p.n_envs), dim3(64 * W), lds, st, p, K, actions, \
+                       obs, rew, rew64, done_out, status_out, auto_reset);                                    \
+    return hipGetLastError();                                                                                \
+  }
+  HEIST_MULTI_VARIANTS(HEIST_MULTI_CASE)
+#undef HEIST_MULTI_CASE
+  const size_t n = (size_t)p.n_envs;  // no K-tick variant (or instrumentation armed): K single-tick launches
+  for (int k = 0; k < K; ++k) {
+    const hipError_t e = launch_step(p, actions + k * n, obs + k * n * 3 * p.RC, rew + k * n, rew64 ? rew64 + k * n : nullptr,
+                                     done_out + k * n, status_out + k * n, auto_reset, st);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_export(const EnvParams& p, int32_t* scalars, int8_t* grid, double* cam_heading, int32_t* guard_idx,

@@ -21,8 +21,14 @@ SOURCES = ["heist_env.hip", "heist_arch.hip", "heist_ppo.hip", "heist_policy.hip
 HEADERS = ["heist_device.h", "heist_trig.h", "heist_sincos_table.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # heist_env.hip: no SLP vectorization -- ROCm 7.2 clang miscompiles the packed-fp32
-# (v_pk_*_f32) forms of the fast raycast (see the fast path notes in heist_env.hip).
-FILE_FLAGS = {"heist_env.hip": ["-fno-slp-vectorize"]}
+# (v_pk_*_f32) forms of the fast raycast (see the fast path notes in heist_env.hip).  No
+# machine LICM: it hoists the raycast's literal constants (the sin/cos polynomial
+# coefficients, lane masks) out of the K-tick loop of step_multi_kernel and the chunk loops,
+# where they stay live in VGPRs across every other phase: 175 VGPRs spilled in
+# step_multi_kernel<2,4,8,1024> with it, 46 (reloaded once per tick) without; the
+# single-tick step kernel drops from 64 VGPRs + 3 spilled to 53 with none.
+# HEIST_ENV_FLAGS replaces this list (A/B builds).
+FILE_FLAGS = {"heist_env.hip": os.environ.get("HEIST_ENV_FLAGS", "-fno-slp-vectorize -mllvm -disable-machine-licm").split()}
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
           "--offload-arch=" + ARCH, "-I", INCLUDE, "-I", CSRC]
 

@@ -30,6 +30,7 @@ SIGNATURES = {
     "heist_set_layout": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "heist_reset": (_i, [_vp, _vp, _vp, _vp]),
     "heist_step": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
+    "heist_step_multi": (_i, [_vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
     "heist_export": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "heist_count_samples": (_i, [_vp, _vp]),
     "heist_count_redo": (_i, [_vp, _vp]),

@@ -238,6 +238,46 @@ class HeistEnv:
         nat.check(rc, "heist_step")
         return obs, self.reward, self._done_bool, self.status
 
+    def step_multi(self, actions: torch.Tensor, obs_out: Optional[torch.Tensor] = None,
+                   auto_reset: Optional[bool] = None, reward64: bool = False):
+        """K steps in one launch (heist_step_multi) for actions [K, N] known in advance:
+        tick k's observation, reward, done and status land in obs[k], reward[k], ... exactly
+        as K step() calls would produce them.  Returns (obs [K,N,3,R,C], reward [K,N] f32,
+        done [K,N] bool, status [K,N] int8, reward64 [K,N] f64 or None).  The per-env state
+        is on chip between the ticks; env.obs is not updated (obs[K-1] is the latest)."""
+        a = actions
+        if a.device != self.device or a.dtype != torch.int64 or not a.is_contiguous():
+            a = a.to(device=self.device, dtype=torch.int64).contiguous()
+        if a.dim() != 2 or a.shape[1] != self.n_envs:
+            raise ValueError("step_multi: actions must be [K, %d]" % self.n_envs)
+        K = int(a.shape[0])
+        kw = dict(device=self.device)
+        shape = (K, self.n_envs, 3, self.rows, self.cols)
+        if obs_out is None:
+            obs_out = torch.empty(shape, dtype=torch.float32, **kw)
+        elif (tuple(obs_out.shape) != shape or obs_out.dtype != torch.float32 or obs_out.device != self.device
+              or not obs_out.is_contiguous()):
+            raise ValueError("step_multi: obs_out must be a contiguous float32 %s tensor on %s" % (shape, self.device))
+        rew = torch.empty((K, self.n_envs), dtype=torch.float32, **kw)
+        r64 = torch.empty((K, self.n_envs), dtype=torch.float64, **kw) if reward64 else None
+        done = torch.empty((K, self.n_envs), dtype=torch.uint8, **kw)
+        status = torch.empty((K, self.n_envs), dtype=torch.int8, **kw)
+        ar = self.auto_reset if auto_reset is None else auto_reset
+        with torch.cuda.device(self.device):
+            nat.check(nat.lib().heist_step_multi(self._h, K, nat.ptr(a), nat.ptr(obs_out), nat.ptr(rew), nat.ptr(r64),
+                                                 nat.ptr(done), nat.ptr(status), 1 if ar else 0, self._stream()),
+                      "heist_step_multi")
+        return obs_out, rew, done.view(torch.bool), status, r64
+
+    def step_multi_raw(self, K: int, actions: torch.Tensor, obs_out: torch.Tensor, reward: torch.Tensor,
+                       done: torch.Tensor, status: torch.Tensor, auto_reset: bool = True) -> None:
+        """heist_step_multi on caller-owned buffers with no checks or allocation (the
+        benchmark's timed loop; shapes as step_multi's)."""
+        rc = nat.lib().heist_step_multi(self._h, K, actions.data_ptr(), obs_out.data_ptr(), reward.data_ptr(), None,
+                                        done.data_ptr(), status.data_ptr(), 1 if auto_reset else 0,
+                                        torch.cuda.current_stream(self.device).cuda_stream)
+        nat.check(rc, "heist_step_multi")
+
     # -- introspection -------------------------------------------------------------
     def export(self, grid: bool = False) -> dict:
         """Per-env state (get_environment_state source) as device tensors."""

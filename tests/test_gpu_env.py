@@ -545,3 +545,102 @@ def test_observation_store_forms_agree(R, n, gpu_device, monkeypatch):
             for x, y in zip(r[0], r[k]):
                 assert torch.equal(x, y), (t, k)
             assert torch.equal(envs[0].reward64, envs[k].reward64), (t, k)
+
+
+def _twin_envs(n, cfg, lays, budget, gpu_device, cones=True, **kw):
+    envs = []
+    for _ in range(2):
+        env = HeistEnv(n, cfg, device=gpu_device, **kw)
+        env.set_guard_cones(cones)
+        v = env.set_layouts(lays, budget=budget)
+        env.reset()
+        envs.append((env, v.clone()))
+    assert torch.equal(envs[0][1], envs[1][1])
+    return envs[0][0], envs[1][0]
+
+
+def _compare_multi_vs_single(a, b, acts, chunks, auto_reset=True):
+    """env a: heist_step_multi over `chunks` (tick counts per launch); env b: one heist_step
+    per tick.  Every tick's obs, float64 reward, done and status must be bit-identical,
+    and so must the state both end in."""
+    k0 = 0
+    for K in chunks:
+        obs, rew, done, status, r64 = a.step_multi(acts[k0:k0 + K], auto_reset=auto_reset, reward64=True)
+        for k in range(K):
+            o, r, d, s = b.step(acts[k0 + k], auto_reset=auto_reset)
+            ctx = "tick %d" % (k0 + k)
+            assert torch.equal(obs[k], o), ctx
+            assert torch.equal(r64[k], b.reward64), ctx
+            assert torch.equal(rew[k], r), ctx
+            assert torch.equal(done[k], d), ctx
+            assert torch.equal(status[k], s), ctx
+        k0 += K
+    sa, sb = a.export(grid=True), b.export(grid=True)
+    for key in sb:
+        assert torch.equal(sa[key], sb[key]), key
+
+
+@pytest.mark.parametrize("cones", [True, False], ids=["guard_cones", "live_guards"])
+@pytest.mark.parametrize("auto_reset", [True, False], ids=["auto_reset", "no_reset"])
+def test_step_multi_equals_single_steps(gpu_device, cones, auto_reset):
+    """heist_step_multi (K ticks per launch, state on chip) == K heist_step launches, bit for
+    bit, over 60 ticks in launches of 1, 17 and 42 ticks, with short episodes (max_steps
+    25) so that timeouts, detections and auto-resets with guards off their start happen
+    inside a launch."""
+    n, R = 512, 20
+    cfg = EnvironmentConfig(max_steps=25)
+    lays = synthetic_layouts(n, R, R, 15, seed=61)
+    a, b = _twin_envs(n, cfg, lays, 15, gpu_device, cones=cones)
+    g = torch.Generator(device="cpu").manual_seed(62)
+    acts = torch.randint(0, 5, (60, n), generator=g).to(gpu_device)
+    acts[::7, ::3] = 7  # out-of-range actions do not move
+    _compare_multi_vs_single(a, b, acts, [1, 17, 42], auto_reset=auto_reset)
+
+
+def test_step_multi_c5_32x32_four_waves(gpu_device):
+    """BASELINE config 5 geometry (32x32, 4 cameras + 3 guards, 2048 envs: 4 waves per env)."""
+    n, R = 2048, 32
+    cfg = EnvironmentConfig(grid_rows=R, grid_cols=R, max_steps=40, architect_budget=40)
+    lays = synthetic_layouts(n, R, R, 40, seed=63, n_cams=4, n_guards=3)
+    a, b = _twin_envs(n, cfg, lays, 40, gpu_device, max_cams=13, max_guards=8)
+    assert a.kernel_config()["step_waves"] in (2, 4)
+    g = torch.Generator(device="cpu").manual_seed(64)
+    acts = torch.randint(0, 5, (50, n), generator=g).to(gpu_device)
+    _compare_multi_vs_single(a, b, acts, [50])
+
+
+def test_step_multi_c2_checkpoint_layouts(gpu_device):
+    """The headline workload (4096 envs, C2 checkpoint layouts): K-tick launches == single
+    ticks, plus 32 envs replayed through the oracle."""
+    import os
+    from heist_amd.layouts import architect_checkpoint_layouts
+    from heist_amd.training import _lb_rows
+    ckpt = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "checkpoints",
+                        "architect_c2_fixed.pt")
+    n, budget = 4096, 15
+    cfg = EnvironmentConfig(architect_budget=budget)
+    envs = []
+    for _ in range(2):
+        env = HeistEnv(n, cfg, max_cams=5, max_guards=3, max_path=16, device=gpu_device)
+        lb, ok = architect_checkpoint_layouts(env, budget, seed=1234, ckpt=ckpt)
+        assert ok
+        env.reset()
+        envs.append(env)
+    a, b = envs
+    g = torch.Generator(device="cpu").manual_seed(65)
+    acts = torch.randint(0, 5, (80, n), generator=g).to(gpu_device)
+    pick = np.random.default_rng(66).choice(n, 32, replace=False)
+    oracles = _oracle_envs(cfg, _lb_rows(lb, pick).to_lists(), budget)
+    obs, rew, done, status, r64 = a.step_multi(acts[:80], reward64=True)
+    r64n, dn, stn = (x.cpu().numpy() for x in (r64, done, status))
+    obs_p = obs[:, torch.from_numpy(pick).to(gpu_device)].cpu().numpy()
+    for k in range(80):
+        for j, i in enumerate(pick):
+            r, d, s = oracles[j].step(int(acts[k, i]))
+            if d:
+                oracles[j].reset()
+            assert (r64n[k, i], bool(dn[k, i]), int(stn[k, i])) == (r, d, s), "env %d t %d" % (i, k)
+            assert obs_p[k, j].tobytes() == oracles[j].state_tensor().tobytes(), "env %d t %d" % (i, k)
+    for k in range(80):
+        o, r, d, s = b.step(acts[k])
+        assert torch.equal(obs[k], o) and torch.equal(done[k], d) and torch.equal(status[k], s), k

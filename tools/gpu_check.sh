@@ -29,6 +29,11 @@ for s in ${STEPS:-pytest smoke bench prof}; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     driver) step bench_driver 900 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    multitest) step pytest_multi 300 python -u -m pytest tests/test_gpu_env.py -k multi -x -v --timeout 200 --timeout-method thread ;;
+    quickk) step bench_quick_k 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary ;;
+    quick1) step bench_quick_1 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary --ticks-per-launch 1 ;;
+    quicklicm) HEIST_LIB=$PWD/rl-project-heist-architect-adversarial-reinforcement-learning-framework-cse4019_amd/heist_amd/libheist_hip_licm.so step bench_quick_licm 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary --ticks-per-launch 1 ;;
+    benchtest) step pytest_bench 900 python -u -m pytest tests/test_gpu_bench.py -x -v --timeout 800 --timeout-method thread ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o heist --output-format csv -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-secondary ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary
          step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary ;;

@@ -412,7 +412,7 @@ def main():
 
     if rank == 0:
         traffic, traffic_src = None, None
-        tf = os.path.join(ROOT, "profiles", "heist_step_traffic.json")
+        tf = os.path.join(ROOT, "profiles", "heist_step_multi_traffic.json" if K > 1 else "heist_step_traffic.json")
         if os.path.exists(tf) and N == 4096:
             with open(tf) as f:
                 tj = json.load(f)

@@ -1293,7 +1293,7 @@ __device__ __forceinline__ void write_obs_static_lds(const EnvParams& p, const E
 // point 0, same heading) only then.  A cached guard's heading is the one its slot names;
 // it is read from the cone entry once, at the end.  Results are bit-identical to K
 // heist_step launches (tests/test_gpu_env.py).
-template <int W, int U, int O, int D>
+template <int W, int U, int O, int D, bool STAMP = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) void step_multi_kernel(
     EnvParams p, int K, const int64_t* __restrict__ actions, float* __restrict__ obs, float* __restrict__ rew,
     double* __restrict__ rew64, uint8_t* __restrict__ done_out, int8_t* __restrict__ status_out, int auto_reset) {
@@ -1311,6 +1311,23 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
                                                   align16(sizeof(float) * (size_t)RC));  // [n_slot] records
   uint8_t* act = reinterpret_cast<uint8_t*>(rec + n_slot);
   const EnvBase eb = env_base(p, e);
+  // STAMP (instrumentation, heist_step_stamps): lane 0 of every wave sums the shader clock
+  // spent in each of 7 tick segments over the launch into LDS (after the K actions), and
+  // writes [segment sums 0..6, launch lifetime, HW_ID, XCC_ID] to stamps[env][wave][10]
+  unsigned long long* st_acc = reinterpret_cast<unsigned long long*>(act + align16((size_t)K));
+  unsigned long long st_last = 0, st_start = 0;
+  if (STAMP && (t & 63) == 0) {
+    st_start = st_last = __builtin_amdgcn_s_memtime();
+    for (int j = 0; j < 7; ++j) st_acc[(t >> 6) * 8 + j] = 0;
+  }
+#define HEIST_MULTI_STAMP(seg)                                                  \
+  do {                                                                          \
+    if (STAMP && (threadIdx.x & 63) == 0) {                                     \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime();             \
+      st_acc[(threadIdx.x >> 6) * 8 + (seg)] += now_ - st_last;                 \
+      st_last = now_;                                                           \
+    }                                                                           \
+  } while (0)
 
   // prologue: the env's layout and state, once per launch
   {
@@ -1368,6 +1385,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     const EnvBase eb = env_base(p, e);
     const int RC = p.RC, N = p.n_envs;
     __syncthreads();  // the previous pass's readers of vis / em / meta / cones are done
+    HEIST_MULTI_STAMP(6);  // 6: end of the previous tick's stores -> through the top barrier
     Emit E;
     E.kind = -1;
     const bool act_now = !s.done;
@@ -1421,11 +1439,15 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     }
     clear_vis<NT>(p, L);
     publish_emitters(L, E, n_slot);
+    HEIST_MULTI_STAMP(0);  // 0: emitter update, static channels, clears
     __syncthreads();  // emitter table, cone rows, cleared vis
+    HEIST_MULTI_STAMP(1);  // 1: waiting at the raycast barrier
     // 3. visibility (environment.py:257-258)
     if (live_guard && E.kind == 1) L.vis[L.at(E.row, E.col)] = 1;  // visibility.py:59
     cast_rays<NT, U, D, false>(smem, L, p.ray_mode, 0, p.half_deg);
+    HEIST_MULTI_STAMP(2);  // 2: raycast
     __syncthreads();  // vis complete
+    HEIST_MULTI_STAMP(3);  // 3: waiting for the other waves' raycast
 
     int cset = 0;
     if (!reset_pass) {
@@ -1512,6 +1534,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
       }
     }
     reset_pass = false;
+    HEIST_MULTI_STAMP(4);  // 4: move, reward, detection, auto-reset
     if (live_guard && cached && k + 1 < K) next_entry(eb, as_guard(rec[t]), !s.done);  // lands during the next update
     write_obs_dynamic<NT>(p, e, s, L, cset, obs + (size_t)k * N * 3 * RC);
     if (t == 0) {
@@ -1521,8 +1544,10 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
       done_out[ko] = (uint8_t)done_now;
       status_out[ko] = (int8_t)status;
     }
+    HEIST_MULTI_STAMP(5);  // 5: channel 1 + solver quad, outputs
     ++k;
   }
+#undef HEIST_MULTI_STAMP
   // epilogue: the state the next launch (or heist_export) starts from
   {
   const int mc = p.max_cams, mg = p.max_guards, n_slot = mc + mg;
@@ -1531,6 +1556,13 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   const EmitterRaw* rec = reinterpret_cast<const EmitterRaw*>(reinterpret_cast<unsigned char*>(plane) +
                                                               align16(sizeof(float) * (size_t)p.RC));
   if (t == 0) p.scal[e] = s;
+  if (STAMP && (t & 63) == 0) {
+    unsigned long long* q = p.stamps + ((size_t)e * W + (t >> 6)) * 10;
+    for (int j = 0; j < 7; ++j) q[j] = st_acc[(t >> 6) * 8 + j];
+    q[7] = __builtin_amdgcn_s_memtime() - st_start;
+    q[8] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+    q[9] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+  }
   if (live_cam) eb.cams[(uint32_t)t].heading = as_cam(rec[t]).heading;
   if (live_guard) {
     Guard gd = as_guard(rec[t]);
@@ -2138,7 +2170,8 @@ hipError_t launch_step(const EnvParams& p, const int64_t* actions, float* obs, f
 size_t step_multi_lds(const EnvParams& p, int K) {
   const int n_slot = p.max_cams + p.max_guards;
   return align16(env_lds_bytes(p.R, p.C, n_slot, p.max_guards * p.max_path, p.vis_gap, p.step_waves, p.max_guards)) +
-         align16(sizeof(float) * (size_t)p.RC) + 32 * (size_t)n_slot + align16((size_t)K);
+         align16(sizeof(float) * (size_t)p.RC) + 32 * (size_t)n_slot + align16((size_t)K) +
+         (p.stamps ? 64 * (size_t)p.step_waves : 0);
 }
 
 hipError_t launch_step_multi(const EnvParams& p, const EnvParams* pg, int K, const int64_t* actions, float* obs,
@@ -2147,9 +2180,13 @@ hipError_t launch_step_multi(const EnvParams& p, const EnvParams* pg, int K, con
   const size_t lds = step_multi_lds(p, K);
 #define HEIST_MULTI_CASE(W, U, O, D)                                                                        \
   if (p.step_waves == W && p.ray_chunk == U && p.step_occ == O && p.vis_gap == D && p.probe_mode == 0 &&   \
-      !p.stamps && !p.sample_counter && !p.redo_counter) {                                                   \
-    hipLaunchKernelGGL((step_multi_kernel<W, U, O, D>), dim3(p.n_envs), dim3(64 * W), lds, st, p, K, actions, \
-                       obs, rew, rew64, done_out, status_out, auto_reset);                                    \
+      !p.sample_counter && !p.redo_counter) {                                                                \
+    if (p.stamps)                                                                                            \
+      hipLaunchKernelGGL((step_multi_kernel<W, U, O, D, true>), dim3(p.n_envs), dim3(64 * W), lds, st, p, K,  \
+                         actions, obs, rew, rew64, done_out, status_out, auto_reset);                         \
+    else                                                                                                     \
+      hipLaunchKernelGGL((step_multi_kernel<W, U, O, D>), dim3(p.n_envs), dim3(64 * W), lds, st, p, K,        \
+                         actions, obs, rew, rew64, done_out, status_out, auto_reset);                         \
     return hipGetLastError();                                                                                \
   }
   HEIST_MULTI_VARIANTS(HEIST_MULTI_CASE)

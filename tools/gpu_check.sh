@@ -33,6 +33,16 @@ for s in ${STEPS:-pytest smoke bench prof}; do
     quickk) step bench_quick_k 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary ;;
     quick1) step bench_quick_1 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary --ticks-per-launch 1 ;;
     quicklicm) HEIST_LIB=$PWD/rl-project-heist-architect-adversarial-reinforcement-learning-framework-cse4019_amd/heist_amd/libheist_hip_licm.so step bench_quick_licm 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary --ticks-per-launch 1 ;;
+    mstamp) step multi_stamps 300 python tools/probe_multi_stamps.py ;;
+    profm) step prof_multi 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o heist --output-format csv -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-secondary
+           cp "$OUT"/prof/*kernel_stats.csv "$OUT/kernel_stats.csv" 2>/dev/null; true ;;
+    pmcm) step pmc_fetch_m 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch_m" -o heist --output-format csv -- python3 bench.py --steps 60 --warmup 20 --no-cpu-baseline --no-secondary
+          step pmc_write_m 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write_m" -o heist --output-format csv -- python3 bench.py --steps 60 --warmup 20 --no-cpu-baseline --no-secondary
+          python tools/pmc_traffic.py "$OUT/pmc_fetch_m" "$OUT/pmc_write_m" --ticks 20 --profile ${TAG:-run} --out "$OUT/heist_step_multi_traffic.json" > "$OUT/traffic_m.log" 2>&1; true ;;
+    sqm) step pmc_sq_m 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d "$OUT/pmc_sq_m" -o heist --output-format csv -- python3 bench.py --steps 60 --warmup 20 --no-cpu-baseline --no-secondary
+         step pmc_sq2_m 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d "$OUT/pmc_sq2_m" -o heist --output-format csv -- python3 bench.py --steps 60 --warmup 20 --no-cpu-baseline --no-secondary
+         python tools/pmc_summary.py "$(find "$OUT/pmc_sq_m" -name "*counter_collection.csv" | head -n 1)" step_multi_kernel "$OUT/pmc_sq_m.json" > /dev/null 2>&1
+         python tools/pmc_summary.py "$(find "$OUT/pmc_sq2_m" -name "*counter_collection.csv" | head -n 1)" step_multi_kernel "$OUT/pmc_sq2_m.json" > /dev/null 2>&1; true ;;
     benchtest) step pytest_bench 900 python -u -m pytest tests/test_gpu_bench.py -x -v --timeout 800 --timeout-method thread ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o heist --output-format csv -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-secondary ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary

@@ -14,12 +14,14 @@ import json
 import os
 import statistics
 
+KERNEL = "step_kernel"
+
 
 def per_dispatch(d, counter):
     vals = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "step_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            if KERNEL in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 key = r.get("Dispatch_Id") or r.get("Correlation_Id")
                 vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
     return list(vals.values())
@@ -32,20 +34,26 @@ def main():
     ap.add_argument("--envs", type=int, default=4096)
     ap.add_argument("--workload", default="architect", help="bench.py --layouts of the profiled command")
     ap.add_argument("--profile", default=None, help="run tag the passes come from (e.g. r02a)")
-    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                                  "profiles", "heist_step_traffic.json"))
+    ap.add_argument("--ticks", type=int, default=1, help="ticks per launch (bench.py --ticks-per-launch)")
+    ap.add_argument("--out", default=None)
     a = ap.parse_args()
+    global KERNEL
+    KERNEL = "step_multi_kernel" if a.ticks > 1 else "step_kernel"
+    if a.out is None:
+        a.out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                             "heist_step_multi_traffic.json" if a.ticks > 1 else "heist_step_traffic.json")
     fetch = per_dispatch(a.fetch_dir, "FETCH_SIZE")
     write = per_dispatch(a.write_dir, "WRITE_SIZE")
     f_kb, w_kb = statistics.median(fetch), statistics.median(write)
     fetch_b = 2 * f_kb * 1024.0
     write_b = w_kb * 1024.0
-    out = {"kernel": "heist::step_kernel", "envs": a.envs, "workload": a.workload,
+    out = {"kernel": "heist::" + KERNEL, "envs": a.envs, "workload": a.workload, "ticks_per_launch": a.ticks,
            "profile": a.profile or os.path.basename(os.path.dirname(os.path.abspath(a.fetch_dir))), "dispatches": [len(fetch), len(write)],
            "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
            "fetch_bytes_corrected": fetch_b, "write_bytes": write_b,
            "hbm_bytes_per_launch": fetch_b + write_b,
-           "hbm_bytes_per_env_step": (fetch_b + write_b) / a.envs,
+           "hbm_bytes_per_tick": (fetch_b + write_b) / a.ticks,
+           "hbm_bytes_per_env_step": (fetch_b + write_b) / a.ticks / a.envs,
            "note": "FETCH_SIZE x2 (gfx950 128-B requests tallied at 64 B); Infinity-Cache hits are "
                    "counted by these memory-side counters"}
     with open(a.out, "w") as fh:

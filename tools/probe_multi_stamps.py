@@ -1,0 +1,61 @@
+"""Where does a heist_step_multi launch spend its time?  The STAMP variant of the K-tick
+kernel (heist_step_stamps armed) sums the shader clock each wave spends in 7 tick segments
+over the launch: 0 emitter update + static channels + clears, 1 wait at the raycast
+barrier, 2 raycast, 3 wait for the other waves' raycast, 4 move/reward/detection/
+auto-reset, 5 channel 1 + outputs, 6 end of tick -> through the top barrier.  Workload:
+bench.py's headline (4096 envs, C2 checkpoint layouts, K ticks per launch).
+
+Prints one JSON line: per-segment cycles per tick (mean over waves, by wave index),
+launch lifetime per tick, effective clock (cycles per tick x ticks / launch time)."""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "rl-project-heist-architect-adversarial-reinforcement-learning-framework-cse4019_amd")]
+import torch  # noqa: E402
+
+from heist_amd import EnvironmentConfig, HeistEnv  # noqa: E402
+from heist_amd import _native as nat  # noqa: E402
+
+SEGS = ["update+static", "wait_raycast_barrier", "raycast", "wait_raycast_end", "reward+reset", "obs_ch1+out",
+        "tick_end_barrier"]
+
+
+def main():
+    import bench
+    n = int(os.environ.get("PROBE_N", "4096"))
+    K = int(os.environ.get("PROBE_K", "20"))
+    env = HeistEnv(n, EnvironmentConfig(architect_budget=15), max_cams=5, max_guards=3, max_path=16, device="cuda")
+    bench.architect_layouts(env, 15, seed=1234)
+    env.reset()
+    W = nat.lib().heist_step_waves(env._h)
+    acts = torch.randint(0, 5, (4 * K, n), device="cuda")
+    for j in range(2):
+        env.step_multi(acts[j * K:(j + 1) * K])
+    buf = torch.zeros((n, W, 10), dtype=torch.int64, device="cuda")
+    out = {"n": n, "K": K, "waves": W, "launches": []}
+    for j in range(2, 4):
+        nat.check(nat.lib().heist_step_stamps(env._h, nat.ptr(buf)), "heist_step_stamps")
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ev0.record()
+        env.step_multi(acts[j * K:(j + 1) * K])
+        ev1.record()
+        nat.check(nat.lib().heist_step_stamps(env._h, None), "heist_step_stamps")
+        torch.cuda.synchronize()
+        s = buf.cpu().numpy().astype(np.int64)
+        rec = {"launch_ms": ev0.elapsed_time(ev1)}
+        for w in range(W):
+            rec["wave%d_cycles_per_tick" % w] = {nm: float(s[:, w, i].mean()) / K for i, nm in enumerate(SEGS)}
+        life = s[:, 0, 7]
+        rec["lifetime_cycles_per_tick"] = {"p10": float(np.percentile(life, 10)) / K, "p50": float(np.median(life)) / K,
+                                           "p90": float(np.percentile(life, 90)) / K, "max": float(life.max()) / K}
+        rec["effective_clock_ghz_from_max_lifetime"] = float(life.max()) / (rec["launch_ms"] * 1e6)
+        out["launches"].append(rec)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

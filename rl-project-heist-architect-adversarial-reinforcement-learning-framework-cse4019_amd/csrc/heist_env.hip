@@ -1277,31 +1277,76 @@ __device__ __forceinline__ void write_obs_static_lds(const EnvParams& p, const E
   }
 }
 
+// Channel 1 of observation row `o` plus the solver's quad of channel 2, stored by waves
+// 1.. only (wave 0 issues no observation stores, so waiting for its own loads never waits
+// for them: vmcnt counts loads and stores together, in issue order).  The solver's quad
+// belongs to the thread that stored channel 2's quad in write_obs_static_lds (program
+// order to one address).
+template <int NT>
+__device__ __forceinline__ void write_obs_ch1_tail(const EnvParams& p, const EnvScalars& s, const EnvLds& L, int cset,
+                                                   float* __restrict__ o) {
+  constexpr int PW = NT - 64;
+  const int t = (int)threadIdx.x - 64;
+  if (t < 0) return;
+  const int RC = p.RC, C = p.C, n4 = RC / 4, c4 = C / 4;
+  const int mc = p.max_cams, mg = p.max_guards;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(o, (short)0, 12 * RC, 0x00020000);
+  const int pol = p.obs_store;
+  for (int q = t; q < n4; q += PW) {
+    const int r = q / c4, c0 = 4 * (q - r * c4);
+    const int a = L.at(r, c0);
+    uint32_t v;
+    if ((kRing & 3) == 0) {
+      v = *reinterpret_cast<const uint32_t*>(L.vis + a);
+    } else {
+      const uint16_t* vp2 = reinterpret_cast<const uint16_t*>(L.vis + a);
+      v = (uint32_t)vp2[0] | ((uint32_t)vp2[1] << 16);
+    }
+    v |= cone_vis4(L, mc, mg, cset, r, c0);
+    obs_put(rs, pol, 16 * (n4 + q),
+            make_float4((float)(v & 0xff), (float)((v >> 8) & 0xff), (float)((v >> 16) & 0xff), (float)(v >> 24)));
+  }
+  const int solver = s.pos_r * C + s.pos_c, qs = solver >> 2;
+  if (qs % PW == t) {
+    const int vault = p.vr * C + p.vc;
+    float4 v = reinterpret_cast<const float4*>(p.plane0)[qs];
+    patch4(v, solver & 3, p.plane1[solver]);
+    if (qs == (vault >> 2)) patch4(v, vault & 3, p.vault_val);
+    obs_put(rs, pol, 16 * (2 * n4 + qs), v);
+  }
+}
+
 // K consecutive heist_step ticks of one env per workgroup (environment.py:216-299 and
 // :347-374 K times), with actions[k][env] known up front: what env-only throughput and
 // action replay need.  The per-env state stays on chip for the whole launch -- grid, stop
-// map, patrol paths, the static position plane and the K actions in LDS, camera and guard
-// records in the registers of wave 0's emitter lanes, the solver scalars in registers --
-// and is written back once at the end; every tick still writes its full observation row
-// (obs[k][env], non-temporal 16-byte stores), reward, done and status.  Per tick: wave 0
-// advances cameras and guards in registers and publishes the emitter table while waves
-// 1.. store the tick's static observation channels, barrier, raycast (all waves),
-// barrier, move / reward / detection / auto-reset / channel 1, and the next tick's cached
-// guard cone entries are loaded before channel 1 is stored (so that waiting for them does
-// not wait for those stores: vmcnt counts in issue order), to land during the barrier and
-// the next emitter update.  A finishing env loads its cached guards' reset cones (patrol
-// point 0, same heading) only then.  A cached guard's heading is the one its slot names;
-// it is read from the cone entry once, at the end.  Results are bit-identical to K
-// heist_step launches (tests/test_gpu_env.py).
+// map, patrol paths, the static position plane, the emitter records and the K actions in
+// LDS, the solver scalars in scalar registers -- and is written back once at the end;
+// every tick still writes its full observation row (obs[k][env], non-temporal 16-byte
+// stores), reward, done and status.  Per tick:
+//   A  every thread: the solver's move and the reward terms that precede detection
+//      (environment.py:235-269; they need the grid, not the visibility); wave 0: cameras
+//      and guards advance (security.py:49-51, :145-159), the cached guard cone entries
+//      loaded during the previous tick go to LDS, the emitter table is published; waves
+//      1..: the tick's static observation channels 0 and 2, the plane clears;
+//   barrier, raycast (all waves), barrier;
+//   C  every thread: detection, vault, timeout, auto-reset (environment.py:271-297,
+//      :183-214); wave 0: the next tick's cone entries are loaded (they land during the
+//      barrier and the next update), reward / done / status stored; waves 1..: channel 1.
+// Wave 0 issues no observation stores, so its wait for the cone entries is only for them.
+// A finishing env loads its cached guards' reset cones (patrol point 0, same heading) then;
+// a live-raycast guard off its start costs a second raycast pass from the reset poses.  A
+// cached guard's heading is the one its slot names: read from a cone entry once, at the
+// end.  Results are bit-identical to K heist_step launches (tests/test_gpu_env.py).
 template <int W, int U, int O, int D, bool STAMP = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) void step_multi_kernel(
     EnvParams p, int K, const int64_t* __restrict__ actions, float* __restrict__ obs, float* __restrict__ rew,
     double* __restrict__ rew64, uint8_t* __restrict__ done_out, int8_t* __restrict__ status_out, int auto_reset) {
   constexpr int NT = 64 * W;
-  static_assert(W >= 2, "channels 0/2 are stored by the waves after wave 0");
+  static_assert(W >= 2, "the observation is stored by the waves after wave 0");
   extern __shared__ __align__(16) unsigned char smem[];
   const int e = p.dispatch_order ? p.order[blockIdx.x] : (int)blockIdx.x;
   const int t = threadIdx.x;
+  const bool w0 = (t >> 6) == 0;
   const int RC = p.RC, N = p.n_envs;
   const int mc = p.max_cams, mg = p.max_guards, n_slot = mc + mg;
   const int path_words = mg * p.max_path;
@@ -1312,19 +1357,19 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   uint8_t* act = reinterpret_cast<uint8_t*>(rec + n_slot);
   const EnvBase eb = env_base(p, e);
   // STAMP (instrumentation, heist_step_stamps): lane 0 of every wave sums the shader clock
-  // spent in each of 7 tick segments over the launch into LDS (after the K actions), and
-  // writes [segment sums 0..6, launch lifetime, HW_ID, XCC_ID] to stamps[env][wave][10]
+  // spent in each of 9 tick segments over the launch into LDS (after the K actions), and
+  // writes [segment sums 0..8, launch lifetime] to stamps[env][wave][10]
   unsigned long long* st_acc = reinterpret_cast<unsigned long long*>(act + align16((size_t)K));
   unsigned long long st_last = 0, st_start = 0;
   if (STAMP && (t & 63) == 0) {
     st_start = st_last = __builtin_amdgcn_s_memtime();
-    for (int j = 0; j < 7; ++j) st_acc[(t >> 6) * 8 + j] = 0;
+    for (int j = 0; j < 9; ++j) st_acc[(t >> 6) * 10 + j] = 0;
   }
 #define HEIST_MULTI_STAMP(seg)                                                  \
   do {                                                                          \
     if (STAMP && (threadIdx.x & 63) == 0) {                                     \
       const unsigned long long now_ = __builtin_amdgcn_s_memtime();             \
-      st_acc[(threadIdx.x >> 6) * 8 + (seg)] += now_ - st_last;                 \
+      st_acc[(threadIdx.x >> 6) * 10 + (seg)] += now_ - st_last;                \
       st_last = now_;                                                           \
     }                                                                           \
   } while (0)
@@ -1333,7 +1378,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   {
     EmitterRaw raw;
     prefetch<NT>(p, e, eb, L, raw);
-    if (t < n_slot) rec[t] = raw;  // the emitter records live in LDS between ticks
+    if (t < n_slot) rec[t] = raw;
   }
   for (int i = t; i < path_words; i += NT) L.path[i] = eb.paths[i];
   for (int i = t; i < RC; i += NT) plane[i] = p.plane0[i];
@@ -1349,7 +1394,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   // its move (idx + step, nslot) if the env acts and the patrol has >= 2 points
   // (security.py:147), else the pose it holds
   uint4 ca = make_uint4(0u, 0u, 0u, 0u), cb = ca;
-  auto next_entry = [&](const EnvBase& eb, const Guard& gd, bool acts) {
+  auto next_entry = [&](const Guard& gd, bool acts) {
     int idx = gd.idx, slot = gd.hslot;
     if (acts && gd.len >= 2) {
       idx += gd.step;
@@ -1365,7 +1410,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     const Guard gd = as_guard(rec[t]);
     cached = gd.hslot != kUncached;
     L.rpos[g] = gd.pos0;
-    if (cached) next_entry(eb, gd, !s.done);
+    if (cached) next_entry(gd, !s.done);
   }
 
   // Tick k is one or two raycast passes: pass 0 the tick itself; pass 1 only when the env
@@ -1375,112 +1420,123 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   bool reset_pass = false;
   double reward = 0.0;
   int status = kAlreadyDone, done_now = 0;
+  bool act_now = true;
+  int curr = 0;
   while (k < K) {
-    const int mc = p.max_cams, mg = p.max_guards, n_slot = mc + mg;
-    const EnvLds L = carve<D>(smem, p.R, p.C, n_slot, mg * p.max_path, W, mg);
-    float* plane = reinterpret_cast<float*>(smem + align16(env_lds_bytes(p.R, p.C, n_slot, mg * p.max_path, D, W, mg)));
-    EmitterRaw* rec = reinterpret_cast<EmitterRaw*>(reinterpret_cast<unsigned char*>(plane) +
-                                                    align16(sizeof(float) * (size_t)p.RC));
-    const uint8_t* act = reinterpret_cast<const uint8_t*>(rec + n_slot);
-    const EnvBase eb = env_base(p, e);
-    const int RC = p.RC, N = p.n_envs;
     __syncthreads();  // the previous pass's readers of vis / em / meta / cones are done
-    HEIST_MULTI_STAMP(6);  // 6: end of the previous tick's stores -> through the top barrier
+    HEIST_MULTI_STAMP(8);  // 8: end of the previous tick -> through the top barrier
     Emit E;
     E.kind = -1;
-    const bool act_now = !s.done;
     if (!reset_pass) {
-      if (t == 0) L.meta[5] = 0;
-      // 2. cameras rotate, guards patrol (security.py:49-51, :145-159)
-      if (live_cam) {
-        Cam cm = as_cam(rec[t]);
-        if (act_now) {
-          cm.heading = py_mod360(cm.heading + cm.speed * 1.0);
-          rec[t] = __builtin_bit_cast(EmitterRaw, cm);
-        }
-        E = cam_emit(cm);
-      } else if (live_guard) {
-        Guard gd = as_guard(rec[t]);
-        const bool moves = act_now && gd.len >= 2;
-        int nidx = gd.idx;
-        if (moves) {
-          nidx += gd.step;
-          if (nidx >= gd.len) nidx -= gd.len;
-        }
-        const uint16_t np = moves ? L.path[__umul24((uint32_t)g, (uint32_t)p.max_path) + (uint32_t)nidx] : gd.pos;
-        if (cached) {
-          if (moves) gd.hslot = gd.nslot;
-          gd.nslot = (uint8_t)(cb.w >> 16);  // row 15: the slot after the next move
-          uint4* dst = reinterpret_cast<uint4*>(L.cone + 16 * g);
-          dst[0] = ca;
-          dst[1] = cb;
-        } else if (moves) {
-          gd.heading = guard_heading_after(p, unpack_r(np) - unpack_r(gd.pos), unpack_c(np) - unpack_c(gd.pos),
-                                           gd.heading);
-        }
-        gd.idx = (int16_t)nidx;
-        gd.pos = np;
-        if (gd.pos != gd.pos0) atomicOr(reinterpret_cast<unsigned int*>(&L.meta[5]), cached ? 2u : 1u);
-        rec[t] = __builtin_bit_cast(EmitterRaw, gd);
-        E = guard_emit(gd);
-      }
-      write_obs_static_lds<NT>(p, L, plane, obs + ((size_t)k * N + e) * 3 * RC);
-    } else {  // the emitters with every guard back at patrol point 0, headings kept
-      if (live_cam) E = cam_emit(as_cam(rec[t]));
-      if (live_guard) {
-        E = guard_emit(as_guard(rec[t]));
-        if (cached) {
-          uint4* dst = reinterpret_cast<uint4*>(L.cone + 16 * g);
-          const uint4* srcr = reinterpret_cast<const uint4*>(L.cone + 16 * (mg + g));
-          dst[0] = srcr[0];
-          dst[1] = srcr[1];
-        }
-      }
-    }
-    clear_vis<NT>(p, L);
-    publish_emitters(L, E, n_slot);
-    HEIST_MULTI_STAMP(0);  // 0: emitter update, static channels, clears
-    __syncthreads();  // emitter table, cone rows, cleared vis
-    HEIST_MULTI_STAMP(1);  // 1: waiting at the raycast barrier
-    // 3. visibility (environment.py:257-258)
-    if (live_guard && E.kind == 1) L.vis[L.at(E.row, E.col)] = 1;  // visibility.py:59
-    cast_rays<NT, U, D, false>(smem, L, p.ray_mode, 0, p.half_deg);
-    HEIST_MULTI_STAMP(2);  // 2: raycast
-    __syncthreads();  // vis complete
-    HEIST_MULTI_STAMP(3);  // 3: waiting for the other waves' raycast
-
-    int cset = 0;
-    if (!reset_pass) {
+      act_now = !s.done;
       reward = 0.0;
       status = kAlreadyDone;
       if (act_now) {
-        // 1. move (environment.py:239-246)
+        // 1. move (environment.py:239-246): needs the grid, not this tick's visibility
         const int a = act[k];
         const int nr = s.pos_r + (a == 1 ? -1 : (a == 2 ? 1 : 0)), nc = s.pos_c + (a == 3 ? -1 : (a == 4 ? 1 : 0));
         if (nr >= 0 && nr < p.R && nc >= 0 && nc < p.C && L.grid[nr * p.C + nc] != kWall) {
           s.pos_r = nr;
           s.pos_c = nc;
         }
-        // 4-5. shaping, detection, vault, timeout (environment.py:235, :261-297); the
-        // float64 reward on wave 0 only (thread 0 stores it)
-        const bool rw = (threadIdx.x >> 6) == 0;
+        s.pos_r = uni(s.pos_r);
+        s.pos_c = uni(s.pos_c);
+        // 4. shaping and proximity (environment.py:235, :261-269); the float64 reward on
+        // wave 0 only (thread 0 stores it); detection, vault and timeout follow the raycast
         status = kRunning;
-        const int curr = iabs_(s.pos_r - p.vr) + iabs_(s.pos_c - p.vc);
-        if (rw) {
+        curr = iabs_(s.pos_r - p.vr) + iabs_(s.pos_c - p.vc);
+        if (w0) {
           reward = p.r_step;
           reward += (double)(s.prev_dist - curr) * 0.1;
           if (curr <= 3 && s.initial_dist > 3) reward += 0.05 * (double)(3 - curr);
         }
         s.prev_dist = curr;
+      }
+      HEIST_MULTI_STAMP(0);  // 0: the solver's move, shaping reward
+      if (w0) {
+        if (t == 0) L.meta[5] = 0;
+        // 2. cameras rotate, guards patrol (security.py:49-51, :145-159)
+        if (live_cam) {
+          Cam cm = as_cam(rec[t]);
+          if (act_now) {
+            cm.heading = py_mod360(cm.heading + cm.speed * 1.0);
+            rec[t] = __builtin_bit_cast(EmitterRaw, cm);
+          }
+          E = cam_emit(cm);
+        } else if (live_guard) {
+          Guard gd = as_guard(rec[t]);
+          const bool moves = act_now && gd.len >= 2;
+          int nidx = gd.idx;
+          if (moves) {
+            nidx += gd.step;
+            if (nidx >= gd.len) nidx -= gd.len;
+          }
+          const uint16_t np = moves ? L.path[__umul24((uint32_t)g, (uint32_t)p.max_path) + (uint32_t)nidx] : gd.pos;
+          if (cached) {
+            if (moves) gd.hslot = gd.nslot;
+            gd.nslot = (uint8_t)(cb.w >> 16);  // row 15: the slot after the next move
+            uint4* dst = reinterpret_cast<uint4*>(L.cone + 16 * g);
+            dst[0] = ca;
+            dst[1] = cb;
+          } else if (moves) {
+            gd.heading = guard_heading_after(p, unpack_r(np) - unpack_r(gd.pos), unpack_c(np) - unpack_c(gd.pos),
+                                             gd.heading);
+          }
+          gd.idx = (int16_t)nidx;
+          gd.pos = np;
+          if (gd.pos != gd.pos0) atomicOr(reinterpret_cast<unsigned int*>(&L.meta[5]), cached ? 2u : 1u);
+          rec[t] = __builtin_bit_cast(EmitterRaw, gd);
+          E = guard_emit(gd);
+        }
+        HEIST_MULTI_STAMP(1);  // 1: emitter update (wave 0)
+        publish_emitters(L, E, n_slot);
+      } else {
+        write_obs_static_lds<NT>(p, L, plane, obs + ((size_t)k * N + e) * 3 * RC);
+        HEIST_MULTI_STAMP(1);  // 1: static channels (waves 1..)
+        uint32_t* v4 = reinterpret_cast<uint32_t*>(L.vis);
+        for (int i = t - 64; i < (padded_bytes(p.R, p.C) + 3) / 4; i += NT - 64) v4[i] = 0u;
+      }
+    } else {  // the emitters with every guard back at patrol point 0, headings kept
+      if (w0) {
+        if (live_cam) E = cam_emit(as_cam(rec[t]));
+        if (live_guard) {
+          E = guard_emit(as_guard(rec[t]));
+          if (cached) {
+            uint4* dst = reinterpret_cast<uint4*>(L.cone + 16 * g);
+            const uint4* srcr = reinterpret_cast<const uint4*>(L.cone + 16 * (mg + g));
+            dst[0] = srcr[0];
+            dst[1] = srcr[1];
+          }
+        }
+        publish_emitters(L, E, n_slot);
+      } else {
+        uint32_t* v4 = reinterpret_cast<uint32_t*>(L.vis);
+        for (int i = t - 64; i < (padded_bytes(p.R, p.C) + 3) / 4; i += NT - 64) v4[i] = 0u;
+      }
+    }
+    HEIST_MULTI_STAMP(2);  // 2: publish (wave 0), clears (waves 1..)
+    __syncthreads();  // emitter table, cone rows, cleared vis
+    HEIST_MULTI_STAMP(3);  // 3: waiting at the raycast barrier
+    // 3. visibility (environment.py:257-258)
+    if (live_guard && E.kind == 1) L.vis[L.at(E.row, E.col)] = 1;  // visibility.py:59
+    cast_rays<NT, U, D, false>(smem, L, p.ray_mode, 0, p.half_deg);
+    HEIST_MULTI_STAMP(4);  // 4: raycast
+    __syncthreads();  // vis complete
+    HEIST_MULTI_STAMP(5);  // 5: waiting for the other waves' raycast
+
+    int cset = 0;
+    if (!reset_pass) {
+      if (act_now) {
+        // 5. detection, vault, timeout (environment.py:271-297), in the reference's order
         if (L.vis[L.at(s.pos_r, s.pos_c)] | (cone_vis4(L, mc, mg, 0, s.pos_r, s.pos_c) & 1u)) {
           s.detected = 1;
-          if (rw) reward += p.r_detect;
+          if (w0) reward += p.r_detect;
           s.done = 1;
           status = kDetected;
         }
         if (s.pos_r == p.vr && s.pos_c == p.vc) {
           s.vault_reached = 1;
-          if (rw) reward += p.r_vault;
+          if (w0) reward += p.r_vault;
           s.done = 1;
           status = kVaultReached;
         }
@@ -1488,17 +1544,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
         if (s.tick >= p.max_steps) {
           s.done = 1;
           status = kTimeout;
-          if (rw) {
+          if (w0) {
             double frac = 1.0 - (double)curr / (double)(s.initial_dist > 1 ? s.initial_dist : 1);
             if (frac < 0.0) frac = 0.0;
             reward += frac * 2.0;
           }
         }
       }
-      s.pos_r = uni(s.pos_r);  // block-uniform state in scalar registers
-      s.pos_c = uni(s.pos_c);
-      s.prev_dist = uni(s.prev_dist);
-      s.done = uni(s.done);
+      s.done = uni(s.done);  // block-uniform state in scalar registers
       s.detected = uni(s.detected);
       s.vault_reached = uni(s.vault_reached);
       s.tick = uni(s.tick);
@@ -1534,34 +1587,29 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
       }
     }
     reset_pass = false;
-    HEIST_MULTI_STAMP(4);  // 4: move, reward, detection, auto-reset
-    if (live_guard && cached && k + 1 < K) next_entry(eb, as_guard(rec[t]), !s.done);  // lands during the next update
-    write_obs_dynamic<NT>(p, e, s, L, cset, obs + (size_t)k * N * 3 * RC);
-    if (t == 0) {
-      const size_t ko = (size_t)k * N + e;
-      rew[ko] = (float)reward;
-      if (rew64) rew64[ko] = reward;
-      done_out[ko] = (uint8_t)done_now;
-      status_out[ko] = (int8_t)status;
+    HEIST_MULTI_STAMP(6);  // 6: detection, vault, timeout, auto-reset
+    if (w0) {
+      if (live_guard && cached && k + 1 < K) next_entry(as_guard(rec[t]), !s.done);  // lands during the next update
+      if (t == 0) {
+        const size_t ko = (size_t)k * N + e;
+        rew[ko] = (float)reward;
+        if (rew64) rew64[ko] = reward;
+        done_out[ko] = (uint8_t)done_now;
+        status_out[ko] = (int8_t)status;
+      }
+    } else {
+      write_obs_ch1_tail<NT>(p, s, L, cset, obs + ((size_t)k * N + e) * 3 * RC);
     }
-    HEIST_MULTI_STAMP(5);  // 5: channel 1 + solver quad, outputs
+    HEIST_MULTI_STAMP(7);  // 7: channel 1 + solver quad (waves 1..), outputs (wave 0)
     ++k;
   }
 #undef HEIST_MULTI_STAMP
   // epilogue: the state the next launch (or heist_export) starts from
-  {
-  const int mc = p.max_cams, mg = p.max_guards, n_slot = mc + mg;
-  const EnvBase eb = env_base(p, e);
-  float* plane = reinterpret_cast<float*>(smem + align16(env_lds_bytes(p.R, p.C, n_slot, mg * p.max_path, D, W, mg)));
-  const EmitterRaw* rec = reinterpret_cast<const EmitterRaw*>(reinterpret_cast<unsigned char*>(plane) +
-                                                              align16(sizeof(float) * (size_t)p.RC));
   if (t == 0) p.scal[e] = s;
   if (STAMP && (t & 63) == 0) {
     unsigned long long* q = p.stamps + ((size_t)e * W + (t >> 6)) * 10;
-    for (int j = 0; j < 7; ++j) q[j] = st_acc[(t >> 6) * 8 + j];
-    q[7] = __builtin_amdgcn_s_memtime() - st_start;
-    q[8] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
-    q[9] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+    for (int j = 0; j < 9; ++j) q[j] = st_acc[(t >> 6) * 10 + j];
+    q[9] = __builtin_amdgcn_s_memtime() - st_start;
   }
   if (live_cam) eb.cams[(uint32_t)t].heading = as_cam(rec[t]).heading;
   if (live_guard) {
@@ -1576,7 +1624,6 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     gp->pos = gd.pos;
     gp->hslot = gd.hslot;
     gp->nslot = gd.nslot;
-  }
   }
 }
 
@@ -2171,7 +2218,7 @@ size_t step_multi_lds(const EnvParams& p, int K) {
   const int n_slot = p.max_cams + p.max_guards;
   return align16(env_lds_bytes(p.R, p.C, n_slot, p.max_guards * p.max_path, p.vis_gap, p.step_waves, p.max_guards)) +
          align16(sizeof(float) * (size_t)p.RC) + 32 * (size_t)n_slot + align16((size_t)K) +
-         (p.stamps ? 64 * (size_t)p.step_waves : 0);
+         (p.stamps ? 80 * (size_t)p.step_waves : 0);
 }
 
 hipError_t launch_step_multi(const EnvParams& p, const EnvParams* pg, int K, const int64_t* actions, float* obs,

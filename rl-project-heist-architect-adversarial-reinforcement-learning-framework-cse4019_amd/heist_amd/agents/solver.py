@@ -272,6 +272,50 @@ class SolverAgent:  # agents/solver.py:18-259
         m["solver_samples"] = n
         return m
 
+    def layout_batch_advantages(self, ro: Rollout, sel: torch.Tensor):
+        """The reference's per-layout buffer statistics for a layout-batch rollout
+        (agents/solver.py:142-147 for every env at once): GAE per env column with bootstrap 0
+        (each env's selected ticks end with its A-th done, so its buffer's GAE is the
+        column's up to there), returns = adv + values, then the advantages normalised over
+        each env's selected samples with the unbiased std (+ 1e-8), a buffer of one sample
+        left as is.  Returns (adv_norm, ret, env_index, tick_index) of the selected samples,
+        env-major, in time order within an env."""
+        T, N = ro.rewards.shape
+        adv, ret = compute_gae(ro.rewards, ro.values, ro.dones, None, self.gamma, self.gae_lambda)
+        m = sel.clone()
+        if ro.mask is not None:
+            m &= ro.mask.reshape(1, N)
+        idx = m.t().nonzero()  # [n, 2] (env, tick), env-major
+        e_i, t_i = idx[:, 0], idx[:, 1]
+        a = adv[t_i, e_i]
+        cnt = torch.zeros(N, dtype=torch.float64, device=a.device).index_add_(0, e_i, torch.ones_like(a, dtype=torch.float64))
+        s1 = torch.zeros(N, dtype=torch.float64, device=a.device).index_add_(0, e_i, a.double())
+        mean = s1 / cnt.clamp(min=1)
+        dev2 = (a.double() - mean[e_i]) ** 2
+        s2 = torch.zeros(N, dtype=torch.float64, device=a.device).index_add_(0, e_i, dev2)
+        std = (s2 / (cnt - 1).clamp(min=1)).sqrt()
+        an = ((a.double() - mean[e_i]) / (std[e_i] + 1e-8)).float()
+        an = torch.where(cnt[e_i] > 1, an, a)
+        return an, ret[t_i, e_i], e_i, t_i
+
+    def update_layout_batch(self, ro: Rollout, sel: torch.Tensor, minibatch: int = 4096) -> Dict[str, float]:
+        """One PPO update on a layout-batch rollout (AdversarialTrainer solver_cadence=
+        "layout_batch"): the selected transitions of every env's A attempts, per-layout GAE
+        and advantage normalisation (layout_batch_advantages), then the clipped update of
+        _ppo_epochs (collective inside a process group, as update_rollout)."""
+        an, ret, e_i, t_i = self.layout_batch_advantages(ro, sel)
+        self.last_layout_batch = (an, ret, e_i, t_i)
+        n = int(an.shape[0])
+        if n == 0 and not dist_utils.is_multi():
+            return {"solver_loss": 0.0}
+        states = ro.obs[t_i, e_i]
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(int(torch.randint(0, 2 ** 31, (1,)).item()))
+        perm = lambda k: torch.randperm(k, device=self.device, generator=gen)  # noqa: E731
+        m = self._ppo_epochs(states, ro.actions[t_i, e_i], ro.logp[t_i, e_i], an, ret, n, perm, minibatch=minibatch)
+        m["solver_samples"] = n
+        return m
+
     # -- checkpoints ---------------------------------------------------------------------
     def save(self, path: str):  # agents/solver.py:246-252 dict format
         torch.save({"network": self.network.state_dict(), "optimizer": self.optimizer.state_dict(),

@@ -140,7 +140,8 @@ class AdversarialTrainer:  # training.py:115-790
                  architect_lr: float = 3e-4, solver_lr: float = 1e-3, n_envs: int = 256,
                  rollout_len: Optional[int] = None, minibatch: int = 4096, device=None, max_budget: Optional[int] = None,
                  seed: Optional[int] = None, update_precision: str = "fp32", rollout_precision: str = "fp32",
-                 curriculum: Union[str, Sequence[Tuple], None] = None, architect_update: str = "per_layout"):
+                 curriculum: Union[str, Sequence[Tuple], None] = None, architect_update: str = "per_layout",
+                 solver_cadence: str = "rollout"):
         self.config = config or EnvironmentConfig()
         self.solver_episodes = solver_episodes_per_layout
         self.total_episodes = total_episodes
@@ -159,6 +160,14 @@ class AdversarialTrainer:  # training.py:115-790
         if architect_update not in ("batched", "per_layout"):
             raise ValueError("architect_update must be 'batched' or 'per_layout'")
         self.architect_update = architect_update
+        # "rollout": one Solver update per rollout_len-tick window (V(s_T) bootstrap where the
+        # window cuts an attempt); "layout_batch": the reference's cadence (training.py:515-565)
+        # for all envs at once -- every env plays its layout's A attempts to done, then one
+        # update on exactly those transitions, GAE bootstrapping 0 at each env's buffer end and
+        # advantages normalised per layout buffer (agents/solver.py:142-147)
+        if solver_cadence not in ("rollout", "layout_batch"):
+            raise ValueError("solver_cadence must be 'rollout' or 'layout_batch'")
+        self.solver_cadence = solver_cadence
         if seed is not None:  # one stream per rank: ranks must not replay each other's layouts and actions
             torch.manual_seed(seed + dist_utils.rank())
             np.random.seed(seed + dist_utils.rank())
@@ -335,6 +344,49 @@ class AdversarialTrainer:  # training.py:115-790
         return Rollout(obs_buf, act_buf, lp_buf, v_buf, r_buf, d_buf, mask=self.b_valid.clone(),
                        last_value=last_value)
 
+    @torch.no_grad()
+    def _rollout_layout_batch(self) -> Tuple[Rollout, torch.Tensor]:
+        """Play until every valid env has finished its layout's A attempts (at most
+        A * max_steps ticks; the loop checks every 16 ticks).  Returns the [T, N] rollout and
+        sel [T, N] bool: the transitions of each env's A attempts -- the reference's per-layout
+        buffer (training.py:515-544) -- in time order; later ticks (an env waiting for the
+        others, auto-reset into attempt A + 1) are not selected."""
+        env, n, d = self.env, self.n_envs, self.device
+        A = self.solver_episodes
+        T_max = A * self.config.max_steps
+        vault, det = STATUS_CODES["vault_reached"], STATUS_CODES["detected"]
+        bufs = {k: [] for k in ("obs", "act", "lp", "v", "r", "d", "sel")}
+        obs = env.obs.clone()
+        t = 0
+        while t < T_max:
+            counting = self.b_valid & (self.b_attempts < A)
+            if t % 16 == 0 and not bool(counting.any()):
+                break
+            a, lp, v, (self.h, self.c) = self.solver.act(obs, (self.h, self.c))
+            nxt, rew, done, status = env.step(a)
+            for k, x in (("obs", obs), ("act", a), ("lp", lp), ("v", v), ("r", rew.clone()),
+                         ("d", done.to(torch.uint8)), ("sel", counting)):
+                bufs[k].append(x)
+            if self._trace is not None:
+                self._trace.append((a.clone(), env.reward64.clone(), done.clone(), status.clone()))
+            self.b_steps += counting.int()
+            self.b_reward += torch.where(counting, env.reward64, torch.zeros_like(self.b_reward))
+            fin = counting & done
+            st = status.to(torch.int32)
+            self.b_solve += (fin & (st == vault)).int()
+            self.b_detect += (fin & (st == det)).int()
+            self.b_timeout += (fin & (st != vault) & (st != det)).int()
+            self.b_attempts += fin.int()
+            keep = (~done).to(self.h.dtype).reshape(1, n, 1)  # solver.reset() per attempt (training.py:517)
+            self.h = self.h * keep
+            self.c = self.c * keep
+            obs = nxt.clone()
+            t += 1
+        st = {k: torch.stack(v) for k, v in bufs.items()}
+        ro = Rollout(st["obs"], st["act"], st["lp"], st["v"], st["r"], st["d"], mask=self.b_valid.clone(),
+                     last_value=None)
+        return ro, st["sel"]
+
     def _score_finished(self, overrides: Optional[dict] = None) -> np.ndarray:
         """Score every env whose layout has had its A attempts; returns those env ids."""
         A = self.solver_episodes
@@ -409,10 +461,18 @@ class AdversarialTrainer:  # training.py:115-790
         """One rollout of rollout_len ticks over all envs + the agents' updates.
         Collective inside a process group (every rank calls it with the same overrides)."""
         ov = overrides or {}
-        ro = self._rollout(self.rollout_len)
         out = {}
-        if not ov.get("freeze_solver", False):
-            out.update(self.solver.update_rollout(ro, minibatch=self.minibatch))
+        if self.solver_cadence == "layout_batch":
+            ro, sel = self._rollout_layout_batch()
+            if self._trace is not None:  # kept for parity tests
+                self._last_layout_batch = (ro, sel)
+            if not ov.get("freeze_solver", False):
+                out.update(self.solver.update_layout_batch(ro, sel, minibatch=self.minibatch))
+            out["rollout_ticks"] = int(ro.rewards.shape[0])
+        else:
+            ro = self._rollout(self.rollout_len)
+            if not ov.get("freeze_solver", False):
+                out.update(self.solver.update_rollout(ro, minibatch=self.minibatch))
         done_ids = self._score_finished(ov)
         if not self.warmup and not ov.get("freeze_architect", False):
             out.update(self._architect_step())

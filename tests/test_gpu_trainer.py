@@ -170,6 +170,46 @@ def test_interactive_episodes_mask_training_envs(gpu_device, tmp_path):
     assert tr.b_valid.any()  # training resumes on every env afterwards
 
 
+def test_layout_batch_cadence_reference_buffers(gpu_device, tmp_path):
+    """solver_cadence="layout_batch" (SURVEY 8 a20's parity mode): every env plays its
+    layout's A attempts to done, and the one Solver update runs on exactly those
+    transitions -- the reference's per-layout buffer (training.py:515-565) -- with GAE
+    bootstrapping 0 at the buffer end and advantages normalised over the buffer
+    (agents/solver.py:142-147, :228-244): equal to the oracle's GAE over each env's
+    concatenated attempts, normalised in float32, within 1e-5; no V(s_T) bootstrap."""
+    A = 3
+    tr = _trainer(tmp_path, 24, R=12, T=40, A=A, device=gpu_device, minibatch=512, solver_cadence="layout_batch")
+    ids = np.nonzero(tr.b_valid.cpu().numpy())[0]
+    assert len(ids) >= 12
+    from trainer_replay import oracle_envs
+    envs = oracle_envs(tr, ids)
+    tr._trace = []
+    out = tr.train_iteration()
+    assert replay(tr, ids, tr._trace, envs) == out["rollout_ticks"] * len(ids)
+    ro, sel = tr._last_layout_batch
+    assert ro.last_value is None  # bootstrap 0
+    an, ret, e_i, t_i = (x.cpu().numpy() for x in tr.solver.last_layout_batch)
+    r, v, d, s = (x.cpu().numpy() for x in (ro.rewards, ro.values, ro.dones, sel))
+    assert out["solver_samples"] == len(an) == int(s[:, ids].sum())
+    assert out["layouts_scored"] == len(ids)
+    for e in ids:
+        rows = np.nonzero(s[:, e])[0]
+        assert len(rows) and rows[0] == 0 and np.all(np.diff(rows) == 1)  # one contiguous buffer from tick 0
+        de = d[rows, e]
+        assert de[-1] == 1 and int(de.sum()) == A  # exactly A attempts, the last one ended
+        ref = po.gae(r[rows, e], v[rows, e], de)
+        mine = e_i == e
+        np.testing.assert_array_equal(t_i[mine], rows)
+        np.testing.assert_allclose(ret[mine], ref + v[rows, e], rtol=0, atol=1e-5)
+        if len(ref) > 1:
+            ref32 = ref.astype(np.float32)
+            refn = (ref32 - ref32.mean(dtype=np.float32)) / (np.float32(ref32.std(ddof=1, dtype=np.float32)) + np.float32(1e-8))
+        else:
+            refn = ref
+        np.testing.assert_allclose(an[mine], refn, rtol=0, atol=1e-5)
+    assert np.isfinite(out["solver_policy_loss"])
+
+
 def test_interactive_episodes_more_than_envs(gpu_device, tmp_path):
     """num_episodes > n_envs: the layouts are played in blocks of n_envs, every one of them."""
     tr = _trainer(tmp_path, 6, R=10, T=30, A=1, device=gpu_device, minibatch=256)

@@ -43,6 +43,7 @@ for s in ${STEPS:-pytest smoke bench prof}; do
          step pmc_sq2_m 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d "$OUT/pmc_sq2_m" -o heist --output-format csv -- python3 bench.py --steps 60 --warmup 20 --no-cpu-baseline --no-secondary
          python tools/pmc_summary.py "$(find "$OUT/pmc_sq_m" -name "*counter_collection.csv" | head -n 1)" step_multi_kernel "$OUT/pmc_sq_m.json" > /dev/null 2>&1
          python tools/pmc_summary.py "$(find "$OUT/pmc_sq2_m" -name "*counter_collection.csv" | head -n 1)" step_multi_kernel "$OUT/pmc_sq2_m.json" > /dev/null 2>&1; true ;;
+    lbtest) step pytest_lb 600 python -u -m pytest tests/test_gpu_trainer.py -k "layout_batch or interactive or c3" -x -v --timeout 500 --timeout-method thread ;;
     benchtest) step pytest_bench 900 python -u -m pytest tests/test_gpu_bench.py -x -v --timeout 800 --timeout-method thread ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o heist --output-format csv -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-secondary ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary

@@ -1,8 +1,6 @@
 """Where does a heist_step_multi launch spend its time?  The STAMP variant of the K-tick
 kernel (heist_step_stamps armed) sums the shader clock each wave spends in 7 tick segments
-over the launch: 0 emitter update + static channels + clears, 1 wait at the raycast
-barrier, 2 raycast, 3 wait for the other waves' raycast, 4 move/reward/detection/
-auto-reset, 5 channel 1 + outputs, 6 end of tick -> through the top barrier.  Workload:
+over the launch (SEGS below; "a|b": wave 0 does a, waves 1.. do b).  Workload:
 bench.py's headline (4096 envs, C2 checkpoint layouts, K ticks per launch).
 
 Prints one JSON line: per-segment cycles per tick (mean over waves, by wave index),
@@ -20,8 +18,8 @@ import torch  # noqa: E402
 from heist_amd import EnvironmentConfig, HeistEnv  # noqa: E402
 from heist_amd import _native as nat  # noqa: E402
 
-SEGS = ["update+static", "wait_raycast_barrier", "raycast", "wait_raycast_end", "reward+reset", "obs_ch1+out",
-        "tick_end_barrier"]
+SEGS = ["move+shaping", "emitters|static", "publish|clear", "wait_raycast_barrier", "raycast", "wait_raycast_end",
+        "detect+reset", "out|ch1", "tick_end_barrier"]
 
 
 def main():
@@ -49,7 +47,7 @@ def main():
         rec = {"launch_ms": ev0.elapsed_time(ev1)}
         for w in range(W):
             rec["wave%d_cycles_per_tick" % w] = {nm: float(s[:, w, i].mean()) / K for i, nm in enumerate(SEGS)}
-        life = s[:, 0, 7]
+        life = s[:, 0, 9]
         rec["lifetime_cycles_per_tick"] = {"p10": float(np.percentile(life, 10)) / K, "p50": float(np.median(life)) / K,
                                            "p90": float(np.percentile(life, 90)) / K, "max": float(life.max()) / K}
         rec["effective_clock_ghz_from_max_lifetime"] = float(life.max()) / (rec["launch_ms"] * 1e6)

@@ -121,16 +121,18 @@ int heist_count_redo(heist_t h, uint64_t* counter);
  * table published, 3 raycast done, 4 reward done, 5 auto-reset done, 6 observation written,
  * 7 exit.  NULL switches stamping off (default). */
 int heist_step_stamps(heist_t h, uint64_t* buf);
+/* (heist_step_multi with stamps armed writes buf[env][multi_waves][16] instead: clock
+ * cycles summed per tick segment 0..8 over the launch, lifetime, start clock, HW_ID, XCC_ID.) */
 
 /* Wavefronts per env of h's step / reset kernels (2 unless HEIST_STEP_WAVES chose 1 or 4
  * at heist_create); no reference counterpart. */
 int heist_step_waves(heist_t h);
 
 /* The handle's effective kernel configuration, no reference counterpart (what a benchmark
- * records next to its numbers): out[0..n) with n <= 10 receives step_waves, ray_chunk,
+ * records next to its numbers): out[0..n) with n <= 11 receives step_waves, ray_chunk,
  * step_occ, vis_gap, obs_store, ray_mode, probe_mode, dispatch_order, split_obs,
- * guard_cones (the HEIST_* environment knobs as heist_create resolved them, then any
- * heist_set_* calls).  probe_mode != 0 selects the profiling step kernel, whose results are
+ * guard_cones, multi_waves (the HEIST_* environment knobs as heist_create resolved them,
+ * then any heist_set_* calls).  probe_mode != 0 selects the profiling step kernel, whose results are
  * wrong by design (phases skipped). */
 int heist_get_config(heist_t h, int32_t* out, int n);
 

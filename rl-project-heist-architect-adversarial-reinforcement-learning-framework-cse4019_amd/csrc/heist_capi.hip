@@ -32,6 +32,7 @@ hipError_t launch_bfs(const int32_t* grid, int n, int R, int C, int sr, int sc, 
 int vis_gap_for(int R, int C);
 int stop_map_bytes(int R, int C);
 bool env_variant_exists(int W, int U, int O, int D);
+bool multi_variant_exists(int W, int U, int O, int D);
 hipError_t launch_cone_order(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
                              uint32_t* keys_out, hipStream_t st);
 hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
@@ -219,6 +220,15 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
     p.step_occ = 8;
     p.vis_gap = heist::vis_gap_for(R, C);
   }
+  // K-tick kernel: the step kernel's waves per env unless HEIST_MULTI_WAVES says otherwise
+  // (1 wave per env runs at 4 waves per SIMD with 128 VGPRs)
+  p.multi_waves = p.step_waves;
+  if (const char* m = getenv("HEIST_MULTI_WAVES")) p.multi_waves = atoi(m);
+  p.multi_occ = p.multi_waves == 1 ? 4 : 8;
+  if (!heist::multi_variant_exists(p.multi_waves, p.ray_chunk, p.multi_occ, p.vis_gap)) {
+    p.multi_waves = p.step_waves;
+    p.multi_occ = 8;
+  }
   // Heaviest-raycast-first dispatch (order_kernel) also pays when the whole grid is
   // resident at once: it deals every CU one env of each cost stratum.  Block b = env b
   // (HEIST_DISPATCH_ORDER=0, no order[] load) measured 16.29 vs 15.37 us per 4096-env step
@@ -391,10 +401,10 @@ int heist_step_waves(heist_t h) {
 
 int heist_get_config(heist_t h, int32_t* out, int n) {
   if (int rc = check_handle(h)) return rc;
-  HEIST_REQUIRE(out != nullptr && n >= 0 && n <= 10, "heist_get_config: need out != NULL and 0 <= n <= 10");
+  HEIST_REQUIRE(out != nullptr && n >= 0 && n <= 11, "heist_get_config: need out != NULL and 0 <= n <= 11");
   const EnvParams& p = h->p;
-  const int32_t v[10] = {p.step_waves, p.ray_chunk,  p.step_occ,       p.vis_gap,   p.obs_store,
-                         p.ray_mode,   p.probe_mode, p.dispatch_order, p.split_obs, p.guard_cones};
+  const int32_t v[11] = {p.step_waves, p.ray_chunk,  p.step_occ,       p.vis_gap,   p.obs_store,  p.ray_mode,
+                         p.probe_mode, p.dispatch_order, p.split_obs, p.guard_cones, p.multi_waves};
   for (int k = 0; k < n; ++k) out[k] = v[k];
   return 0;
 }

@@ -105,6 +105,8 @@ struct EnvParams {
   float tile_lut[8];          // float32(tile) / 5  (environment.py:319)
   double axis_heading[4];     // heading_tab at (dr,dc) = (-1,0), (1,0), (0,-1), (0,1)
   int step_waves;             // wavefronts per env in step/reset (1, 2 or 4)
+  int multi_waves;            // wavefronts per env in the K-tick kernel (heist_step_multi; HEIST_MULTI_WAVES)
+  int multi_occ;              // min waves per SIMD it is compiled for (8 at 2 or 4 waves, 4 at 1: 128 VGPRs)
   int ray_chunk;              // samples per ray computed together (2, 4)
   int step_occ;               // min waves per SIMD the step kernel is compiled for (1, 8)
   int vis_gap;                // LDS distance stop map -> vis plane (1024, 2048 or 6144), see heist_env.hip

@@ -256,6 +256,35 @@ constexpr TieBits make_tie_bits() {
 }
 __constant__ TieBits kTieBits = make_tie_bits();
 
+// The same tie points as one byte per 64-wide bucket of t = |d| * 27720 (tie points are at
+// least 27720 / 132 = 210 apart, so a bucket holds at most one): tie[b] = its offset in
+// bucket b, 0xFF if none; rank[b] = the tie points in buckets below b.  The K-tick kernel
+// keeps both in LDS (868 B): the screen and the dedup key (cast_rays, DEDUP) read them there.
+constexpr int kTieBuckets = kTieL / 64 + 1;  // 434
+struct TieBuckets {
+  uint8_t tie[kTieBuckets];
+  uint8_t rank[kTieBuckets];
+};
+constexpr TieBuckets make_tie_buckets() {
+  TieBuckets t{};
+  for (int b = 0; b < kTieBuckets; ++b) t.tie[b] = 0xFF;
+  const TieBits bits = make_tie_bits();
+  int below = 0;
+  for (int b = 0; b < kTieBuckets; ++b) {
+    t.rank[b] = (uint8_t)below;
+    for (int o = 0; o < 64; ++o) {
+      const int n = 64 * b + o;
+      if (n <= kTieL && ((bits.w[n >> 5] >> (n & 31)) & 1u)) {
+        t.tie[b] = (uint8_t)o;
+        ++below;
+      }
+    }
+  }
+  return t;
+}
+__constant__ TieBuckets kTieBuckets_ = make_tie_buckets();
+static_assert(kTieL / 132 > 64, "at most one tie point per 64-wide bucket");
+
 // 1.5 * 2^23: for |v| < 2^22, fl32(v + kMagic32) = kMagic32 + rint(v), and the low 22 bits
 // of its bit pattern hold the integer (plus any offset folded into the constant).
 constexpr float kMagic32 = 12582912.0f;
@@ -299,6 +328,30 @@ __device__ __forceinline__ bool near_tie(float c, float s, float x, bool camera)
   const bool cy = __builtin_fabsf(ty - (my - kMagic32)) < kTieRad;
   return ((((wx >> (nx & 31)) & (uint32_t)cx) | ((wy >> (ny & 31)) & (uint32_t)cy)) & 1u) ||
          (camera && __builtin_fabsf(x) < kAxisRad);
+}
+
+// near_tie with the bucket tables in LDS (tb = TieBuckets copied there), plus the fast
+// path's dedup key: rays whose |dx| and |dy| lie in the same intervals between consecutive
+// tie points, with the same signs, have the same offsets rint(k dx / 2), rint(k dy / 2) for
+// every sample k <= 12 (rint of a non-tie value is translation-invariant by integers), so
+// the same tile sequence from any emitter tile (cast_rays, DEDUP).  key = interval of |dx|
+// | interval of |dy| << 8 | sign bits << 16.
+__device__ __forceinline__ bool near_tie_key(float c, float s, float x, bool camera, const TieBuckets* tb,
+                                             uint32_t* key) {
+  const float tx = __builtin_fabsf(c) * (float)kTieL, ty = __builtin_fabsf(s) * (float)kTieL;
+  const float mx = tx + kMagic32, my = ty + kMagic32;
+  const uint32_t nx = __builtin_bit_cast(uint32_t, mx) - 0x4B400000u;
+  const uint32_t ny = __builtin_bit_cast(uint32_t, my) - 0x4B400000u;
+  const uint32_t bx = tb->tie[nx >> 6], by = tb->tie[ny >> 6];
+  const uint32_t rx = tb->rank[nx >> 6], ry = tb->rank[ny >> 6];
+  const float fx = mx - kMagic32, fy = my - kMagic32;  // rint(t)
+  const bool cx = __builtin_fabsf(tx - fx) < kTieRad, cy = __builtin_fabsf(ty - fy) < kTieRad;
+  const uint32_t ox = nx & 63u, oy = ny & 63u;
+  // tie points of the bucket below t: those before its offset, and the offset itself when t > it
+  const uint32_t kx = rx + (uint32_t)(bx != 0xFFu && (ox > bx || (ox == bx && tx > fx)));
+  const uint32_t ky = ry + (uint32_t)(by != 0xFFu && (oy > by || (oy == by && ty > fy)));
+  *key = kx | (ky << 8) | ((uint32_t)(c < 0.0f) << 16) | ((uint32_t)(s < 0.0f) << 17);
+  return (cx && bx == ox) || (cy && by == oy) || (camera && __builtin_fabsf(x) < kAxisRad);
 }
 
 // LDS byte at an absolute LDS address (the dynamic LDS base is folded into the address
@@ -476,8 +529,16 @@ __device__ __forceinline__ int emitter_of_chunk(const EnvLds& L, int n_em, int k
 // Visibility stores are idempotent, so the pass order does not matter.  COUNT: samples (up
 // to the one that ends each ray) are summed in LDS meta[2] and exact casts in meta[4] (the
 // ALU work figures of SURVEY 8(d)); raycast_pass adds the env's totals to its counters.
-template <int NT, int U, int D, bool COUNT>
-__device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int probe, const double* hd) {
+// DEDUP (the K-tick kernel): the fast path marches one ray per distinct tile sequence.
+// Fast rays of a direction group whose dedup key (near_tie_key) equals the previous
+// lane's are dropped -- their sequence, and so the tiles they mark from every member's
+// tile, is the previous ray's -- and the others go to the wave's unique queue uq (128
+// directions in LDS), which is marched 64 at a time (and whenever the group changes): an
+// Architect camera fan of 0.5-degree rays has about a third as many distinct sequences as
+// rays.  tb: the tie bucket tables in LDS.
+template <int NT, int U, int D, bool COUNT, bool DEDUP = false>
+__device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int probe, const double* hd,
+                          const TieBuckets* tb = nullptr, float2* uq = nullptr) {
   static_assert(U == 2 || U == 4, "exact-path chunk");
   static_assert(kRing >= U, "the exact path's chunks stay inside the ring");
   constexpr int W = NT / 64;
@@ -492,6 +553,36 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
   int qn = 0;               // near-tie rays met by this wave (queued while <= 64)
   bool exact_em = false;    // this wave owns chunks of an exact-only emitter
   int k = 0;
+  // DEDUP: the unique queue of group uk (uqn entries); flush(n) marches entries 0 .. n-1
+  int uqn = 0, uk = -1;
+  if (DEDUP) uq += wave * 128;
+  auto flush = [&](int cnt) {
+    const Emit Eq = uni(L.em[uk]);
+    const int n_samp = Eq.kind == 0 ? 2 * Eq.range : Eq.range;
+    if (lane < cnt) {
+      const float2 d = uq[lane];
+      auto group = [&](auto ns, auto clamp) {
+        constexpr int NS = decltype(ns)::value;
+        constexpr bool CL = decltype(clamp)::value;
+        for (int m = 0; m < Eq.members; ++m) {
+          const int row = m == 0 ? Eq.row : uni(L.em[uk + m].row);
+          const int col = m == 0 ? Eq.col : uni(L.em[uk + m].col);
+          const uint32_t own = base + (uint32_t)((row + kRing) * PC + (col + kRing));
+          const float mx = __builtin_bit_cast(float, base + (uint32_t)(col + kRing));
+          const float my = __builtin_bit_cast(float, (uint32_t)(row + kRing));
+          march_fast<D, NS, CL, false>(PC, own, d.x, d.y, mx, my, n_samp);
+        }
+      };
+      if (n_samp == 2 * kTieMaxRange)
+        group(std::integral_constant<int, 2 * kTieMaxRange>{}, std::false_type{});
+      else if (n_samp == 4)
+        group(std::integral_constant<int, 4>{}, std::false_type{});
+      else if (n_samp < 4)
+        group(std::integral_constant<int, 4>{}, std::true_type{});
+      else
+        group(std::integral_constant<int, 2 * kTieMaxRange>{}, std::true_type{});
+    }
+  };
   // pass 1: fp32 fast path
   for (int c = wave; c < n_chunk; c += W) {
     k = emitter_of_chunk(L, n_em, k, c);
@@ -512,13 +603,39 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
       sf = 0.3f + 1e-3f * (float)i;
       cf = 0.7f;
     }
-    const bool tie = active && probe != 3 && near_tie(cf, sf, xr, E.kind == 0);
+    uint32_t key = 0;
+    const bool tie = active && probe != 3 &&
+                     (DEDUP ? near_tie_key(cf, sf, xr, E.kind == 0, tb, &key) : near_tie(cf, sf, xr, E.kind == 0));
     const unsigned long long b = __ballot(tie);
     if (tie) {
       const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
       if (pos < 64) queue[pos] = (k << 16) | i;
     }
     qn += __popcll(b);
+    if constexpr (DEDUP) {
+      const uint32_t mine = (active && !tie) ? key : 0xFFFFFFFFu;
+      const uint32_t prev = (uint32_t)__shfl_up((int)mine, 1, 64);
+      const bool fresh = active && !tie && (lane == 0 || prev != mine);
+      if (k != uk && uqn > 0) {  // the queue (< 64 entries) holds another group's rays
+        flush(uqn);
+        uqn = 0;
+      }
+      uk = k;
+      const unsigned long long fb = __ballot(fresh);
+      if (fresh) {
+        const int pos = uqn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(fb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fb, 0u));
+        const float h = E.kind == 0 ? 0.5f : 1.0f;
+        uq[pos] = make_float2(below_one(cf) * h, -below_one(sf) * h);
+      }
+      uqn += __popcll(fb);
+      if (uqn >= 64) {
+        flush(64);
+        const float2 d = uq[64 + (lane & 63)];
+        if (lane < uqn - 64) uq[lane] = d;
+        uqn -= 64;
+      }
+      continue;
+    }
     if (active && !tie) {
       const int n_samp = E.kind == 0 ? 2 * E.range : E.range;  // every member of a group: same range
       const float h = E.kind == 0 ? 0.5f : 1.0f;  // sample stride: camera half tiles, guard whole tiles
@@ -547,6 +664,7 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
         group(std::integral_constant<int, 2 * kTieMaxRange>{}, std::true_type{});
     }
   }
+  if (DEDUP && uqn > 0) flush(uqn);
   if (probe == 2) return;
   // pass 2: exact path (the wave's own LDS writes to its queue are ordered before its reads)
   __builtin_amdgcn_wave_barrier();
@@ -618,20 +736,24 @@ __device__ __forceinline__ void publish_emitters(const EnvLds& L, Emit E, int n_
     const unsigned long long above = t < 63 ? lead >> (t + 1) : 0ull;
     E.members = cont ? 0 : (above ? (int)__builtin_ctzll(above) + 1 : 64 - t);
     const int cnt = (t < n_em && !cont && (E.kind == 0 || E.kind == 1)) ? (E.num_rays + 1 + 63) / 64 : 0;  // 2: cached cone
-    int incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int v = __shfl_up(incl, d, 64);
-      if (t >= d) incl += v;
+    // exclusive prefix sum of cnt over the lanes, bit slice by bit slice: lane t's share of
+    // slice b is 2^b x (lanes below t with bit b set), one ballot + mbcnt per slice and no
+    // LDS round trip (a shuffle scan is six dependent ds_bpermutes); cnt < 2^9
+    int excl = 0, total = 0;
+    for (int b = 0; b < 9; ++b) {
+      const unsigned long long m = __ballot((cnt >> b) & 1);
+      excl += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
+      total += __popcll(m) << b;
+      if (__ballot(cnt >> (b + 1)) == 0ull) break;
     }
     if (t < n_em) {
-      E.first = incl - cnt;
+      E.first = excl;
       L.em[t] = E;
     }
     const unsigned long long cached = __ballot(t < n_em && E.kind == 2);  // guards with a cached cone
     if (t == 63) {
       L.meta[0] = n_em;
-      L.meta[1] = incl;
+      L.meta[1] = total;
       L.meta[2] = 0;
       L.meta[4] = 0;
       L.meta[6] = (int)(uint32_t)cached;
@@ -1251,16 +1373,26 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
 // K ticks per launch (heist_step_multi)
 // ---------------------------------------------------------------------------
 
+// Observation lanes: the threads that store a tick's observation row -- waves 1.. when the
+// env has two or more waves (wave 0, which updates the emitters and loads the next cone
+// entries, then issues no observation stores: vmcnt counts loads and stores together, in
+// issue order, so its wait for a load never waits for them), every lane of the one wave
+// otherwise.  LB is the first observation lane, PW their count.
+template <int NT>
+struct ObsLanes {
+  static constexpr int LB = NT > 64 ? 64 : 0;
+  static constexpr int PW = NT - LB;
+};
+
 // Channels 0 and 2 of observation row `o` (the env's [3][R][C] floats of one tick) except
 // the solver's quad, from LDS (the tile grid and the handle's static position plane,
-// copied in at the start of the launch): waves 1.. store them while wave 0 updates the
-// emitters.  Quad q belongs to thread 64 + q % (NT - 64), which stores the solver's quad
-// again in write_obs_dynamic (program order to one address).
+// copied in at the start of the launch).  Quad q belongs to observation lane q % PW, which
+// stores the solver's quad again in write_obs_ch1_tail (program order to one address).
 template <int NT>
 __device__ __forceinline__ void write_obs_static_lds(const EnvParams& p, const EnvLds& L, const float* plane,
                                                      float* __restrict__ o) {
-  constexpr int PW = NT - 64;
-  const int t = (int)threadIdx.x - 64;
+  constexpr int PW = ObsLanes<NT>::PW;
+  const int t = (int)threadIdx.x - ObsLanes<NT>::LB;
   if (t < 0) return;
   const int RC = p.RC, n4 = RC / 4;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(o, (short)0, 12 * RC, 0x00020000);
@@ -1277,32 +1409,29 @@ __device__ __forceinline__ void write_obs_static_lds(const EnvParams& p, const E
   }
 }
 
-// Channel 1 of observation row `o` plus the solver's quad of channel 2, stored by waves
-// 1.. only (wave 0 issues no observation stores, so waiting for its own loads never waits
-// for them: vmcnt counts loads and stores together, in issue order).  The solver's quad
-// belongs to the thread that stored channel 2's quad in write_obs_static_lds (program
-// order to one address).
+// Channel 1 of observation row `o` (ray plane | guard plane) plus the solver's quad of
+// channel 2, by the observation lanes.
 template <int NT>
-__device__ __forceinline__ void write_obs_ch1_tail(const EnvParams& p, const EnvScalars& s, const EnvLds& L, int cset,
-                                                   float* __restrict__ o) {
-  constexpr int PW = NT - 64;
-  const int t = (int)threadIdx.x - 64;
+__device__ __forceinline__ void write_obs_ch1_tail(const EnvParams& p, const EnvScalars& s, const EnvLds& L,
+                                                   const uint8_t* gvis, float* __restrict__ o) {
+  constexpr int PW = ObsLanes<NT>::PW;
+  const int t = (int)threadIdx.x - ObsLanes<NT>::LB;
   if (t < 0) return;
   const int RC = p.RC, C = p.C, n4 = RC / 4, c4 = C / 4;
-  const int mc = p.max_cams, mg = p.max_guards;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(o, (short)0, 12 * RC, 0x00020000);
   const int pol = p.obs_store;
+  static_assert((kRing & 1) == 0, "padded vis rows of a C % 4 == 0 grid are 2-byte aligned");
   for (int q = t; q < n4; q += PW) {
     const int r = q / c4, c0 = 4 * (q - r * c4);
     const int a = L.at(r, c0);
     uint32_t v;
     if ((kRing & 3) == 0) {
-      v = *reinterpret_cast<const uint32_t*>(L.vis + a);
+      v = *reinterpret_cast<const uint32_t*>(L.vis + a) | *reinterpret_cast<const uint32_t*>(gvis + a);
     } else {
       const uint16_t* vp2 = reinterpret_cast<const uint16_t*>(L.vis + a);
-      v = (uint32_t)vp2[0] | ((uint32_t)vp2[1] << 16);
+      const uint16_t* gp2 = reinterpret_cast<const uint16_t*>(gvis + a);
+      v = ((uint32_t)vp2[0] | ((uint32_t)vp2[1] << 16)) | ((uint32_t)gp2[0] | ((uint32_t)gp2[1] << 16));
     }
-    v |= cone_vis4(L, mc, mg, cset, r, c0);
     obs_put(rs, pol, 16 * (n4 + q),
             make_float4((float)(v & 0xff), (float)((v >> 8) & 0xff), (float)((v >> 16) & 0xff), (float)(v >> 24)));
   }
@@ -1316,6 +1445,52 @@ __device__ __forceinline__ void write_obs_ch1_tail(const EnvParams& p, const Env
   }
 }
 
+// The ray plane and the guard plane zeroed by the observation lanes.
+template <int NT>
+__device__ __forceinline__ void clear_planes(const EnvParams& p, const EnvLds& L, uint8_t* gvis, bool rays) {
+  constexpr int PW = ObsLanes<NT>::PW;
+  const int t = (int)threadIdx.x - ObsLanes<NT>::LB;
+  uint32_t* v4 = reinterpret_cast<uint32_t*>(L.vis);
+  uint32_t* g4 = reinterpret_cast<uint32_t*>(gvis);
+  for (int i = t; i >= 0 && i < (padded_bytes(p.R, p.C) + 3) / 4; i += PW) {
+    if (rays) v4[i] = 0u;
+    g4[i] = 0u;
+  }
+}
+
+// The cached guard cones of cone set `set` (the kind-2 emitter slots of meta[6..7]; set 0:
+// this tick's poses from the emitter table, set 1: the auto-reset poses, patrol point 0)
+// stamped into the guard plane gvis (the vis geometry, cleared each tick) by the
+// observation lanes: lane 15 i + j writes row j of cone i (mod the PW / 15 cones per
+// pass), one byte per visible tile.  A cone names in-grid tiles only (guard_cone_kernel),
+// so every write lands on the grid.
+template <int NT>
+__device__ __forceinline__ void stamp_guard_cones(const EnvLds& L, uint8_t* gvis, int mc, int mg, int set) {
+  constexpr int G = ObsLanes<NT>::PW / 15;  // cones per pass
+  const int l = (int)threadIdx.x - ObsLanes<NT>::LB;
+  const int grp = l / 15, j = l - 15 * grp;
+  if (l < 0 || grp >= G) return;
+  uint64_t m = ((uint64_t)(uint32_t)uni(L.meta[7]) << 32) | (uint32_t)uni(L.meta[6]);
+  for (int c = 0; m; ++c) {
+    const int k = (int)__builtin_ctzll(m);
+    m &= m - 1;
+    if (c % G != grp) continue;
+    const int g = k - mc;
+    int gr, gc;
+    if (set) {
+      const int rp = (int)L.rpos[g];
+      gr = unpack_r(rp);
+      gc = unpack_c(rp);
+    } else {
+      gr = L.em[k].row;
+      gc = L.em[k].col;
+    }
+    const uint32_t bits = L.cone[16 * (set * mg + g) + j] & 0x7fffu;
+    uint8_t* row = gvis + L.off0 + (gr + j - kConeRange) * L.PC + (gc - kConeRange);
+    for (uint32_t b = bits; b; b &= b - 1) row[__builtin_ctz(b)] = 1;
+  }
+}
+
 // K consecutive heist_step ticks of one env per workgroup (environment.py:216-299 and
 // :347-374 K times), with actions[k][env] known up front: what env-only throughput and
 // action replay need.  The per-env state stays on chip for the whole launch -- grid, stop
@@ -1325,24 +1500,30 @@ __device__ __forceinline__ void write_obs_ch1_tail(const EnvParams& p, const Env
 // stores), reward, done and status.  Per tick:
 //   A  every thread: the solver's move and the reward terms that precede detection
 //      (environment.py:235-269; they need the grid, not the visibility); wave 0: cameras
-//      and guards advance (security.py:49-51, :145-159), the cached guard cone entries
-//      loaded during the previous tick go to LDS, the emitter table is published; waves
-//      1..: the tick's static observation channels 0 and 2, the plane clears;
-//   barrier, raycast (all waves), barrier;
-//   C  every thread: detection, vault, timeout, auto-reset (environment.py:271-297,
-//      :183-214); wave 0: the next tick's cone entries are loaded (they land during the
-//      barrier and the next update), reward / done / status stored; waves 1..: channel 1.
-// Wave 0 issues no observation stores, so its wait for the cone entries is only for them.
-// A finishing env loads its cached guards' reset cones (patrol point 0, same heading) then;
-// a live-raycast guard off its start costs a second raycast pass from the reset poses.  A
-// cached guard's heading is the one its slot names: read from a cone entry once, at the
-// end.  Results are bit-identical to K heist_step launches (tests/test_gpu_env.py).
-template <int W, int U, int O, int D, bool STAMP = false>
+//      and guards advance (security.py:49-51, :145-159) and the emitter table is
+//      published; observation lanes: the tick's static channels 0 and 2, the plane clears;
+//   barrier, raycast (all waves), the cached guards' cones stamped into the guard plane
+//      by the observation lanes (their raycast share is the smaller one), barrier;
+//   C  every thread: detection (ray plane | guard plane), vault, timeout, auto-reset
+//      (environment.py:271-297, :183-214); wave 0: the next tick's cone entries are
+//      loaded, reward / done / status stored; observation lanes: channel 1.
+// The cone entry a cached guard needs at tick k + 1 is loaded at the end of tick k and
+// lands in LDS at tick k + 1 (phase A with two or more waves; after the raycast with one,
+// where the entry has had the whole raycast to arrive and the wait for it is not held up
+// by the observation stores issued since).  A finishing env loads its cached guards'
+// reset cones (patrol point 0, same heading) then; a live-raycast guard off its start
+// costs a second raycast pass from the reset poses.  A cached guard's heading is the one
+// its slot names: read from a cone entry once, at the end.  Results are bit-identical to
+// K heist_step launches (tests/test_gpu_env.py).
+// PROBE (profiling variant, HEIST_PROBE_MODE at heist_create; results wrong on purpose):
+// bit 0 skips the raycast and the cone stamps, bit 1 the observation stores, bit 2 the
+// rays' marches (directions and tie screens only).
+template <int W, int U, int O, int D, bool STAMP = false, int PROBE = 0>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) void step_multi_kernel(
     EnvParams p, int K, const int64_t* __restrict__ actions, float* __restrict__ obs, float* __restrict__ rew,
     double* __restrict__ rew64, uint8_t* __restrict__ done_out, int8_t* __restrict__ status_out, int auto_reset) {
   constexpr int NT = 64 * W;
-  static_assert(W >= 2, "the observation is stored by the waves after wave 0");
+  constexpr bool SOLO = W == 1;  // one wave does every role
   extern __shared__ __align__(16) unsigned char smem[];
   const int e = p.dispatch_order ? p.order[blockIdx.x] : (int)blockIdx.x;
   const int t = threadIdx.x;
@@ -1355,11 +1536,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   EmitterRaw* rec = reinterpret_cast<EmitterRaw*>(reinterpret_cast<unsigned char*>(plane) +
                                                   align16(sizeof(float) * (size_t)RC));  // [n_slot] records
   uint8_t* act = reinterpret_cast<uint8_t*>(rec + n_slot);
+  uint8_t* gvis = act + align16((size_t)K);  // cached guard cones of the tick, vis geometry (stamp_guard_cones)
   const EnvBase eb = env_base(p, e);
   // STAMP (instrumentation, heist_step_stamps): lane 0 of every wave sums the shader clock
-  // spent in each of 9 tick segments over the launch into LDS (after the K actions), and
-  // writes [segment sums 0..8, launch lifetime] to stamps[env][wave][10]
-  unsigned long long* st_acc = reinterpret_cast<unsigned long long*>(act + align16((size_t)K));
+  // spent in each of 9 tick segments over the launch into LDS, and writes [segment sums
+  // 0..8, lifetime, start clock, HW_ID, XCC_ID] to stamps[env][wave][16]
+  TieBuckets* tb = reinterpret_cast<TieBuckets*>(gvis + D);  // the tie screen's tables (868 B)
+  float2* uq = reinterpret_cast<float2*>(reinterpret_cast<unsigned char*>(tb) + align16(sizeof(TieBuckets)));
+  unsigned long long* st_acc = reinterpret_cast<unsigned long long*>(uq + 128 * W);  // after the unique queues
   unsigned long long st_last = 0, st_start = 0;
   if (STAMP && (t & 63) == 0) {
     st_start = st_last = __builtin_amdgcn_s_memtime();
@@ -1382,6 +1566,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   }
   for (int i = t; i < path_words; i += NT) L.path[i] = eb.paths[i];
   for (int i = t; i < RC; i += NT) plane[i] = p.plane0[i];
+  for (int i = t; i < (int)sizeof(TieBuckets) / 4; i += NT)
+    reinterpret_cast<uint32_t*>(tb)[i] = reinterpret_cast<const uint32_t*>(&kTieBuckets_)[i];
   for (int k = t; k < K; k += NT) {
     const int64_t a = actions[(size_t)k * N + e];
     act[k] = (uint8_t)((a < 0 || a > 4) ? 0 : a);  // unknown actions do not move (environment.py:239)
@@ -1404,6 +1590,15 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     const uint4* src = reinterpret_cast<const uint4*>(eb.cones + cone_off(g, idx, slot));
     ca = src[0];
     cb = src[1];
+  };
+  // the entry's cone rows into LDS (cone set 0) and the slot after the guard's next move
+  auto take_entry = [&]() {
+    Guard gd = as_guard(rec[t]);
+    gd.nslot = (uint8_t)(cb.w >> 16);  // row 15
+    rec[t] = __builtin_bit_cast(EmitterRaw, gd);
+    uint4* dst = reinterpret_cast<uint4*>(L.cone + 16 * g);
+    dst[0] = ca;
+    dst[1] = cb;
   };
   __syncthreads();  // records in LDS
   if (live_guard) {
@@ -1473,11 +1668,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
           }
           const uint16_t np = moves ? L.path[__umul24((uint32_t)g, (uint32_t)p.max_path) + (uint32_t)nidx] : gd.pos;
           if (cached) {
-            if (moves) gd.hslot = gd.nslot;
-            gd.nslot = (uint8_t)(cb.w >> 16);  // row 15: the slot after the next move
-            uint4* dst = reinterpret_cast<uint4*>(L.cone + 16 * g);
-            dst[0] = ca;
-            dst[1] = cb;
+            if (moves) gd.hslot = gd.nslot;  // the slot the entry loaded for this tick was taken with
           } else if (moves) {
             gd.heading = guard_heading_after(p, unpack_r(np) - unpack_r(gd.pos), unpack_c(np) - unpack_c(gd.pos),
                                              gd.heading);
@@ -1487,15 +1678,13 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
           if (gd.pos != gd.pos0) atomicOr(reinterpret_cast<unsigned int*>(&L.meta[5]), cached ? 2u : 1u);
           rec[t] = __builtin_bit_cast(EmitterRaw, gd);
           E = guard_emit(gd);
+          if (cached && !SOLO) take_entry();  // then nslot := the entry's row 15
         }
-        HEIST_MULTI_STAMP(1);  // 1: emitter update (wave 0)
+        HEIST_MULTI_STAMP(1);  // 1: emitter update
         publish_emitters(L, E, n_slot);
-      } else {
-        write_obs_static_lds<NT>(p, L, plane, obs + ((size_t)k * N + e) * 3 * RC);
-        HEIST_MULTI_STAMP(1);  // 1: static channels (waves 1..)
-        uint32_t* v4 = reinterpret_cast<uint32_t*>(L.vis);
-        for (int i = t - 64; i < (padded_bytes(p.R, p.C) + 3) / 4; i += NT - 64) v4[i] = 0u;
       }
+      if (!(PROBE & 2)) write_obs_static_lds<NT>(p, L, plane, obs + ((size_t)k * N + e) * 3 * RC);
+      clear_planes<NT>(p, L, gvis, true);
     } else {  // the emitters with every guard back at patrol point 0, headings kept
       if (w0) {
         if (live_cam) E = cam_emit(as_cam(rec[t]));
@@ -1509,26 +1698,26 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
           }
         }
         publish_emitters(L, E, n_slot);
-      } else {
-        uint32_t* v4 = reinterpret_cast<uint32_t*>(L.vis);
-        for (int i = t - 64; i < (padded_bytes(p.R, p.C) + 3) / 4; i += NT - 64) v4[i] = 0u;
       }
+      clear_planes<NT>(p, L, gvis, true);
     }
-    HEIST_MULTI_STAMP(2);  // 2: publish (wave 0), clears (waves 1..)
-    __syncthreads();  // emitter table, cone rows, cleared vis
+    HEIST_MULTI_STAMP(2);  // 2: publish, static channels, clears
+    __syncthreads();  // emitter table, cone rows, cleared planes
     HEIST_MULTI_STAMP(3);  // 3: waiting at the raycast barrier
     // 3. visibility (environment.py:257-258)
     if (live_guard && E.kind == 1) L.vis[L.at(E.row, E.col)] = 1;  // visibility.py:59
-    cast_rays<NT, U, D, false>(smem, L, p.ray_mode, 0, p.half_deg);
-    HEIST_MULTI_STAMP(4);  // 4: raycast
-    __syncthreads();  // vis complete
+    if (!(PROBE & 1)) cast_rays<NT, U, D, false, true>(smem, L, p.ray_mode, (PROBE & 4) ? 2 : 0, p.half_deg, tb, uq);
+    if (SOLO && cached && !reset_pass) take_entry();  // loaded a tick ago; the raycast covered its latency
+    if (!(PROBE & 1)) stamp_guard_cones<NT>(L, gvis, mc, mg, 0);
+    HEIST_MULTI_STAMP(4);  // 4: raycast, cone stamps
+    __syncthreads();  // planes complete
     HEIST_MULTI_STAMP(5);  // 5: waiting for the other waves' raycast
 
-    int cset = 0;
     if (!reset_pass) {
       if (act_now) {
         // 5. detection, vault, timeout (environment.py:271-297), in the reference's order
-        if (L.vis[L.at(s.pos_r, s.pos_c)] | (cone_vis4(L, mc, mg, 0, s.pos_r, s.pos_c) & 1u)) {
+        const int at = L.at(s.pos_r, s.pos_c);
+        if (L.vis[at] | gvis[at]) {
           s.detected = 1;
           if (w0) reward += p.r_detect;
           s.done = 1;
@@ -1580,16 +1769,19 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
           reset_pass = true;
           continue;
         }
-        if (moved & 2) {
-          __syncthreads();  // the reset cones in LDS
-          cset = 1;
+        if (moved & 2) {  // cached guards off their start: the guard plane from the reset cones
+          __syncthreads();  // the reset cones in LDS; every wave's detection read is done
+          clear_planes<NT>(p, L, gvis, false);
+          if constexpr (W > 2) __syncthreads();
+          stamp_guard_cones<NT>(L, gvis, mc, mg, 1);
+          if constexpr (W > 2) __syncthreads();
         }
       }
     }
     reset_pass = false;
     HEIST_MULTI_STAMP(6);  // 6: detection, vault, timeout, auto-reset
     if (w0) {
-      if (live_guard && cached && k + 1 < K) next_entry(as_guard(rec[t]), !s.done);  // lands during the next update
+      if (live_guard && cached && k + 1 < K) next_entry(as_guard(rec[t]), !s.done);  // lands during the next tick
       if (t == 0) {
         const size_t ko = (size_t)k * N + e;
         rew[ko] = (float)reward;
@@ -1597,19 +1789,21 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
         done_out[ko] = (uint8_t)done_now;
         status_out[ko] = (int8_t)status;
       }
-    } else {
-      write_obs_ch1_tail<NT>(p, s, L, cset, obs + ((size_t)k * N + e) * 3 * RC);
     }
-    HEIST_MULTI_STAMP(7);  // 7: channel 1 + solver quad (waves 1..), outputs (wave 0)
+    if (!(PROBE & 2)) write_obs_ch1_tail<NT>(p, s, L, gvis, obs + ((size_t)k * N + e) * 3 * RC);
+    HEIST_MULTI_STAMP(7);  // 7: outputs, channel 1 + solver quad
     ++k;
   }
 #undef HEIST_MULTI_STAMP
   // epilogue: the state the next launch (or heist_export) starts from
   if (t == 0) p.scal[e] = s;
   if (STAMP && (t & 63) == 0) {
-    unsigned long long* q = p.stamps + ((size_t)e * W + (t >> 6)) * 10;
+    unsigned long long* q = p.stamps + ((size_t)e * W + (t >> 6)) * 16;
     for (int j = 0; j < 9; ++j) q[j] = st_acc[(t >> 6) * 10 + j];
     q[9] = __builtin_amdgcn_s_memtime() - st_start;
+    q[10] = st_start;
+    q[11] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+    q[12] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
   }
   if (live_cam) eb.cams[(uint32_t)t].heading = as_cam(rec[t]).heading;
   if (live_guard) {
@@ -2212,21 +2406,42 @@ hipError_t launch_step(const EnvParams& p, const int64_t* actions, float* obs, f
 // K ticks per launch: (W, U, O, D) variants with two or more waves per env; another
 // configuration (HEIST_STEP_WAVES=1) runs K single-tick launches instead (same results).
 #define HEIST_MULTI_VARIANTS(X) \
-  X(2, 4, 8, 1024) X(2, 4, 8, 2048) X(2, 4, 8, 6144) X(4, 4, 8, 1024) X(4, 4, 8, 2048) X(4, 4, 8, 6144)
+  X(2, 4, 8, 1024) X(2, 4, 8, 2048) X(2, 4, 8, 6144) X(4, 4, 8, 1024) X(4, 4, 8, 2048) X(4, 4, 8, 6144) \
+  X(1, 4, 4, 1024) X(1, 4, 4, 2048)
+
+bool multi_variant_exists(int W, int U, int O, int D) {
+#define HEIST_HAS_MULTI(W_, U_, O_, D_) \
+  if (W == W_ && U == U_ && O == O_ && D == D_) return true;
+  HEIST_MULTI_VARIANTS(HEIST_HAS_MULTI)
+#undef HEIST_HAS_MULTI
+  return false;
+}
 
 size_t step_multi_lds(const EnvParams& p, int K) {
   const int n_slot = p.max_cams + p.max_guards;
-  return align16(env_lds_bytes(p.R, p.C, n_slot, p.max_guards * p.max_path, p.vis_gap, p.step_waves, p.max_guards)) +
-         align16(sizeof(float) * (size_t)p.RC) + 32 * (size_t)n_slot + align16((size_t)K) +
-         (p.stamps ? 80 * (size_t)p.step_waves : 0);
+  return align16(env_lds_bytes(p.R, p.C, n_slot, p.max_guards * p.max_path, p.vis_gap, p.multi_waves, p.max_guards)) +
+         align16(sizeof(float) * (size_t)p.RC) + 32 * (size_t)n_slot + align16((size_t)K) + (size_t)p.vis_gap +
+         align16(sizeof(TieBuckets)) + 1024 * (size_t)p.multi_waves + (p.stamps ? 80 * (size_t)p.multi_waves : 0);
 }
 
 hipError_t launch_step_multi(const EnvParams& p, const EnvParams* pg, int K, const int64_t* actions, float* obs,
                              float* rew, double* rew64, uint8_t* done_out, int8_t* status_out, int auto_reset,
                              hipStream_t st) {
   const size_t lds = step_multi_lds(p, K);
+  if (p.probe_mode >= 1 && p.probe_mode <= 4 && p.ray_chunk == 4 && p.vis_gap == 1024 &&
+      ((p.multi_waves == 2 && p.multi_occ == 8) || (p.multi_waves == 1 && p.multi_occ == 4))) {
+    // profiling variants (default 20 x 20 geometry only)
+#define HEIST_PROBE_CASE(W_, O_, M)                                                                              \
+  if (p.multi_waves == W_ && p.probe_mode == M)                                                                \
+    hipLaunchKernelGGL((step_multi_kernel<W_, 4, O_, 1024, false, M>), dim3(p.n_envs), dim3(64 * W_), lds, st, p, K, \
+                       actions, obs, rew, rew64, done_out, status_out, auto_reset);
+    HEIST_PROBE_CASE(2, 8, 1) HEIST_PROBE_CASE(2, 8, 2) HEIST_PROBE_CASE(2, 8, 3) HEIST_PROBE_CASE(2, 8, 4)
+    HEIST_PROBE_CASE(1, 4, 1) HEIST_PROBE_CASE(1, 4, 2) HEIST_PROBE_CASE(1, 4, 3) HEIST_PROBE_CASE(1, 4, 4)
+#undef HEIST_PROBE_CASE
+    return hipGetLastError();
+  }
 #define HEIST_MULTI_CASE(W, U, O, D)                                                                        \
-  if (p.step_waves == W && p.ray_chunk == U && p.step_occ == O && p.vis_gap == D && p.probe_mode == 0 &&   \
+  if (p.multi_waves == W && p.ray_chunk == U && p.multi_occ == O && p.vis_gap == D && p.probe_mode == 0 && \
       !p.sample_counter && !p.redo_counter) {                                                                \
     if (p.stamps)                                                                                            \
       hipLaunchKernelGGL((step_multi_kernel<W, U, O, D, true>), dim3(p.n_envs), dim3(64 * W), lds, st, p, K,  \

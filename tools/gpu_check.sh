@@ -31,6 +31,8 @@ for s in ${STEPS:-pytest smoke bench prof}; do
     driver) step bench_driver 900 python3 bench.py --gpus 1 --steps 20 --warmup 5 ;;
     multitest) step pytest_multi 300 python -u -m pytest tests/test_gpu_env.py -k multi -x -v --timeout 200 --timeout-method thread ;;
     quickk) step bench_quick_k 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary ;;
+    quickw1) HEIST_MULTI_WAVES=1 step bench_quick_w1 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary ;;
+    mstampw1) HEIST_MULTI_WAVES=1 step multi_stamps_w1 300 python tools/probe_multi_stamps.py ;;
     quick1) step bench_quick_1 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary --ticks-per-launch 1 ;;
     quicklicm) HEIST_LIB=$PWD/rl-project-heist-architect-adversarial-reinforcement-learning-framework-cse4019_amd/heist_amd/libheist_hip_licm.so step bench_quick_licm 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary --ticks-per-launch 1 ;;
     mstamp) step multi_stamps 300 python tools/probe_multi_stamps.py ;;
@@ -44,6 +46,16 @@ for s in ${STEPS:-pytest smoke bench prof}; do
          python tools/pmc_summary.py "$(find "$OUT/pmc_sq_m" -name "*counter_collection.csv" | head -n 1)" step_multi_kernel "$OUT/pmc_sq_m.json" > /dev/null 2>&1
          python tools/pmc_summary.py "$(find "$OUT/pmc_sq2_m" -name "*counter_collection.csv" | head -n 1)" step_multi_kernel "$OUT/pmc_sq2_m.json" > /dev/null 2>&1; true ;;
     lbtest) step pytest_lb 600 python -u -m pytest tests/test_gpu_trainer.py -k "layout_batch or interactive or c3" -x -v --timeout 500 --timeout-method thread ;;
+    mmodesw1) export HEIST_MULTI_WAVES=1; step multi_modes 300 python tools/probe_multi_modes.py
+            step pmc_modes_m1 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d "$OUT/pmm1" -o m --output-format csv -- python3 tools/probe_multi_modes.py
+            step pmc_modes_m2 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d "$OUT/pmm2" -o m --output-format csv -- python3 tools/probe_multi_modes.py
+            python tools/pmc_summary.py "$(find "$OUT/pmm1" -name "*counter_collection.csv" | head -n 1)" step_multi_kernel "$OUT/pmc_modes_m1.json" --modes 5 3 > /dev/null 2>&1
+            python tools/pmc_summary.py "$(find "$OUT/pmm2" -name "*counter_collection.csv" | head -n 1)" step_multi_kernel "$OUT/pmc_modes_m2.json" --modes 5 3 > /dev/null 2>&1; unset HEIST_MULTI_WAVES; true ;;
+    mmodes) step multi_modes 300 python tools/probe_multi_modes.py
+            step pmc_modes_m1 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d "$OUT/pmm1" -o m --output-format csv -- python3 tools/probe_multi_modes.py
+            step pmc_modes_m2 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d "$OUT/pmm2" -o m --output-format csv -- python3 tools/probe_multi_modes.py
+            python tools/pmc_summary.py "$(find "$OUT/pmm1" -name "*counter_collection.csv" | head -n 1)" step_multi_kernel "$OUT/pmc_modes_m1.json" --modes 5 3 > /dev/null 2>&1
+            python tools/pmc_summary.py "$(find "$OUT/pmm2" -name "*counter_collection.csv" | head -n 1)" step_multi_kernel "$OUT/pmc_modes_m2.json" --modes 5 3 > /dev/null 2>&1; true ;;
     benchtest) step pytest_bench 900 python -u -m pytest tests/test_gpu_bench.py -x -v --timeout 800 --timeout-method thread ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o heist --output-format csv -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-secondary ;;
     pmc) step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o heist --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary

@@ -29,11 +29,11 @@ def main():
     env = HeistEnv(n, EnvironmentConfig(architect_budget=15), max_cams=5, max_guards=3, max_path=16, device="cuda")
     bench.architect_layouts(env, 15, seed=1234)
     env.reset()
-    W = nat.lib().heist_step_waves(env._h)
+    W = env.kernel_config()["multi_waves"]
     acts = torch.randint(0, 5, (4 * K, n), device="cuda")
     for j in range(2):
         env.step_multi(acts[j * K:(j + 1) * K])
-    buf = torch.zeros((n, W, 10), dtype=torch.int64, device="cuda")
+    buf = torch.zeros((n, W, 16), dtype=torch.int64, device="cuda")
     out = {"n": n, "K": K, "waves": W, "launches": []}
     for j in range(2, 4):
         nat.check(nat.lib().heist_step_stamps(env._h, nat.ptr(buf)), "heist_step_stamps")
@@ -51,6 +51,24 @@ def main():
         rec["lifetime_cycles_per_tick"] = {"p10": float(np.percentile(life, 10)) / K, "p50": float(np.median(life)) / K,
                                            "p90": float(np.percentile(life, 90)) / K, "max": float(life.max()) / K}
         rec["effective_clock_ghz_from_max_lifetime"] = float(life.max()) / (rec["launch_ms"] * 1e6)
+        # residency: blocks alive at once per CU (the clock is per CU: compare within one)
+        hw, xcc, start = s[:, 0, 11], s[:, 0, 12], s[:, 0, 10]
+        cu = (xcc & 0xF) * 1024 + ((hw >> 8) & 0xFF)
+        conc, per_cu = [], []
+        for c in np.unique(cu):
+            idx = np.nonzero(cu == c)[0]
+            st, en = start[idx], start[idx] + s[idx, 0, 9]
+            per_cu.append(len(idx))
+            ev = sorted([(x, 1) for x in st] + [(x, -1) for x in en])
+            cur = best = 0
+            for _, dlt in ev:
+                cur += dlt
+                best = max(best, cur)
+            conc.append(best)
+        rec["blocks_per_cu"] = {"min": int(min(per_cu)), "max": int(max(per_cu)), "p50": float(np.median(per_cu))}
+        rec["max_concurrent_blocks_per_cu"] = {"min": int(min(conc)), "max": int(max(conc)),
+                                               "p50": float(np.median(conc))}
+        rec["cus"] = int(len(per_cu))
         out["launches"].append(rec)
     print(json.dumps(out), flush=True)
 

@@ -1069,12 +1069,19 @@ __device__ __forceinline__ void write_obs_static(const EnvParams& p, int e, floa
   const int RC = p.RC, n4 = RC / 4;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(obs + (size_t)e * 3 * RC, (short)0, 12 * RC, 0x00020000);
-  const uint32_t* s4 = reinterpret_cast<const uint32_t*>(p.grid + (size_t)e * RC);
+  // Both loads go through buffer descriptors sized to their object (the env's grid row,
+  // the handle's R*C position plane): the hardware range check returns 0 for an offset past
+  // num_records instead of touching memory, so no index here can fault whatever the
+  // compiler schedules (the round-2 r02bn fault).
+  const __amdgpu_buffer_rsrc_t gs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.grid + (size_t)e * RC), (short)0, RC, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ps =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.plane0), (short)0, 4 * RC, 0x00020000);
   const int vault = p.vr * p.C + p.vc, qv = vault >> 2;
   const int pol = p.obs_store;
   for (int q = t; q < n4; q += PW) {
-    const uint32_t b = s4[q];
-    float4 v = reinterpret_cast<const float4*>(p.plane0)[q];
+    const uint32_t b = __builtin_amdgcn_raw_buffer_load_b32(gs, 4 * q, 0, 0);
+    float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ps, 16 * q, 0, 0));
     obs_put(rs, pol, 16 * q,
             make_float4((float)(b & 0xff) * 0.2f, (float)((b >> 8) & 0xff) * 0.2f, (float)((b >> 16) & 0xff) * 0.2f,
                         (float)(b >> 24) * 0.2f));

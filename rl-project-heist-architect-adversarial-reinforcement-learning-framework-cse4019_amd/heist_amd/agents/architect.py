@@ -171,6 +171,81 @@ class ArchitectAgent:  # agents/architect.py:16-170
         self._clear()
         return metrics
 
+    def update_sequence(self, log_probs: torch.Tensor, values: torch.Tensor, rewards: torch.Tensor) -> Dict[str, float]:
+        """k single-transition updates in order: update() called after each layout with one
+        (log_prob, value, reward) in its buffer, k times (the reference's cadence,
+        training.py:479-480 / :558-559).  With one reward the value target is the raw
+        reward and the policy term is a constant, so update i is one Adam step on
+        value_coeff * (V(s0) - r_i)^2 (V on the constant grid state, grad-norm clipped to
+        0.5).  On a HIP device the step is captured once in a HIP graph (forward, backward,
+        clip, capturable Adam, the reward index advanced on the device) and replayed k
+        times with no host synchronisation; the first steps run eagerly as the capture's
+        warm-up.  Returns update()'s metrics for the last transition."""
+        k = int(rewards.numel())
+        if k == 0:
+            return {"architect_loss": 0.0}
+        d = self.device
+        r32 = rewards.to(device=d, dtype=torch.float32).reshape(-1)
+        lp = log_probs.to(device=d, dtype=torch.float32).reshape(-1)
+        v = values.to(device=d, dtype=torch.float32).reshape(-1)
+        self.network.train()
+        n_eager = k if d.type != "cuda" or k < 8 else 3
+        vlast = None
+        for i in range(n_eager):
+            vlast = self._value_step(r32[i])
+        if n_eager < k:
+            vl = self._replay_steps(r32[n_eager:])
+            vlast = vl[-1]
+        policy_loss = -(lp[k - 1] * (r32[k - 1] - v[k - 1]))
+        total = policy_loss + self.value_coeff * vlast
+        return {"architect_policy_loss": float(policy_loss), "architect_value_loss": float(vlast),
+                "architect_total_loss": float(total), "architect_layouts": 1,
+                "architect_avg_reward": self.total_reward / max(self.episode_count, 1)}
+
+    def _value_step(self, r: torch.Tensor) -> torch.Tensor:
+        """One eager single-reward step (update() with len(rewards) == 1); returns the value loss."""
+        new_value = self.network.value(self.grid_state()).squeeze()
+        value_loss = F.mse_loss(new_value, r)
+        self._step(self.value_coeff * value_loss, collective=False)
+        return value_loss.detach()
+
+    def _replay_steps(self, r32: torch.Tensor) -> torch.Tensor:
+        """value steps for every reward of r32 [k'] by graph replay; returns the k' value losses."""
+        k = r32.numel()
+        g = getattr(self, "_graph", None)
+        if g is None or self._g_r.numel() < k:
+            g = self._capture(max(k, 1024))
+        self._g_r[:k].copy_(r32)
+        self._g_i.zero_()
+        for _ in range(k):
+            g.replay()
+        return self._g_vl[:k].clone()
+
+    def _capture(self, cap: int):
+        d = self.device
+        for grp in self.optimizer.param_groups:  # device-side step counters: no host sync in Adam
+            grp["capturable"] = True
+        for st in self.optimizer.state.values():
+            if "step" in st and st["step"].device != d:
+                st["step"] = st["step"].to(d, torch.float32)
+        self._g_r = torch.zeros(cap, dtype=torch.float32, device=d)
+        self._g_vl = torch.zeros(cap, dtype=torch.float32, device=d)
+        self._g_i = torch.zeros(1, dtype=torch.int64, device=d)
+        self._g_s = self.grid_state()
+        params = list(self.network.parameters())
+        self.optimizer.zero_grad(set_to_none=True)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            r = self._g_r.index_select(0, self._g_i).squeeze()
+            value_loss = F.mse_loss(self.network.value(self._g_s).squeeze(), r)
+            self._g_vl.index_copy_(0, self._g_i, value_loss.detach().reshape(1))
+            (self.value_coeff * value_loss).backward()
+            nn.utils.clip_grad_norm_(params, 0.5)
+            self.optimizer.step()
+            self._g_i.add_(1)
+        self._graph = g
+        return g
+
     def _clear(self):
         self.log_probs.clear()
         self.values.clear()

@@ -449,13 +449,9 @@ class AdversarialTrainer:  # training.py:115-790
             rows[:, 3] = torch.as_tensor(self._arch_eps[:k], dtype=torch.float64, device=self.device)
         allrows, _ = dist_utils.allgather_rows(rows, self.device)
         A._clear()
-        out = {}
-        for r in allrows[torch.argsort(allrows[:, 3])].tolist():
-            A.log_probs.append(torch.tensor(r[0], dtype=torch.float32, device=self.device))
-            A.values.append(torch.tensor(r[1], dtype=torch.float32, device=self.device))
-            A.rewards.append(r[2])
-            out = A.update(collective=False)
-        return out
+        allrows = allrows[torch.argsort(allrows[:, 3], stable=True)]
+        # one update per layout, replayed from a HIP graph (ArchitectAgent.update_sequence)
+        return A.update_sequence(allrows[:, 0], allrows[:, 1], allrows[:, 2])
 
     def train_iteration(self, overrides: Optional[dict] = None, reassign: bool = True) -> Dict[str, float]:
         """One rollout of rollout_len ticks over all envs + the agents' updates.

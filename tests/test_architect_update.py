@@ -86,3 +86,35 @@ def test_architect_reward_kat():
     for s, want in table.items():
         assert rc.architect_reward_from_rate(True, float(s)) == want, s
     assert rc.architect_reward_from_rate(False, 0.3) == -1.0
+
+
+def _sequence_vs_updates(device, ks=(12,)):
+    """update_sequence (the per-layout cadence; graph-replayed on a HIP device) equals k
+    calls of update() with one transition each (agents/architect.py:91-155, one reward),
+    over consecutive sequences of lengths ks on the same agents."""
+    torch.manual_seed(5)
+    a, b = (ArchitectAgent(grid_rows=12, grid_cols=12, device=device) for _ in range(2))
+    b.network.load_state_dict(a.network.state_dict())
+    g = torch.Generator().manual_seed(9)
+    for k in ks:
+        lp, v, r = (torch.randn(k, generator=g, dtype=torch.float64) for _ in range(3))
+        for i in range(k):
+            b.log_probs.append(torch.tensor(float(lp[i]), device=device))
+            b.values.append(torch.tensor(float(v[i]), device=device))
+            b.rewards.append(float(r[i]))
+            mb = b.update(collective=False)
+        ma = a.update_sequence(lp, v, r)
+        for key in ("architect_policy_loss", "architect_value_loss", "architect_total_loss"):
+            assert abs(ma[key] - mb[key]) < 1e-6, (k, key)
+        for (n, p), q in zip(a.network.state_dict().items(), b.network.state_dict().values()):
+            torch.testing.assert_close(p, q, rtol=0, atol=1e-6, msg=n)
+
+
+def test_architect_update_sequence_cpu():
+    _sequence_vs_updates(torch.device("cpu"), ks=(12, 5))
+
+
+@pytest.mark.gpu
+def test_architect_update_sequence_gpu_graph(gpu_device):
+    # 40: the first capture (1,024 slots); 5: eager only; 1500: past the slots, captured again
+    _sequence_vs_updates(gpu_device, ks=(40, 5, 1500))

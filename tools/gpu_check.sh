@@ -45,6 +45,8 @@ for s in ${STEPS:-pytest smoke bench prof}; do
          step pmc_sq2_m 300 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD GRBM_GUI_ACTIVE -d "$OUT/pmc_sq2_m" -o heist --output-format csv -- python3 bench.py --steps 60 --warmup 20 --no-cpu-baseline --no-secondary
          python tools/pmc_summary.py "$(find "$OUT/pmc_sq_m" -name "*counter_collection.csv" | head -n 1)" step_multi_kernel "$OUT/pmc_sq_m.json" > /dev/null 2>&1
          python tools/pmc_summary.py "$(find "$OUT/pmc_sq2_m" -name "*counter_collection.csv" | head -n 1)" step_multi_kernel "$OUT/pmc_sq2_m.json" > /dev/null 2>&1; true ;;
+    archtest) step pytest_arch 600 python -u -m pytest tests/test_architect_update.py tests/test_gpu_trainer.py -k "architect or per_layout or c3" -x -v --timeout 500 --timeout-method thread ;;
+    trainq) step bench_train 900 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
     lbtest) step pytest_lb 600 python -u -m pytest tests/test_gpu_trainer.py -k "layout_batch or interactive or c3" -x -v --timeout 500 --timeout-method thread ;;
     mmodesw1) export HEIST_MULTI_WAVES=1; step multi_modes 300 python tools/probe_multi_modes.py
             step pmc_modes_m1 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d "$OUT/pmm1" -o m --output-format csv -- python3 tools/probe_multi_modes.py

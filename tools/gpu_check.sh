@@ -47,6 +47,9 @@ for s in ${STEPS:-pytest smoke bench prof}; do
          python tools/pmc_summary.py "$(find "$OUT/pmc_sq2_m" -name "*counter_collection.csv" | head -n 1)" step_multi_kernel "$OUT/pmc_sq2_m.json" > /dev/null 2>&1; true ;;
     archtest) step pytest_arch 600 python -u -m pytest tests/test_architect_update.py tests/test_gpu_trainer.py -k "architect or per_layout or c3" -x -v --timeout 500 --timeout-method thread ;;
     trainq) step bench_train 900 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ;;
+    agraph) step probe_arch_graph 300 python tools/probe_arch_graph.py ;;
+    occ) for o in 8 7 6; do HEIST_MULTI_OCC=$o step bench_occ$o 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary; done
+         HEIST_MULTI_OCC=8 step bench_occ8b 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary ;;
     lbtest) step pytest_lb 600 python -u -m pytest tests/test_gpu_trainer.py -k "layout_batch or interactive or c3" -x -v --timeout 500 --timeout-method thread ;;
     mmodesw1) export HEIST_MULTI_WAVES=1; step multi_modes 300 python tools/probe_multi_modes.py
             step pmc_modes_m1 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d "$OUT/pmm1" -o m --output-format csv -- python3 tools/probe_multi_modes.py

@@ -225,6 +225,7 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   p.multi_waves = p.step_waves;
   if (const char* m = getenv("HEIST_MULTI_WAVES")) p.multi_waves = atoi(m);
   p.multi_occ = p.multi_waves == 1 ? 4 : 8;
+  if (const char* m = getenv("HEIST_MULTI_OCC")) p.multi_occ = atoi(m);  // A/B: waves per SIMD it is built for
   if (!heist::multi_variant_exists(p.multi_waves, p.ray_chunk, p.multi_occ, p.vis_gap)) {
     p.multi_waves = p.step_waves;
     p.multi_occ = 8;

@@ -1392,9 +1392,11 @@ struct ObsLanes {
 };
 
 // Channels 0 and 2 of observation row `o` (the env's [3][R][C] floats of one tick) except
-// the solver's quad, from LDS (the tile grid and the handle's static position plane,
-// copied in at the start of the launch).  Quad q belongs to observation lane q % PW, which
-// stores the solver's quad again in write_obs_ch1_tail (program order to one address).
+// the solver's quad: the tile grid from LDS, the handle's static position plane from L2
+// (one 1.6 KB plane shared by every env; an LDS copy of it per block cost 1.6 KB of the
+// block's LDS, which held the K-tick kernel to 14 resident blocks per CU instead of 16).
+// Quad q belongs to observation lane q % PW, which stores the solver's quad again in
+// write_obs_ch1_tail (program order to one address).
 template <int NT>
 __device__ __forceinline__ void write_obs_static_lds(const EnvParams& p, const EnvLds& L, const float* plane,
                                                      float* __restrict__ o) {
@@ -1501,8 +1503,8 @@ __device__ __forceinline__ void stamp_guard_cones(const EnvLds& L, uint8_t* gvis
 // K consecutive heist_step ticks of one env per workgroup (environment.py:216-299 and
 // :347-374 K times), with actions[k][env] known up front: what env-only throughput and
 // action replay need.  The per-env state stays on chip for the whole launch -- grid, stop
-// map, patrol paths, the static position plane, the emitter records and the K actions in
-// LDS, the solver scalars in scalar registers -- and is written back once at the end;
+// map, patrol paths, the emitter records and the K actions in LDS (the static position
+// plane, one for the handle, is read from L2), the solver scalars in scalar registers -- and is written back once at the end;
 // every tick still writes its full observation row (obs[k][env], non-temporal 16-byte
 // stores), reward, done and status.  Per tick:
 //   A  every thread: the solver's move and the reward terms that precede detection
@@ -1539,9 +1541,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   const int mc = p.max_cams, mg = p.max_guards, n_slot = mc + mg;
   const int path_words = mg * p.max_path;
   const EnvLds L = carve<D>(smem, p.R, p.C, n_slot, path_words, W, mg);
-  float* plane = reinterpret_cast<float*>(smem + align16(env_lds_bytes(p.R, p.C, n_slot, path_words, D, W, mg)));
-  EmitterRaw* rec = reinterpret_cast<EmitterRaw*>(reinterpret_cast<unsigned char*>(plane) +
-                                                  align16(sizeof(float) * (size_t)RC));  // [n_slot] records
+  const float* plane = p.plane0;  // static position plane (L2)
+  EmitterRaw* rec = reinterpret_cast<EmitterRaw*>(
+      smem + align16(env_lds_bytes(p.R, p.C, n_slot, path_words, D, W, mg)));  // [n_slot] records
   uint8_t* act = reinterpret_cast<uint8_t*>(rec + n_slot);
   uint8_t* gvis = act + align16((size_t)K);  // cached guard cones of the tick, vis geometry (stamp_guard_cones)
   const EnvBase eb = env_base(p, e);
@@ -1572,7 +1574,6 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     if (t < n_slot) rec[t] = raw;
   }
   for (int i = t; i < path_words; i += NT) L.path[i] = eb.paths[i];
-  for (int i = t; i < RC; i += NT) plane[i] = p.plane0[i];
   for (int i = t; i < (int)sizeof(TieBuckets) / 4; i += NT)
     reinterpret_cast<uint32_t*>(tb)[i] = reinterpret_cast<const uint32_t*>(&kTieBuckets_)[i];
   for (int k = t; k < K; k += NT) {
@@ -2414,7 +2415,7 @@ hipError_t launch_step(const EnvParams& p, const int64_t* actions, float* obs, f
 // configuration (HEIST_STEP_WAVES=1) runs K single-tick launches instead (same results).
 #define HEIST_MULTI_VARIANTS(X) \
   X(2, 4, 8, 1024) X(2, 4, 8, 2048) X(2, 4, 8, 6144) X(4, 4, 8, 1024) X(4, 4, 8, 2048) X(4, 4, 8, 6144) \
-  X(1, 4, 4, 1024) X(1, 4, 4, 2048)
+  X(1, 4, 4, 1024) X(1, 4, 4, 2048) X(2, 4, 6, 1024) X(2, 4, 7, 1024)
 
 bool multi_variant_exists(int W, int U, int O, int D) {
 #define HEIST_HAS_MULTI(W_, U_, O_, D_) \
@@ -2427,7 +2428,7 @@ bool multi_variant_exists(int W, int U, int O, int D) {
 size_t step_multi_lds(const EnvParams& p, int K) {
   const int n_slot = p.max_cams + p.max_guards;
   return align16(env_lds_bytes(p.R, p.C, n_slot, p.max_guards * p.max_path, p.vis_gap, p.multi_waves, p.max_guards)) +
-         align16(sizeof(float) * (size_t)p.RC) + 32 * (size_t)n_slot + align16((size_t)K) + (size_t)p.vis_gap +
+         32 * (size_t)n_slot + align16((size_t)K) + (size_t)p.vis_gap +
          align16(sizeof(TieBuckets)) + 1024 * (size_t)p.multi_waves + (p.stamps ? 80 * (size_t)p.multi_waves : 0);
 }
 

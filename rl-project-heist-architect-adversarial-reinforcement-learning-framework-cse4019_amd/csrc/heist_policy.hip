@@ -65,9 +65,8 @@ struct ConvGeom {
   static constexpr int POOL = ZERO_END;                    // [64][16] f32
   static constexpr int BIAS = POOL + 64 * 16 * 4;          // b1[32] b2[64] b3[64]
   static constexpr int INVA = BIAS + 160 * 4;              // [16] f32 1/area
-  static constexpr int PM = INVA + 16 * 4;                 // [2*NT2][2][64] pool-membership bytes
   static constexpr int NT2 = (MT + 1) / 2;                 // position tiles per wave (conv2/conv3)
-  static constexpr int W2 = align16c(PM + 2 * NT2 * 128);  // conv2 fragments [2][18][64] x 16 B
+  static constexpr int W2 = align16c(INVA + 16 * 4);       // conv2 fragments [2][18][64] x 16 B
   static constexpr int SINK = W2 + 2 * 18 * 64 * 16;       // [64] x 8 B: stores of positions >= RC
   static constexpr int LDS = SINK + 64 * 8;
   static constexpr int QI = (RC + 255) / 256;              // obs cells per thread
@@ -213,16 +212,18 @@ __device__ __forceinline__ void stage_obs(unsigned char* smem, const float (&v)[
 
 // Epilogue of a D[channel][position] tile: lane holds position m = 32t + (l & 31) and, in
 // register 4g + i, channel n0 + i with n0 = 8g + 4h; relu(acc + bias) -> 4 bf16 -> 8 bytes.
+// bias: the lane's 4 float4 of channels nbase + 8g + 4h (g = 0..3), held in registers (an
+// LDS bias read here would be a full lgkmcnt(0) drain per group, serialised per tile).
 template <int R, int C, int S, int PB>
-__device__ __forceinline__ void store_chan_major(unsigned char* dst, const float* bias, int nbase, const f32x16& acc,
-                                                 int m, int h) {
+__device__ __forceinline__ void store_chan_major(unsigned char* dst, const float4 (&bias)[4], int nbase,
+                                                 const f32x16& acc, int m, int h) {
   using G = ConvGeom<R, C>;
   if (m >= G::RC) return;
   const int po = pos_off<R, C, S, PB>(m);
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int n0 = nbase + 8 * g + 4 * h;
-    const float4 b = *reinterpret_cast<const float4*>(bias + n0);
+    const float4 b = bias[g];
     bf16x4 o;
     o[0] = (__bf16)relu(acc[4 * g + 0] + b.x);
     o[1] = (__bf16)relu(acc[4 * g + 1] + b.y);
@@ -274,22 +275,34 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
     const int area = (pool_hi(ci, R) - pool_lo(ci, R)) * (pool_hi(cj, C) - pool_lo(cj, C));
     reinterpret_cast<float*>(smem + G::INVA)[tid] = 1.0f / (float)area;
   }
-  for (int i = tid; i < 2 * G::NT2 * 128; i += 256) {  // pool membership of the P fragment bits
-    const int t = i >> 7, s = (i >> 6) & 1, ll = i & 63;
-    const int cell = ll & 31, hh = ll >> 5;
-    unsigned bits = 0;
-    if (cell < 16) {
-      const int ci = cell >> 2, cj = cell & 3;
-      for (int j = 0; j < 8; ++j) {
-        const int m = 32 * t + 16 * s + 8 * (j >> 2) + 4 * hh + (j & 3);
-        if (m < G::RC) {
-          const int oy = m / C, ox = m - (m / C) * C;
-          if (oy >= pool_lo(ci, R) && oy < pool_hi(ci, R) && ox >= pool_lo(cj, C) && ox < pool_hi(cj, C))
-            bits |= 1u << j;
+  // conv1 bias and the pool membership of the lane's P fragments in registers for the whole
+  // kernel: an LDS read of either inside the MFMA streams costs a full lgkmcnt(0) drain of
+  // the read ring (12 per env in conv3, 16 in conv1's epilogue).  Byte 2 i + s of pbits =
+  // P fragment s of the wave's tile i (mh + 2 i): bit j set iff row (cell) lr of the
+  // fragment pools position 32 tp + 16 s + 8 (j >> 2) + 4 h + (j & 3).
+  float4 b1v[4];
+#pragma unroll
+  for (int g = 0; g < 4; ++g) b1v[g] = *reinterpret_cast<const float4*>(gbias + 8 * g + 4 * h);
+  uint32_t pbits[(2 * G::NT2 + 3) / 4] = {};
+  if (lr < 16) {
+    const int ci = lr >> 2, cj = lr & 3;
+    for (int i = 0; i < G::NT2; ++i) {
+      for (int s = 0; s < 2; ++s) {
+        unsigned bits = 0;
+        for (int j = 0; j < 8; ++j) {
+          const int m = 32 * (mh + 2 * i) + 16 * s + 8 * (j >> 2) + 4 * h + (j & 3);
+          if (m < G::RC) {
+            const int oy = m / C, ox = m - (m / C) * C;
+            if (oy >= pool_lo(ci, R) && oy < pool_hi(ci, R) && ox >= pool_lo(cj, C) && ox < pool_hi(cj, C))
+              bits |= 1u << j;
+          }
         }
+        const int b = 2 * i + s;
+#pragma unroll
+        for (int d = 0; d < (2 * G::NT2 + 3) / 4; ++d)
+          if (d == (b >> 2)) pbits[d] |= bits << (8 * (b & 3));
       }
     }
-    smem[G::PM + i] = (unsigned char)bits;
   }
 
   // conv1 per-lane tap offsets: k-step s covers taps 4s + 2h, 4s + 2h + 1 (taps >= 9 have
@@ -334,7 +347,7 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
       f32x16 acc = {};
 #pragma unroll
       for (int s = 0; s < kW1Steps; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1[s], f1[i][s], acc, 0, 0, 0);
-      store_chan_major<R, C, G::S1, G::PB1>(smem + G::A1, bias, 0, acc, 32 * (w + 4 * i) + lr, h);
+      store_chan_major<R, C, G::S1, G::PB1>(smem + G::A1, b1v, 0, acc, 32 * (w + 4 * i) + lr, h);
     }
   }
   __syncthreads();  // act1 of the first env ready
@@ -396,10 +409,10 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
       // element per MFMA gap, so it issues under the matrix core instead of stalling it
       f32x16 prev = {};
       bf16x8 x[2], pf[2];
-      auto pool_piece = [&](int tp, int s) {  // piece s of tile tp's epilogue (prev holds its sums)
+      auto pool_piece = [&](int ti, int s) {  // piece s of the wave's tile ti's epilogue (prev holds its sums)
         if (s < 16) x[s >> 3][s & 7] = (__bf16)relu(prev[s] + b3v);
         if (s == 0 || s == 1) {
-          const unsigned bits = smem[G::PM + (tp * 2 + s) * 64 + l];
+          const unsigned bits = (pbits[(2 * ti + s) >> 2] >> (8 * ((2 * ti + s) & 3))) & 0xffu;
 #pragma unroll
           for (int j = 0; j < 8; ++j) pf[s][j] = ((bits >> j) & 1u) ? (__bf16)1.0f : (__bf16)0.0f;
         }
@@ -415,14 +428,14 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
           const bf16x8 f = ring[q % kPre];
           if (q + kPre < NQ) ring[q % kPre] = rd(q + kPre);
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, in_agpr(w3[s]), acc, 0, 0, 0);
-          if (i > 0 && s < 18) pool_piece(mh + 2 * (i - 1), s);
+          if (i > 0 && s < 18) pool_piece(i - 1, s);
         }
         prev = acc;
       }
       __builtin_amdgcn_sched_group_barrier(0x100, kPre, 0);
       sched_ring<kW3Steps, 0>(std::make_integer_sequence<int, NQ>{});
 #pragma unroll
-      for (int s = 0; s < 18; ++s) pool_piece(mh + 2 * (NT2 - 1), s);  // the last tile's epilogue
+      for (int s = 0; s < 18; ++s) pool_piece(NT2 - 1, s);  // the last tile's epilogue
       // conv1 of the next env (its input plane was staged before B3): all reads first,
       // then tile by tile (also after the last env: harmless)
       {
@@ -434,7 +447,7 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
           f32x16 a1 = {};
 #pragma unroll
           for (int k = 0; k < kW1Steps; ++k) a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(w1[k], g1[j][k], a1, 0, 0, 0);
-          store_chan_major<R, C, G::S1, G::PB1>(smem + G::A1, bias, 0, a1, 32 * (w + 4 * j) + lr, h);
+          store_chan_major<R, C, G::S1, G::PB1>(smem + G::A1, b1v, 0, a1, 32 * (w + 4 * j) + lr, h);
         }
       }
     }

@@ -106,8 +106,14 @@ def _sequence_vs_updates(device, ks=(12,)):
         ma = a.update_sequence(lp, v, r)
         for key in ("architect_policy_loss", "architect_value_loss", "architect_total_loss"):
             assert abs(ma[key] - mb[key]) < 1e-6, (k, key)
+        # parameters: within fp32 noise amplified by Adam (a gradient element at rounding-noise
+        # level takes a step of up to lr whatever its size; the graph's backward and capturable
+        # Adam round differently from the eager ones: measured max 4.2e-6 = 0.014 lr over 40
+        # steps, profiles/r03c_probe_arch_graph.log); exact equality on CPU (both eager)
+        tol = 1e-5 if device.type == "cuda" else 1e-6
         for (n, p), q in zip(a.network.state_dict().items(), b.network.state_dict().values()):
-            torch.testing.assert_close(p, q, rtol=0, atol=1e-6, msg=n)
+            d = float((p - q).abs().max())
+            assert d <= tol, (k, n, d)
 
 
 def test_architect_update_sequence_cpu():

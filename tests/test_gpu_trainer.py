@@ -245,6 +245,8 @@ def test_per_layout_architect_updates(gpu_device, tmp_path):
         ref.values.append(torch.tensor(v, device=gpu_device))
         ref.rewards.append(r)
         ref.update()
+    # the trainer replays the updates from a HIP graph (ArchitectAgent.update_sequence):
+    # equal to the eager replay within Adam-amplified fp32 noise (test_architect_update.py)
     for k, v in ref.network.state_dict().items():
-        torch.testing.assert_close(got[k], v, rtol=0, atol=1e-6)
+        torch.testing.assert_close(got[k], v, rtol=0, atol=1e-5)
     del ro

@@ -220,9 +220,11 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
     p.step_occ = 8;
     p.vis_gap = heist::vis_gap_for(R, C);
   }
-  // K-tick kernel: the step kernel's waves per env unless HEIST_MULTI_WAVES says otherwise
-  // (1 wave per env runs at 4 waves per SIMD with 128 VGPRs)
-  p.multi_waves = p.step_waves;
+  // K-tick kernel: one wave per env (every role in one wave, 96 VGPRs, 5 waves per SIMD, no
+  // spills) once the batch gives every SIMD 4 of them -- 4096 envs: 11.9 us per tick vs 13.1
+  // at 2 waves per env (8 per SIMD, 64 VGPRs + 52 spilled), profiles/r03d_bench_w*.log --
+  // else the step kernel's waves per env; HEIST_MULTI_WAVES overrides
+  p.multi_waves = (size_t)n_envs >= 16 * (size_t)n_cu ? 1 : p.step_waves;
   if (const char* m = getenv("HEIST_MULTI_WAVES")) p.multi_waves = atoi(m);
   p.multi_occ = p.multi_waves == 1 ? 4 : 8;
   if (const char* m = getenv("HEIST_MULTI_OCC")) p.multi_occ = atoi(m);  // A/B: waves per SIMD it is built for

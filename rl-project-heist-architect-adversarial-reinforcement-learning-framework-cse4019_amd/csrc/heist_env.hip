@@ -375,28 +375,32 @@ __device__ __forceinline__ uint32_t or_b32(uint32_t a, uint32_t b) {
 // rounded once, as v_fma_f32 does); K is an integer inline constant, i.e. the denormal
 // K * 2^-149, applied to both halves (op_sel_hi).  Inline asm: the compiler's own packed
 // form of this loop is miscompiled by ROCm 7.2 clang (see march_fast).
-template <int K>
+// VM: the addend m (the ray origin) per lane in VGPRs instead of wave-uniform in SGPRs.
+template <int K, bool VM = false>
 __device__ __forceinline__ uint64_t pk_fma_k(uint64_t d, uint64_t m) {
   static_assert(K >= 1 && K <= 12, "inline constant");
   uint64_t r;
-#define HEIST_PKC(n) \
-  if constexpr (K == n) asm("v_pk_fma_f32 %0, %1, " #n ", %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(d), "s"(m));
+#define HEIST_PKC(n)                                                                              \
+  if constexpr (K == n) {                                                                         \
+    if constexpr (VM) asm("v_pk_fma_f32 %0, %1, " #n ", %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(d), "v"(m)); \
+    else asm("v_pk_fma_f32 %0, %1, " #n ", %2 op_sel_hi:[1,0,1]" : "=v"(r) : "v"(d), "s"(m));  \
+  }
   HEIST_PKC(1) HEIST_PKC(2) HEIST_PKC(3) HEIST_PKC(4) HEIST_PKC(5) HEIST_PKC(6)
   HEIST_PKC(7) HEIST_PKC(8) HEIST_PKC(9) HEIST_PKC(10) HEIST_PKC(11) HEIST_PKC(12)
 #undef HEIST_PKC
   return r;
 }
 
-template <int U>
+template <int U, bool VM>
 __device__ __forceinline__ uint32_t fast_addr(uint32_t PC, uint64_t d, uint64_t m) {
-  const uint64_t r = pk_fma_k<U + 1>(d, m);
+  const uint64_t r = pk_fma_k<U + 1, VM>(d, m);
   return __umul24((uint32_t)(r >> 32), PC) + (uint32_t)r;
 }
 
-template <int NS, int... Us>
+template <int NS, bool VM, int... Us>
 __device__ __forceinline__ void fast_addrs(uint32_t (&a)[NS], uint32_t PC, uint64_t d, uint64_t m,
                                            std::integer_sequence<int, Us...>) {
-  ((a[Us] = fast_addr<Us>(PC, d, m)), ...);
+  ((a[Us] = fast_addr<Us, VM>(PC, d, m)), ...);
 }
 
 // Every sample k = 1 .. n_samp of a fast ray in one LDS round trip.  Coordinates are
@@ -416,13 +420,14 @@ __device__ __forceinline__ void fast_addrs(uint32_t (&a)[NS], uint32_t PC, uint6
 // sample count up to and including the sample that ends it (n_samp if none does), when
 // COUNT.  Scalar fp32 on purpose (and this file builds with -fno-slp-vectorize): ROCm 7.2
 // clang miscompiles the float2 / v_pk_fma_f32 form of this loop (a lane's negation is lost).
-template <int D, int NS, bool CLAMP, bool COUNT>
+// VM: the origin (mx, my, own) differs per lane (packed direction-group marches).
+template <int D, int NS, bool CLAMP, bool COUNT, bool VM = false>
 __device__ __forceinline__ int march_fast(uint32_t PC, uint32_t own, float dxs, float dys, float mx, float my,
                                           int n_samp) {
   uint32_t a[NS], w[NS];
   const uint64_t dv = ((uint64_t)__builtin_bit_cast(uint32_t, dys) << 32) | __builtin_bit_cast(uint32_t, dxs);
   const uint64_t mv = ((uint64_t)__builtin_bit_cast(uint32_t, my) << 32) | __builtin_bit_cast(uint32_t, mx);
-  if constexpr (!CLAMP) fast_addrs(a, PC, dv, mv, std::make_integer_sequence<int, NS>{});
+  if constexpr (!CLAMP) fast_addrs<NS, VM>(a, PC, dv, mv, std::make_integer_sequence<int, NS>{});
 #pragma unroll
   for (int u = 0; u < NS; ++u) {
     if (CLAMP) {
@@ -536,6 +541,15 @@ __device__ __forceinline__ int emitter_of_chunk(const EnvLds& L, int n_em, int k
 // directions in LDS), which is marched 64 at a time (and whenever the group changes): an
 // Architect camera fan of 0.5-degree rays has about a third as many distinct sequences as
 // rays.  tb: the tie bucket tables in LDS.
+// HEIST_PACK_FLUSH (build-time A/B switch, default 1): with two or more waves per env the
+// K-tick kernel's dedup flush packs (member, direction) pairs over the lanes (13.1 vs 13.5 us
+// per 4096-env tick at 2 waves); one wave per env keeps one march per member with a
+// wave-uniform origin (11.8 vs 12.15 us packed: the per-lane origins cost it registers),
+// profiles/r03f_bench_*pack*.log.
+#ifndef HEIST_PACK_FLUSH
+#define HEIST_PACK_FLUSH 1
+#endif
+
 template <int NT, int U, int D, bool COUNT, bool DEDUP = false>
 __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int probe, const double* hd,
                           const TieBuckets* tb = nullptr, float2* uq = nullptr) {
@@ -556,21 +570,42 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
   // DEDUP: the unique queue of group uk (uqn entries); flush(n) marches entries 0 .. n-1
   int uqn = 0, uk = -1;
   if (DEDUP) uq += wave * 128;
+  constexpr bool kPackFlush = HEIST_PACK_FLUSH != 0 && W >= 2;
+  // flush(cnt): the group's cnt unique directions uq[0 .. cnt) from each of its `members`
+  // tiles, packed as (member, direction) pairs p = m * cnt + j over the lanes, 64 pairs per
+  // march (a 2-camera group of <= 32 unique directions: one march instead of two)
   auto flush = [&](int cnt) {
     const Emit Eq = uni(L.em[uk]);
     const int n_samp = Eq.kind == 0 ? 2 * Eq.range : Eq.range;
-    if (lane < cnt) {
-      const float2 d = uq[lane];
+    const int n_pair = kPackFlush ? Eq.members * cnt : cnt;
+    for (int p0 = 0; p0 < n_pair; p0 += 64) {
+      int j = p0 + lane, m = 0;
+      if (kPackFlush)
+        for (int mm = 1; mm < Eq.members; ++mm)  // m = pair / cnt, j = pair % cnt (members is small)
+          if (j >= cnt) {
+            j -= cnt;
+            ++m;
+          }
+      if (p0 + lane >= n_pair) continue;
+      const float2 d = uq[j];
       auto group = [&](auto ns, auto clamp) {
         constexpr int NS = decltype(ns)::value;
         constexpr bool CL = decltype(clamp)::value;
-        for (int m = 0; m < Eq.members; ++m) {
-          const int row = m == 0 ? Eq.row : uni(L.em[uk + m].row);
-          const int col = m == 0 ? Eq.col : uni(L.em[uk + m].col);
+        if constexpr (kPackFlush) {
+          const int row = L.em[uk + m].row, col = L.em[uk + m].col;
           const uint32_t own = base + (uint32_t)((row + kRing) * PC + (col + kRing));
           const float mx = __builtin_bit_cast(float, base + (uint32_t)(col + kRing));
           const float my = __builtin_bit_cast(float, (uint32_t)(row + kRing));
-          march_fast<D, NS, CL, false>(PC, own, d.x, d.y, mx, my, n_samp);
+          march_fast<D, NS, CL, false, true>(PC, own, d.x, d.y, mx, my, n_samp);
+        } else {  // one march per member, origin in SGPRs
+          for (int mm = 0; mm < Eq.members; ++mm) {
+            const int row = mm == 0 ? Eq.row : uni(L.em[uk + mm].row);
+            const int col = mm == 0 ? Eq.col : uni(L.em[uk + mm].col);
+            const uint32_t own = base + (uint32_t)((row + kRing) * PC + (col + kRing));
+            const float mx = __builtin_bit_cast(float, base + (uint32_t)(col + kRing));
+            const float my = __builtin_bit_cast(float, (uint32_t)(row + kRing));
+            march_fast<D, NS, CL, false>(PC, own, d.x, d.y, mx, my, n_samp);
+          }
         }
       };
       if (n_samp == 2 * kTieMaxRange)
@@ -2415,7 +2450,7 @@ hipError_t launch_step(const EnvParams& p, const int64_t* actions, float* obs, f
 // configuration (HEIST_STEP_WAVES=1) runs K single-tick launches instead (same results).
 #define HEIST_MULTI_VARIANTS(X) \
   X(2, 4, 8, 1024) X(2, 4, 8, 2048) X(2, 4, 8, 6144) X(4, 4, 8, 1024) X(4, 4, 8, 2048) X(4, 4, 8, 6144) \
-  X(1, 4, 4, 1024) X(1, 4, 4, 2048) X(2, 4, 6, 1024) X(2, 4, 7, 1024)
+  X(1, 4, 4, 1024) X(1, 4, 4, 2048) X(2, 4, 6, 1024) X(2, 4, 7, 1024) X(1, 4, 5, 1024) X(1, 4, 6, 1024)
 
 bool multi_variant_exists(int W, int U, int O, int D) {
 #define HEIST_HAS_MULTI(W_, U_, O_, D_) \

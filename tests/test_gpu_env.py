@@ -646,18 +646,20 @@ def test_step_multi_c2_checkpoint_layouts(gpu_device):
         assert torch.equal(obs[k], o) and torch.equal(done[k], d) and torch.equal(status[k], s), k
 
 
+@pytest.mark.parametrize("waves", [1, 2])
 @pytest.mark.parametrize("cones", [True, False], ids=["guard_cones", "live_guards"])
-def test_step_multi_one_wave_per_env(gpu_device, monkeypatch, cones):
+def test_step_multi_one_wave_per_env(gpu_device, monkeypatch, cones, waves):
     """The K-tick kernel's one-wave-per-env form (HEIST_MULTI_WAVES=1: every role on one
-    wave, 128-VGPR budget) == single ticks, bit for bit, with short episodes."""
+    wave, the default from 16 envs per CU) and its two-wave form == single ticks, bit for
+    bit, with short episodes."""
     n, R = 384, 20
     cfg = EnvironmentConfig(max_steps=25)
     lays = synthetic_layouts(n, R, R, 15, seed=67)
-    monkeypatch.setenv("HEIST_MULTI_WAVES", "1")
+    monkeypatch.setenv("HEIST_MULTI_WAVES", str(waves))
     a = HeistEnv(n, cfg, device=gpu_device)
     monkeypatch.delenv("HEIST_MULTI_WAVES")
     b = HeistEnv(n, cfg, device=gpu_device)
-    assert a.kernel_config()["multi_waves"] == 1
+    assert a.kernel_config()["multi_waves"] == waves
     for env in (a, b):
         env.set_guard_cones(cones)
         env.set_layouts(lays, budget=15)

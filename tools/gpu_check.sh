@@ -50,6 +50,15 @@ for s in ${STEPS:-pytest smoke bench prof}; do
     agraph) step probe_arch_graph 300 python tools/probe_arch_graph.py ;;
     occ) for o in 8 7 6; do HEIST_MULTI_OCC=$o step bench_occ$o 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary; done
          HEIST_MULTI_OCC=8 step bench_occ8b 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary ;;
+    occ1) HEIST_MULTI_OCC=8 step bench_w2o8 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary
+          for o in 4 6; do HEIST_MULTI_WAVES=1 HEIST_MULTI_OCC=$o step bench_w1o$o 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary; done
+          HEIST_MULTI_OCC=8 step bench_w2o8b 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary ;;
+    pab) NP=$PWD/rl-project-heist-architect-adversarial-reinforcement-learning-framework-cse4019_amd/heist_amd/libheist_hip_nopack.so
+         for i in 1 2; do for w in 1 2; do
+           HEIST_MULTI_WAVES=$w step bench_pack_w${w}_$i 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary
+           HEIST_LIB=$NP HEIST_MULTI_WAVES=$w step bench_nopack_w${w}_$i 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary
+         done; done
+         for w in 1 2; do HEIST_MULTI_WAVES=$w step bench_syn_w$w 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary --layouts synthetic; done ;;
     lbtest) step pytest_lb 600 python -u -m pytest tests/test_gpu_trainer.py -k "layout_batch or interactive or c3" -x -v --timeout 500 --timeout-method thread ;;
     mmodesw1) export HEIST_MULTI_WAVES=1; step multi_modes 300 python tools/probe_multi_modes.py
             step pmc_modes_m1 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d "$OUT/pmm1" -o m --output-format csv -- python3 tools/probe_multi_modes.py

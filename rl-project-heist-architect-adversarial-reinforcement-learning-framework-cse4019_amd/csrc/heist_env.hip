@@ -1489,6 +1489,83 @@ __device__ __forceinline__ void write_obs_ch1_tail(const EnvParams& p, const Env
   }
 }
 
+// One-wave K-tick kernel (SOLO): the lane's observation quads q = lane + 64 j (j < kObsQ) keep
+// what does not change within a launch in registers -- channel 0 (tile / 5) and channel 2
+// (the static plane, vault patched) as float4, and the LDS offset of the quad's 4 visibility
+// bytes -- so a tick's observation is 2 stores per quad from registers plus one LDS read and
+// 4 conversions for channel 1.  Loading the plane and converting the grid every tick cost
+// VALU, and the loop's in-order vmcnt made each iteration wait for the previous stores.
+constexpr int kObsQ = 2;  // quads per lane: R * C <= 4 * 64 * kObsQ (20 x 20: 100 quads)
+struct ObsRegs {
+  float4 ch0[kObsQ], ch2[kObsQ];
+  int vis[kObsQ];
+};
+__device__ __forceinline__ void obs_regs_init(const EnvParams& p, const EnvLds& L, ObsRegs& R) {
+  const int lane = threadIdx.x & 63, n4 = p.RC / 4, c4 = p.C / 4;
+  const int vault = p.vr * p.C + p.vc, qv = vault >> 2;
+#pragma unroll
+  for (int j = 0; j < kObsQ; ++j) {
+    const int q = lane + 64 * j;
+    const int qc = q < n4 ? q : n4 - 1;
+    const uint32_t b = *reinterpret_cast<const uint32_t*>(L.grid + 4 * qc);
+    R.ch0[j] = make_float4((float)(b & 0xff) * 0.2f, (float)((b >> 8) & 0xff) * 0.2f, (float)((b >> 16) & 0xff) * 0.2f,
+                           (float)(b >> 24) * 0.2f);
+    float4 v = reinterpret_cast<const float4*>(p.plane0)[qc];
+    if (qc == qv) patch4(v, vault & 3, p.vault_val);
+    R.ch2[j] = v;
+    const int r = qc / c4;
+    R.vis[j] = L.at(r, 4 * (qc - r * c4));
+  }
+}
+// The tick's observation row o from ObsRegs: channels 0 and 2 (static part) when STATIC,
+// else channel 1 (ray plane | guard plane) and the solver's quad of channel 2.
+template <bool STATIC>
+__device__ __forceinline__ void write_obs_regs(const EnvParams& p, const EnvScalars& s, const EnvLds& L,
+                                               const uint8_t* gvis, const ObsRegs& R, float* __restrict__ o) {
+  const int lane = threadIdx.x & 63, n4 = p.RC / 4;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(o, (short)0, 12 * p.RC, 0x00020000);
+  auto body = [&](auto pol) {
+    constexpr int P = decltype(pol)::value;
+#pragma unroll
+    for (int j = 0; j < kObsQ; ++j) {
+      const int q = lane + 64 * j;
+      if (q >= n4) break;
+      if constexpr (STATIC) {
+        obs_put(rs, P, 16 * q, R.ch0[j]);
+        obs_put(rs, P, 16 * (2 * n4 + q), R.ch2[j]);
+      } else {
+        uint32_t v;
+        if ((kRing & 3) == 0) {
+          v = *reinterpret_cast<const uint32_t*>(L.vis + R.vis[j]) | *reinterpret_cast<const uint32_t*>(gvis + R.vis[j]);
+        } else {
+          const uint16_t* vp2 = reinterpret_cast<const uint16_t*>(L.vis + R.vis[j]);
+          const uint16_t* gp2 = reinterpret_cast<const uint16_t*>(gvis + R.vis[j]);
+          v = ((uint32_t)vp2[0] | ((uint32_t)vp2[1] << 16)) | ((uint32_t)gp2[0] | ((uint32_t)gp2[1] << 16));
+        }
+        obs_put(rs, P, 16 * (n4 + q),
+                make_float4((float)(v & 0xff), (float)((v >> 8) & 0xff), (float)((v >> 16) & 0xff), (float)(v >> 24)));
+      }
+    }
+    if constexpr (!STATIC) {
+      const int solver = s.pos_r * p.C + s.pos_c, qs = solver >> 2;
+      if ((qs & 63) == lane) {
+        const int vault = p.vr * p.C + p.vc;
+        float4 v = reinterpret_cast<const float4*>(p.plane0)[qs];
+        patch4(v, solver & 3, p.plane1[solver]);
+        if (qs == (vault >> 2)) patch4(v, vault & 3, p.vault_val);
+        obs_put(rs, P, 16 * (2 * n4 + qs), v);
+      }
+    }
+  };
+  // the store policy is a launch constant: one branch here instead of one per store
+  switch (p.obs_store) {
+    case 1: body(std::integral_constant<int, 1>{}); break;
+    case 2: body(std::integral_constant<int, 2>{}); break;
+    case 3: body(std::integral_constant<int, 3>{}); break;
+    default: body(std::integral_constant<int, 0>{}); break;
+  }
+}
+
 // The ray plane and the guard plane zeroed by the observation lanes.
 template <int NT>
 __device__ __forceinline__ void clear_planes(const EnvParams& p, const EnvLds& L, uint8_t* gvis, bool rays) {
@@ -1619,6 +1696,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   const int g = t - mc;
   const bool live_cam = t < s.n_cams, live_guard = g >= 0 && g < s.n_guards;
   bool cached = false;
+  // one wave per env: the observation's per-launch constants in registers (ObsRegs)
+  const bool reg_obs = SOLO && p.RC <= 256 * kObsQ;
+  ObsRegs obr;
   // a cached guard's cone entry for the coming tick, loaded one tick ahead: the pose after
   // its move (idx + step, nslot) if the env acts and the patrol has >= 2 points
   // (security.py:147), else the pose it holds
@@ -1644,6 +1724,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     dst[1] = cb;
   };
   __syncthreads();  // records in LDS
+  if (SOLO && reg_obs) obs_regs_init(p, L, obr);
   if (live_guard) {
     const Guard gd = as_guard(rec[t]);
     cached = gd.hslot != kUncached;
@@ -1726,7 +1807,12 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
         HEIST_MULTI_STAMP(1);  // 1: emitter update
         publish_emitters(L, E, n_slot);
       }
-      if (!(PROBE & 2)) write_obs_static_lds<NT>(p, L, plane, obs + ((size_t)k * N + e) * 3 * RC);
+      if (!(PROBE & 2)) {
+        if (SOLO && reg_obs)
+          write_obs_regs<true>(p, s, L, gvis, obr, obs + ((size_t)k * N + e) * 3 * RC);
+        else
+          write_obs_static_lds<NT>(p, L, plane, obs + ((size_t)k * N + e) * 3 * RC);
+      }
       clear_planes<NT>(p, L, gvis, true);
     } else {  // the emitters with every guard back at patrol point 0, headings kept
       if (w0) {
@@ -1833,7 +1919,12 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
         status_out[ko] = (int8_t)status;
       }
     }
-    if (!(PROBE & 2)) write_obs_ch1_tail<NT>(p, s, L, gvis, obs + ((size_t)k * N + e) * 3 * RC);
+    if (!(PROBE & 2)) {
+      if (SOLO && reg_obs)
+        write_obs_regs<false>(p, s, L, gvis, obr, obs + ((size_t)k * N + e) * 3 * RC);
+      else
+        write_obs_ch1_tail<NT>(p, s, L, gvis, obs + ((size_t)k * N + e) * 3 * RC);
+    }
     HEIST_MULTI_STAMP(7);  // 7: outputs, channel 1 + solver quad
     ++k;
   }
@@ -2446,8 +2537,9 @@ hipError_t launch_step(const EnvParams& p, const int64_t* actions, float* obs, f
   return hipErrorInvalidValue;
 }
 
-// K ticks per launch: (W, U, O, D) variants with two or more waves per env; another
-// configuration (HEIST_STEP_WAVES=1) runs K single-tick launches instead (same results).
+// K ticks per launch: the (W, U, O, D) variants below, for grids with C % 4 == 0 (the
+// observation rows go out as float4 quads that never cross a grid row); another
+// configuration runs K single-tick launches instead (same results).
 #define HEIST_MULTI_VARIANTS(X) \
   X(2, 4, 8, 1024) X(2, 4, 8, 2048) X(2, 4, 8, 6144) X(4, 4, 8, 1024) X(4, 4, 8, 2048) X(4, 4, 8, 6144) \
   X(1, 4, 4, 1024) X(1, 4, 4, 2048) X(2, 4, 6, 1024) X(2, 4, 7, 1024) X(1, 4, 5, 1024) X(1, 4, 6, 1024)
@@ -2485,7 +2577,7 @@ hipError_t launch_step_multi(const EnvParams& p, const EnvParams* pg, int K, con
   }
 #define HEIST_MULTI_CASE(W, U, O, D)                                                                        \
   if (p.multi_waves == W && p.ray_chunk == U && p.multi_occ == O && p.vis_gap == D && p.probe_mode == 0 && \
-      !p.sample_counter && !p.redo_counter) {                                                                \
+      !p.sample_counter && !p.redo_counter && (p.C & 3) == 0) {                                            \
     if (p.stamps)                                                                                            \
       hipLaunchKernelGGL((step_multi_kernel<W, U, O, D, true>), dim3(p.n_envs), dim3(64 * W), lds, st, p, K,  \
                          actions, obs, rew, rew64, done_out, status_out, auto_reset);                         \

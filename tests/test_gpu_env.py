@@ -667,3 +667,24 @@ def test_step_multi_one_wave_per_env(gpu_device, monkeypatch, cones, waves):
     g = torch.Generator(device="cpu").manual_seed(68)
     acts = torch.randint(0, 5, (60, n), generator=g).to(gpu_device)
     _compare_multi_vs_single(a, b, acts, [13, 47])
+
+
+@pytest.mark.parametrize("waves", [1, 2])
+@pytest.mark.parametrize("R,C", [(13, 17), (9, 23), (16, 20)])
+def test_step_multi_any_grid_width(gpu_device, monkeypatch, waves, R, C):
+    """heist_step_multi on grids whose width is not a multiple of 4 (the K-tick kernel's
+    float4 rows need C % 4 == 0; other widths run K single ticks) and on a 16 x 20 grid (the
+    kernel itself) == single ticks."""
+    n = 256
+    cfg = EnvironmentConfig(grid_rows=R, grid_cols=C, max_steps=30)
+    lays = synthetic_layouts(n, R, C, 15, seed=69)
+    monkeypatch.setenv("HEIST_MULTI_WAVES", str(waves))
+    a = HeistEnv(n, cfg, device=gpu_device)
+    monkeypatch.delenv("HEIST_MULTI_WAVES")
+    b = HeistEnv(n, cfg, device=gpu_device)
+    for env in (a, b):
+        env.set_layouts(lays, budget=15)
+        env.reset()
+    g = torch.Generator(device="cpu").manual_seed(70)
+    acts = torch.randint(0, 5, (45, n), generator=g).to(gpu_device)
+    _compare_multi_vs_single(a, b, acts, [20, 25])

@@ -419,7 +419,7 @@ def main():
             if tj.get("workload") == args.layouts and tj.get("ticks_per_launch", 1) == K:
                 traffic = tj.get("hbm_bytes_per_tick", tj.get("hbm_bytes_per_launch"))
                 traffic_src = "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this command (%s), corrected per " \
-                              "MI355X_MICROARCH.md: profiles/heist_step_traffic.json" % tj.get("profile", "?")
+                              "MI355X_MICROARCH.md, per tick: profiles/%s" % (tj.get("profile", "?"), os.path.basename(tf))
         line = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,

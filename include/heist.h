@@ -129,9 +129,9 @@ int heist_step_stamps(heist_t h, uint64_t* buf);
 int heist_step_waves(heist_t h);
 
 /* The handle's effective kernel configuration, no reference counterpart (what a benchmark
- * records next to its numbers): out[0..n) with n <= 11 receives step_waves, ray_chunk,
+ * records next to its numbers): out[0..n) with n <= 12 receives step_waves, ray_chunk,
  * step_occ, vis_gap, obs_store, ray_mode, probe_mode, dispatch_order, split_obs,
- * guard_cones, multi_waves (the HEIST_* environment knobs as heist_create resolved them,
+ * guard_cones, multi_waves, fan_on (the HEIST_* environment knobs as heist_create resolved them,
  * then any heist_set_* calls).  probe_mode != 0 selects the profiling step kernel, whose results are
  * wrong by design (phases skipped). */
 int heist_get_config(heist_t h, int32_t* out, int n);

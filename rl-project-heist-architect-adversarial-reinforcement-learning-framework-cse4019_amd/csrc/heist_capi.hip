@@ -70,7 +70,7 @@ using heist::EnvParams;
 struct heist_env {
   int device;
   EnvParams p;
-  void* allocs[12];
+  void* allocs[13];
   int n_allocs;
   EnvParams* dev_p;  // device copy of p for the K-tick kernel (read through a pointer, not as kernel arguments)
   EnvParams dev_p_host;  // what dev_p holds
@@ -256,6 +256,7 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
       // guard cone cache: 64 B per (guard, patrol index, heading slot)
       sizeof(uint16_t) * heist::kConeEntry * n * (max_guards > 0 ? max_guards : 1) * heist::kConePath * heist::kConeSlots,
       sizeof(EnvParams),
+      sizeof(heist::FanTick) * heist::kFanTicks,
   };
   h->n_allocs = 0;
   for (size_t k = 0; k < sizeof(sizes) / sizeof(sizes[0]); ++k) {
@@ -282,6 +283,9 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   p.stop_bytes = heist::stop_map_bytes(R, C);
   p.cones = (uint16_t*)h->allocs[10];
   h->dev_p = (EnvParams*)h->allocs[11];
+  p.fan = (heist::FanTick*)h->allocs[12];
+  p.fan_on = 1;
+  if (const char* f = getenv("HEIST_SHARED_FAN")) p.fan_on = atoi(f) ? 1 : 0;
   h->dev_p_valid = false;
   p.guard_cones = 1;
   if (const char* gc = getenv("HEIST_GUARD_CONES")) p.guard_cones = atoi(gc) ? 1 : 0;
@@ -404,10 +408,10 @@ int heist_step_waves(heist_t h) {
 
 int heist_get_config(heist_t h, int32_t* out, int n) {
   if (int rc = check_handle(h)) return rc;
-  HEIST_REQUIRE(out != nullptr && n >= 0 && n <= 11, "heist_get_config: need out != NULL and 0 <= n <= 11");
+  HEIST_REQUIRE(out != nullptr && n >= 0 && n <= 12, "heist_get_config: need out != NULL and 0 <= n <= 12");
   const EnvParams& p = h->p;
-  const int32_t v[11] = {p.step_waves, p.ray_chunk,  p.step_occ,       p.vis_gap,   p.obs_store,  p.ray_mode,
-                         p.probe_mode, p.dispatch_order, p.split_obs, p.guard_cones, p.multi_waves};
+  const int32_t v[12] = {p.step_waves, p.ray_chunk,  p.step_occ,       p.vis_gap,   p.obs_store,  p.ray_mode,
+                         p.probe_mode, p.dispatch_order, p.split_obs, p.guard_cones, p.multi_waves, p.fan_on};
   for (int k = 0; k < n; ++k) out[k] = v[k];
   return 0;
 }

@@ -84,6 +84,22 @@ struct Emit {
 };
 static_assert(sizeof(Emit) == 56, "Emit layout");
 
+// The K-tick kernel's shared camera fan (fan_kernel, heist_env.hip): for tick k of a
+// launch, the fast-path fan of env 0's first camera as that tick casts it -- the emitter
+// (heading - fov / 2, fov, rays, range) and, computed once for the whole batch, its rays'
+// unique fp32 directions (one per dedup key) and its near-tie rays.  A direction group
+// whose emitter equals the tick's entry bit for bit takes its rays from the table instead
+// of computing them (an Architect batch's cameras share one fan, and their headings advance
+// in lockstep); any other group computes its own.  n_uniq < 0: no table for the tick.
+constexpr int kFanRays = 256;   // rays 0 .. num_rays with num_rays < kFanRays
+constexpr int kFanTicks = 1024;  // the K-tick launch's K limit
+struct FanTick {
+  double hmh, fov;
+  int num_rays, range, n_uniq, n_tie;
+  float uniq[2 * kFanRays];  // (dxs, dys) of the unique directions
+  uint16_t tie[kFanRays];    // ray indices of the near-tie rays (exact path)
+};
+
 struct EnvParams {
   int R, C, RC, max_steps;
   int sr, sc, vr, vc;
@@ -119,6 +135,8 @@ struct EnvParams {
   unsigned long long* stamps;          // optional [n_envs][waves][8]: step-kernel phase stamps (s_memtime), else null
   int obs_store;              // observation stores: 0 plain, 1 write-through (sc1), 2 nt, 3 sc1 nt (HEIST_OBS_STORE)
   int ray_mode;               // 0: fp32 fast path with exact fp64 re-cast of near-tie rays; 1: exact fp64 only
+  FanTick* fan;               // [kFanTicks] shared camera fan of the current K-tick launch (fan_kernel)
+  int fan_on;                 // 1 (default): the K-tick kernel uses the shared fan (HEIST_SHARED_FAN)
   int probe_mode;             // profiling only (HEIST_PROBE_MODE): 0 normal, 1 no rays, 2 angles+sin/cos only,
                               // 3 marches with a fixed direction (no sin/cos), 4 no observation write,
                               // 5 neither rays nor observation, 6 return at entry, 7 return after the

@@ -550,9 +550,24 @@ __device__ __forceinline__ int emitter_of_chunk(const EnvLds& L, int n_em, int k
 #define HEIST_PACK_FLUSH 1
 #endif
 
+// The shared fan's emitter for one tick (FanTick header), loaded by the K-tick kernel ahead of
+// the raycast so that the per-chunk test compares registers (a global load per chunk would put
+// its latency on every chunk of every group); n_uniq < 0: no table.
+struct FanHdr {
+  double hmh, fov;
+  int num_rays, range, n_uniq, n_tie;
+};
+__device__ __forceinline__ FanHdr fan_hdr(const FanTick* f) {
+  FanHdr h;
+  h.hmh = uni(f->hmh); h.fov = uni(f->fov);  // wave-uniform: scalar registers across the tick
+  h.num_rays = uni(f->num_rays); h.range = uni(f->range); h.n_uniq = uni(f->n_uniq); h.n_tie = uni(f->n_tie);
+  return h;
+}
+
 template <int NT, int U, int D, bool COUNT, bool DEDUP = false>
 __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int probe, const double* hd,
-                          const TieBuckets* tb = nullptr, float2* uq = nullptr) {
+                          const TieBuckets* tb = nullptr, float2* uq = nullptr, const FanTick* fan = nullptr,
+                          FanHdr fh = FanHdr{0.0, 0.0, 0, 0, -1, 0}) {
   static_assert(U == 2 || U == 4, "exact-path chunk");
   static_assert(kRing >= U, "the exact path's chunks stay inside the ring");
   constexpr int W = NT / 64;
@@ -574,8 +589,8 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
   // flush(cnt): the group's cnt unique directions uq[0 .. cnt) from each of its `members`
   // tiles, packed as (member, direction) pairs p = m * cnt + j over the lanes, 64 pairs per
   // march (a 2-camera group of <= 32 unique directions: one march instead of two)
-  auto flush = [&](int cnt) {
-    const Emit Eq = uni(L.em[uk]);
+  auto march_uniq = [&](int kk, int cnt, auto src) {  // src(j): unique direction j of group kk
+    const Emit Eq = uni(L.em[kk]);
     const int n_samp = Eq.kind == 0 ? 2 * Eq.range : Eq.range;
     const int n_pair = kPackFlush ? Eq.members * cnt : cnt;
     for (int p0 = 0; p0 < n_pair; p0 += 64) {
@@ -587,20 +602,20 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
             ++m;
           }
       if (p0 + lane >= n_pair) continue;
-      const float2 d = uq[j];
+      const float2 d = src(j);
       auto group = [&](auto ns, auto clamp) {
         constexpr int NS = decltype(ns)::value;
         constexpr bool CL = decltype(clamp)::value;
         if constexpr (kPackFlush) {
-          const int row = L.em[uk + m].row, col = L.em[uk + m].col;
+          const int row = L.em[kk + m].row, col = L.em[kk + m].col;
           const uint32_t own = base + (uint32_t)((row + kRing) * PC + (col + kRing));
           const float mx = __builtin_bit_cast(float, base + (uint32_t)(col + kRing));
           const float my = __builtin_bit_cast(float, (uint32_t)(row + kRing));
           march_fast<D, NS, CL, false, true>(PC, own, d.x, d.y, mx, my, n_samp);
         } else {  // one march per member, origin in SGPRs
           for (int mm = 0; mm < Eq.members; ++mm) {
-            const int row = mm == 0 ? Eq.row : uni(L.em[uk + mm].row);
-            const int col = mm == 0 ? Eq.col : uni(L.em[uk + mm].col);
+            const int row = mm == 0 ? Eq.row : uni(L.em[kk + mm].row);
+            const int col = mm == 0 ? Eq.col : uni(L.em[kk + mm].col);
             const uint32_t own = base + (uint32_t)((row + kRing) * PC + (col + kRing));
             const float mx = __builtin_bit_cast(float, base + (uint32_t)(col + kRing));
             const float my = __builtin_bit_cast(float, (uint32_t)(row + kRing));
@@ -618,6 +633,7 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
         group(std::integral_constant<int, 2 * kTieMaxRange>{}, std::true_type{});
     }
   };
+  auto flush = [&](int cnt) { march_uniq(uk, cnt, [&](int j) { return uq[j]; }); };
   // pass 1: fp32 fast path
   for (int c = wave; c < n_chunk; c += W) {
     k = emitter_of_chunk(L, n_em, k, c);
@@ -625,6 +641,26 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
     if (!fast_emitter(E, mode)) {
       exact_em = true;
       continue;
+    }
+    if constexpr (DEDUP) {
+      // the tick's shared fan (FanTick): a camera group casting exactly its emitter takes
+      // its unique directions and near-tie rays from the table, once, at its first chunk
+      if (fh.n_uniq >= 0 && E.kind == 0 && E.hmh == fh.hmh && E.fov == fh.fov && E.num_rays == fh.num_rays &&
+          E.range == fh.range) {
+        if (c == E.first) {
+          if (uqn > 0) {  // another group's queued directions
+            flush(uqn);
+            uqn = 0;
+          }
+          const int nt = fh.n_tie;
+          for (int b0 = 0; b0 < nt; b0 += 64)
+            if (b0 + lane < nt && qn + b0 + lane < 64) queue[qn + b0 + lane] = (k << 16) | (int)fan->tie[b0 + lane];
+          qn += nt;
+          const float* fu = fan->uniq;
+          march_uniq(k, fh.n_uniq, [&](int j) { return make_float2(fu[2 * j], fu[2 * j + 1]); });
+        }
+        continue;
+      }
     }
     const int i = (c - E.first) * 64 + lane;
     const bool active = i <= E.num_rays;  // rays 0 .. num_rays (security.py:68)
@@ -1415,6 +1451,74 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
 // K ticks per launch (heist_step_multi)
 // ---------------------------------------------------------------------------
 
+// The launch's shared camera fan (FanTick), block k = tick k: env 0's first camera after
+// k + 1 rotations (security.py:49-51, every tick of the launch acting), its emitter as
+// cam_emit forms it, and rays 0 .. num_rays through the same fast-path functions as
+// cast_rays (fast_dir, near_tie_key): the near-tie rays, and one ray per run of equal dedup
+// keys (a ray is kept when its key differs from the previous ray's, as cast_rays keeps it
+// when it differs from the previous lane's).  Runs on the launch's stream before the K-tick
+// kernel; a tick without a table (no camera in env 0, range > 6, too many rays, exact-only
+// mode) gets n_uniq = -1.
+__global__ __launch_bounds__(kFanRays) void fan_kernel(EnvParams p) {
+  FanTick* F = p.fan + blockIdx.x;
+  const int t = threadIdx.x;
+  Cam cm = p.cams[0];
+  const bool ok = p.max_cams > 0 && p.scal[0].n_cams > 0 && p.ray_mode == 0 && cm.range <= kTieMaxRange &&
+                  cm.num_rays >= 0 && cm.num_rays < kFanRays;
+  if (!ok) {
+    if (t == 0) F->n_uniq = -1;
+    return;
+  }
+  double h = cm.heading;
+  for (int j = 0; j <= (int)blockIdx.x; ++j) h = py_mod360(h + cm.speed * 1.0);
+  cm.heading = h;
+  const Emit E = cam_emit(cm);
+  const bool active = t <= E.num_rays;
+  float cf, sf, xr;
+  fast_dir(__builtin_fma((double)t, E.step, E.hmh), &cf, &sf, &xr);
+  uint32_t key = 0;
+  const bool tie = active && near_tie_key(cf, sf, xr, true, &kTieBuckets_, &key);
+  const uint32_t mine = (active && !tie) ? key : 0xFFFFFFFFu;
+  __shared__ uint32_t last[kFanRays / 64];
+  __shared__ int nf[kFanRays / 64], nt[kFanRays / 64];
+  if ((t & 63) == 63) last[t >> 6] = mine;
+  uint32_t prev = (uint32_t)__shfl_up((int)mine, 1, 64);
+  const unsigned long long bt = __ballot(tie);
+  __syncthreads();
+  if ((t & 63) == 0 && t > 0) prev = last[(t >> 6) - 1];
+  const bool fresh = active && !tie && (t == 0 || prev != mine);
+  const unsigned long long bf = __ballot(fresh);
+  if ((t & 63) == 0) {
+    nf[t >> 6] = __popcll(bf);
+    nt[t >> 6] = __popcll(bt);
+  }
+  __syncthreads();
+  int of = 0, ot = 0, tf = 0, tt = 0;
+  for (int w = 0; w < kFanRays / 64; ++w) {
+    if (w < (t >> 6)) {
+      of += nf[w];
+      ot += nt[w];
+    }
+    tf += nf[w];
+    tt += nt[w];
+  }
+  of += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bf >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bf, 0u));
+  ot += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bt >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bt, 0u));
+  if (fresh) {
+    F->uniq[2 * of] = below_one(cf) * 0.5f;  // camera sample stride: half tiles (cast_rays)
+    F->uniq[2 * of + 1] = -below_one(sf) * 0.5f;
+  }
+  if (tie) F->tie[ot] = (uint16_t)t;
+  if (t == 0) {
+    F->hmh = E.hmh;
+    F->fov = E.fov;
+    F->num_rays = E.num_rays;
+    F->range = E.range;
+    F->n_uniq = tf;
+    F->n_tie = tt;
+  }
+}
+
 // Observation lanes: the threads that store a tick's observation row -- waves 1.. when the
 // env has two or more waves (wave 0, which updates the emitters and loads the next cone
 // entries, then issues no observation stores: vmcnt counts loads and stores together, in
@@ -1741,9 +1845,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   int status = kAlreadyDone, done_now = 0;
   bool act_now = true;
   int curr = 0;
+  FanHdr fhdr{0.0, 0.0, 0, 0, -1, 0};  // this tick's shared fan (FanTick), -1: none
   while (k < K) {
     __syncthreads();  // the previous pass's readers of vis / em / meta / cones are done
     HEIST_MULTI_STAMP(8);  // 8: end of the previous tick -> through the top barrier
+    if (p.fan_on && PROBE == 0 && !reset_pass) fhdr = fan_hdr(p.fan + k);  // lands during phase A
     Emit E;
     E.kind = -1;
     if (!reset_pass) {
@@ -1835,7 +1941,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     HEIST_MULTI_STAMP(3);  // 3: waiting at the raycast barrier
     // 3. visibility (environment.py:257-258)
     if (live_guard && E.kind == 1) L.vis[L.at(E.row, E.col)] = 1;  // visibility.py:59
-    if (!(PROBE & 1)) cast_rays<NT, U, D, false, true>(smem, L, p.ray_mode, (PROBE & 4) ? 2 : 0, p.half_deg, tb, uq);
+    if (!(PROBE & 1))
+      cast_rays<NT, U, D, false, true>(smem, L, p.ray_mode, (PROBE & 4) ? 2 : 0, p.half_deg, tb, uq, p.fan + k, fhdr);
     if (SOLO && cached && !reset_pass) take_entry();  // loaded a tick ago; the raycast covered its latency
     if (!(PROBE & 1)) stamp_guard_cones<NT>(L, gvis, mc, mg, 0);
     HEIST_MULTI_STAMP(4);  // 4: raycast, cone stamps
@@ -2578,6 +2685,7 @@ hipError_t launch_step_multi(const EnvParams& p, const EnvParams* pg, int K, con
 #define HEIST_MULTI_CASE(W, U, O, D)                                                                        \
   if (p.multi_waves == W && p.ray_chunk == U && p.multi_occ == O && p.vis_gap == D && p.probe_mode == 0 && \
       !p.sample_counter && !p.redo_counter && (p.C & 3) == 0) {                                            \
+    if (p.fan_on) hipLaunchKernelGGL(fan_kernel, dim3(K), dim3(kFanRays), 0, st, p);                        \
     if (p.stamps)                                                                                            \
       hipLaunchKernelGGL((step_multi_kernel<W, U, O, D, true>), dim3(p.n_envs), dim3(64 * W), lds, st, p, K,  \
                          actions, obs, rew, rew64, done_out, status_out, auto_reset);                         \

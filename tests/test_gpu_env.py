@@ -688,3 +688,42 @@ def test_step_multi_any_grid_width(gpu_device, monkeypatch, waves, R, C):
     g = torch.Generator(device="cpu").manual_seed(70)
     acts = torch.randint(0, 5, (45, n), generator=g).to(gpu_device)
     _compare_multi_vs_single(a, b, acts, [20, 25])
+
+
+@pytest.mark.parametrize("waves", [1, 2])
+@pytest.mark.parametrize("auto_reset", [True, False], ids=["auto_reset", "no_reset"])
+def test_step_multi_shared_fan(gpu_device, monkeypatch, waves, auto_reset):
+    """Architect-checkpoint layouts (every camera of the batch shares one fan, so the K-tick
+    kernel takes its rays from the shared fan table, FanTick) with short episodes: timeouts,
+    detections and resets inside a launch, and without auto-reset finished envs stop
+    rotating and fall back to their own fan -- bit-identical to single ticks, and to the
+    same launches with the table off (HEIST_SHARED_FAN=0)."""
+    import os
+    from heist_amd.layouts import architect_checkpoint_layouts
+    ckpt = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "checkpoints",
+                        "architect_c2_fixed.pt")
+    n, budget = 512, 15
+    cfg = EnvironmentConfig(architect_budget=budget, max_steps=25)
+    envs = []
+    for fan in ("1", "0", "1"):
+        monkeypatch.setenv("HEIST_MULTI_WAVES", str(waves))
+        monkeypatch.setenv("HEIST_SHARED_FAN", fan)
+        env = HeistEnv(n, cfg, max_cams=5, max_guards=3, max_path=16, device=gpu_device)
+        monkeypatch.delenv("HEIST_MULTI_WAVES")
+        monkeypatch.delenv("HEIST_SHARED_FAN")
+        _, ok = architect_checkpoint_layouts(env, budget, seed=1234, ckpt=ckpt)
+        assert ok
+        env.reset()
+        envs.append(env)
+    a, c, b = envs
+    assert a.kernel_config()["fan_on"] == 1 and c.kernel_config()["fan_on"] == 0
+    g = torch.Generator(device="cpu").manual_seed(71)
+    acts = torch.randint(0, 5, (60, n), generator=g).to(gpu_device)
+    for k0, kk in ((0, 20), (20, 40)):
+        oa = a.step_multi(acts[k0:k0 + kk], auto_reset=auto_reset, reward64=True)
+        oc = c.step_multi(acts[k0:k0 + kk], auto_reset=auto_reset, reward64=True)
+        for x, y in zip(oa, oc):
+            assert torch.equal(x, y)
+        for k in range(kk):
+            o, r, d, s = b.step(acts[k0 + k], auto_reset=auto_reset)
+            assert torch.equal(oa[0][k], o) and torch.equal(oa[2][k], d) and torch.equal(oa[3][k], s), (k0 + k)

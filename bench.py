@@ -176,7 +176,11 @@ def measure_rollout(env, dev, steps=20, warmup=3, precision="bf16"):
         env.step(a)
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
+    tf = solver_backbone_flop(env.rows) * steps * env.n_envs / dt / 1e12  # rollout MFMA fraction
     return {"value": steps * env.n_envs / dt, "unit": "env-steps/s", "ms_per_step": dt / steps * 1e3,
+            "mfma_roofline": {"achieved": tf, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                              "frac": tf / MFMA_BF16_PEAK_TFLOPS,
+                              "note": "algorithmic conv-backbone flops of the policy forward per env-step"},
             "dtype": "bf16 MFMA policy (fp32 accumulate)" if precision == "bf16" else "fp32 policy (PyTorch-ROCm)",
             "note": ("heist_step + fused Solver select_action (backbone + head kernels)" if precision == "bf16" else
                      "heist_step + reference fp32 select_action (MIOpen convs, fused-gate LSTM)") +

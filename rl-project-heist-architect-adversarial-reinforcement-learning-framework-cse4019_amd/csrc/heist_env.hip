@@ -1675,11 +1675,13 @@ template <int NT>
 __device__ __forceinline__ void clear_planes(const EnvParams& p, const EnvLds& L, uint8_t* gvis, bool rays) {
   constexpr int PW = ObsLanes<NT>::PW;
   const int t = (int)threadIdx.x - ObsLanes<NT>::LB;
-  uint32_t* v4 = reinterpret_cast<uint32_t*>(L.vis);
-  uint32_t* g4 = reinterpret_cast<uint32_t*>(gvis);
-  for (int i = t; i >= 0 && i < (padded_bytes(p.R, p.C) + 3) / 4; i += PW) {
-    if (rays) v4[i] = 0u;
-    g4[i] = 0u;
+  // 16-byte stores: both planes are 16-byte aligned and D >= the padded size rounded to 16
+  uint4* v16 = reinterpret_cast<uint4*>(L.vis);
+  uint4* g16 = reinterpret_cast<uint4*>(gvis);
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = t; i >= 0 && i < (padded_bytes(p.R, p.C) + 15) / 16; i += PW) {
+    if (rays) v16[i] = z;
+    g16[i] = z;
   }
 }
 

@@ -31,6 +31,11 @@
 
 #include <utility>
 
+// LDS reads in flight in conv3's A-fragment ring (build-time A/B knob)
+#ifndef HEIST_CONV3_PRE
+#define HEIST_CONV3_PRE 7
+#endif
+
 namespace heist {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -391,7 +396,7 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
     // last slot) have all-zero pool membership and add nothing.
     f32x16 Y = {};
     {
-      constexpr int NT2 = G::NT2, NQ = NT2 * kW3Steps, kPre = 7;
+      constexpr int NT2 = G::NT2, NQ = NT2 * kW3Steps, kPre = HEIST_CONV3_PRE;
       const unsigned char* base[NT2];
 #pragma unroll
       for (int i = 0; i < NT2; ++i)

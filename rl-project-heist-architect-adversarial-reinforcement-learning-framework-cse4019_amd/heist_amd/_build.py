@@ -28,7 +28,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # step_multi_kernel<2,4,8,1024> with it, 46 (reloaded once per tick) without; the
 # single-tick step kernel drops from 64 VGPRs + 3 spilled to 53 with none.
 # HEIST_ENV_FLAGS replaces this list (A/B builds).
-FILE_FLAGS = {"heist_env.hip": os.environ.get("HEIST_ENV_FLAGS", "-fno-slp-vectorize -mllvm -disable-machine-licm").split()}
+FILE_FLAGS = {"heist_env.hip": os.environ.get("HEIST_ENV_FLAGS", "-fno-slp-vectorize -mllvm -disable-machine-licm").split(),
+              "heist_policy.hip": os.environ.get("HEIST_POLICY_FLAGS", "").split()}  # A/B builds of the policy kernels
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
           "--offload-arch=" + ARCH, "-I", INCLUDE, "-I", CSRC]
 

@@ -12,6 +12,7 @@ layout's log-prob.  update() is the reference's formula over whatever the buffer
 inside a process group it is global: the buffer statistics are all-reduced (one float64
 vector), every rank forms the same value target and takes the same step.
 """
+import os
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -235,7 +236,10 @@ class ArchitectAgent:  # agents/architect.py:16-170
         params = list(self.network.parameters())
         self.optimizer.zero_grad(set_to_none=True)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # HEIST_ARCH_MIOPEN=0 (A/B): the captured batch-1 convolutions on PyTorch's native
+        # kernels instead of MIOpen's
+        miopen = os.environ.get("HEIST_ARCH_MIOPEN", "1") != "0"
+        with torch.backends.cudnn.flags(enabled=miopen), torch.cuda.graph(g):
             r = self._g_r.index_select(0, self._g_i).squeeze()
             value_loss = F.mse_loss(self.network.value(self._g_s).squeeze(), r)
             self._g_vl.index_copy_(0, self._g_i, value_loss.detach().reshape(1))

@@ -67,6 +67,10 @@ for s in ${STEPS:-pytest smoke bench prof}; do
            done; done
            for f in 1 0; do HEIST_SHARED_FAN=$f step bench_fan${f}_syn 300 python bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary --layouts synthetic; done ;;
     ptrain) step probe_train 600 python tools/probe_train.py ;;
+    aseq) step probe_arch_seq 300 python tools/probe_arch_seq.py ;;
+    preab) L=$PWD/rl-project-heist-architect-adversarial-reinforcement-learning-framework-cse4019_amd/heist_amd
+           for i in 1 2; do step probe_policy_pre7_$i 300 python tools/probe_policy.py
+             for pre in 10 13; do HEIST_LIB=$L/libheist_hip_pre$pre.so step probe_policy_pre${pre}_$i 300 python tools/probe_policy.py; done; done ;;
     lbtest) step pytest_lb 600 python -u -m pytest tests/test_gpu_trainer.py -k "layout_batch or interactive or c3" -x -v --timeout 500 --timeout-method thread ;;
     mmodesw1) export HEIST_MULTI_WAVES=1; step multi_modes 300 python tools/probe_multi_modes.py
             step pmc_modes_m1 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU -d "$OUT/pmm1" -o m --output-format csv -- python3 tools/probe_multi_modes.py

@@ -556,18 +556,21 @@ __device__ __forceinline__ int emitter_of_chunk(const EnvLds& L, int n_em, int k
 struct FanHdr {
   double hmh, fov;
   int num_rays, range, n_uniq, n_tie;
+  float2 dir;  // this lane's unique direction uniq[lane] (loaded with the header; lanes >= n_uniq: unused)
 };
 __device__ __forceinline__ FanHdr fan_hdr(const FanTick* f) {
   FanHdr h;
   h.hmh = uni(f->hmh); h.fov = uni(f->fov);  // wave-uniform: scalar registers across the tick
   h.num_rays = uni(f->num_rays); h.range = uni(f->range); h.n_uniq = uni(f->n_uniq); h.n_tie = uni(f->n_tie);
+  const int lane = threadIdx.x & 63;  // < kFanRays: always inside the table
+  h.dir = make_float2(f->uniq[2 * lane], f->uniq[2 * lane + 1]);
   return h;
 }
 
 template <int NT, int U, int D, bool COUNT, bool DEDUP = false>
 __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int probe, const double* hd,
                           const TieBuckets* tb = nullptr, float2* uq = nullptr, const FanTick* fan = nullptr,
-                          FanHdr fh = FanHdr{0.0, 0.0, 0, 0, -1, 0}) {
+                          FanHdr fh = FanHdr{0.0, 0.0, 0, 0, -1, 0, {0.0f, 0.0f}}) {
   static_assert(U == 2 || U == 4, "exact-path chunk");
   static_assert(kRing >= U, "the exact path's chunks stay inside the ring");
   constexpr int W = NT / 64;
@@ -656,8 +659,14 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
           for (int b0 = 0; b0 < nt; b0 += 64)
             if (b0 + lane < nt && qn + b0 + lane < 64) queue[qn + b0 + lane] = (k << 16) | (int)fan->tie[b0 + lane];
           qn += nt;
+          // directions 0 .. 63 from the registers loaded with the header (a lane permute),
+          // the rest of a wide fan from the table
           const float* fu = fan->uniq;
-          march_uniq(k, fh.n_uniq, [&](int j) { return make_float2(fu[2 * j], fu[2 * j + 1]); });
+          march_uniq(k, fh.n_uniq, [&](int j) {
+            if (j < 64)
+              return make_float2(__shfl(fh.dir.x, j, 64), __shfl(fh.dir.y, j, 64));
+            return make_float2(fu[2 * j], fu[2 * j + 1]);
+          });
         }
         continue;
       }
@@ -1847,7 +1856,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   int status = kAlreadyDone, done_now = 0;
   bool act_now = true;
   int curr = 0;
-  FanHdr fhdr{0.0, 0.0, 0, 0, -1, 0};  // this tick's shared fan (FanTick), -1: none
+  FanHdr fhdr{0.0, 0.0, 0, 0, -1, 0, {0.0f, 0.0f}};  // this tick's shared fan (FanTick), -1: none
   while (k < K) {
     __syncthreads();  // the previous pass's readers of vis / em / meta / cones are done
     HEIST_MULTI_STAMP(8);  // 8: end of the previous tick -> through the top barrier

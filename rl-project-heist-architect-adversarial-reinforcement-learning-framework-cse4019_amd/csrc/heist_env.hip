@@ -604,8 +604,11 @@ __device__ void cast_rays(unsigned char* smem, const EnvLds& L, int mode, int pr
             j -= cnt;
             ++m;
           }
+      // src may permute across lanes (the shared fan's directions): every lane calls it, the
+      // lanes past n_pair with a valid index, before they drop out (a lane permute reads
+      // nothing from an inactive lane)
+      const float2 d = src(p0 + lane < n_pair ? j : 0);
       if (p0 + lane >= n_pair) continue;
-      const float2 d = src(j);
       auto group = [&](auto ns, auto clamp) {
         constexpr int NS = decltype(ns)::value;
         constexpr bool CL = decltype(clamp)::value;

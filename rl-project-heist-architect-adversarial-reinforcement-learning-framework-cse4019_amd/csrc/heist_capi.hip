@@ -73,6 +73,7 @@ struct heist_env {
   void* allocs[13];
   int n_allocs;
   EnvParams* dev_p;  // device copy of p for the K-tick kernel (read through a pointer, not as kernel arguments)
+  int fan_pos;       // next entry of the shared fan table (FanTick) for a K-tick launch; -1: refill first
   EnvParams dev_p_host;  // what dev_p holds
   bool dev_p_valid;
 };
@@ -284,6 +285,9 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   p.cones = (uint16_t*)h->allocs[10];
   h->dev_p = (EnvParams*)h->allocs[11];
   p.fan = (heist::FanTick*)h->allocs[12];
+  h->fan_pos = -1;
+  p.fan_base = 0;
+  p.fan_fill = 0;
   p.fan_on = 1;
   if (const char* f = getenv("HEIST_SHARED_FAN")) p.fan_on = atoi(f) ? 1 : 0;
   h->dev_p_valid = false;
@@ -295,6 +299,8 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   int rc = check_hip(hipMemcpy(h->allocs[5], htab.data(), sizes[5], hipMemcpyHostToDevice), "heist_create: upload");
   if (!rc) rc = check_hip(hipMemcpy(h->allocs[6], planes.data(), sizes[6], hipMemcpyHostToDevice), "heist_create: upload");
   if (!rc) rc = check_hip(hipMemset(h->allocs[2], 0, sizes[2]), "heist_create: memset");
+  // fan table: all 0xFF = NaN emitters and n_uniq = -1, an entry no group can match
+  if (!rc) rc = check_hip(hipMemset(h->allocs[12], 0xFF, sizes[12]), "heist_create: memset");
   if (!rc) rc = check_hip(hipMemset(h->allocs[3], 0, sizes[3]), "heist_create: memset");
   if (!rc) rc = check_hip(hipMemset(h->allocs[4], 0, sizes[4]), "heist_create: memset");
   if (!rc) rc = check_hip(hipMemcpy((double*)h->allocs[8] + 2 * heist::kHalfDegN, hrad.data(),
@@ -331,6 +337,7 @@ int heist_set_layout(heist_t h, int max_walls, const int32_t* wall_rc, const int
   HEIST_REQUIRE(max_walls == 0 || wall_rc, "heist_set_layout: wall_rc is null");
   HEIST_REQUIRE(h->p.max_cams == 0 || cam_params, "heist_set_layout: cam_params is null");
   HEIST_REQUIRE(h->p.max_guards == 0 || (guard_paths && guard_meta && guard_fov), "heist_set_layout: guard arrays null");
+  h->fan_pos = -1;  // new cameras: the shared fan table is refilled by the next K-tick launch
   if (int rc = check_hip(heist::launch_set_layout(h->p, max_walls, wall_rc, n_walls, cam_params, n_cams, guard_paths,
                                                    guard_meta, guard_fov, n_guards, budget, mask, valid_out,
                                                    (hipStream_t)stream),
@@ -344,6 +351,7 @@ int heist_set_layout(heist_t h, int max_walls, const int32_t* wall_rc, const int
 int heist_reset(heist_t h, const uint8_t* mask, float* obs_out, heist_stream_t stream) {
   if (int rc = check_handle(h)) return rc;
   HEIST_REQUIRE(obs_out != nullptr, "heist_reset: obs_out is null");
+  h->fan_pos = -1;
   return check_hip(heist::launch_reset(h->p, mask, obs_out, (hipStream_t)stream), "heist_reset");
 }
 
@@ -351,6 +359,7 @@ int heist_step(heist_t h, const int64_t* actions, float* obs_out, float* reward_
                uint8_t* done_out, int8_t* status_out, int auto_reset, heist_stream_t stream) {
   if (int rc = check_handle(h)) return rc;
   HEIST_REQUIRE(actions && obs_out && reward_out && done_out && status_out, "heist_step: null output/input");
+  h->fan_pos = -1;  // headings advanced outside the K-tick launches' accounting
   return check_hip(heist::launch_step(h->p, actions, obs_out, reward_out, reward64_out, done_out, status_out,
                                       auto_reset, (hipStream_t)stream),
                    "heist_step");
@@ -371,7 +380,24 @@ int heist_step_multi(heist_t h, int K, const int64_t* actions, float* obs_out, f
     if (int rc = check_hip(hipStreamSynchronize(st), "heist_step_multi: params upload")) return rc;
     h->dev_p_valid = true;
   }
-  return check_hip(heist::launch_step_multi(h->p, h->dev_p, K, actions, obs_out, reward_out, reward64_out, done_out,
+  // the shared fan table (FanTick): refilled when stale or used up, else read at the launch's
+  // offset -- only when the K-tick kernel runs (otherwise K single ticks advance the headings)
+  EnvParams q = h->p;
+  const bool kt = heist::multi_variant_exists(q.multi_waves, q.ray_chunk, q.multi_occ, q.vis_gap) && (q.C & 3) == 0 &&
+                  q.probe_mode == 0 && !q.sample_counter && !q.redo_counter;
+  q.fan_fill = 0;
+  q.fan_base = 0;
+  if (kt && q.fan_on) {
+    if (h->fan_pos < 0 || h->fan_pos + K > heist::kFanTicks) {
+      q.fan_fill = 1;
+      h->fan_pos = 0;
+    }
+    q.fan_base = h->fan_pos;
+    h->fan_pos += K;
+  } else {
+    h->fan_pos = -1;
+  }
+  return check_hip(heist::launch_step_multi(q, h->dev_p, K, actions, obs_out, reward_out, reward64_out, done_out,
                                             status_out, auto_reset, st),
                    "heist_step_multi");
 }
@@ -418,6 +444,7 @@ int heist_get_config(heist_t h, int32_t* out, int n) {
 
 int heist_set_ray_mode(heist_t h, int ray_mode) {
   if (int rc = check_handle(h)) return rc;
+  h->fan_pos = -1;
   HEIST_REQUIRE(ray_mode == 0 || ray_mode == 1, "heist_set_ray_mode: ray_mode must be 0 or 1");
   h->p.ray_mode = ray_mode;
   return 0;
@@ -425,6 +452,7 @@ int heist_set_ray_mode(heist_t h, int ray_mode) {
 
 int heist_set_guard_cones(heist_t h, int on) {
   if (int rc = check_handle(h)) return rc;
+  h->fan_pos = -1;
   HEIST_REQUIRE(on == 0 || on == 1, "heist_set_guard_cones: on must be 0 or 1");
   h->p.guard_cones = on;
   return 0;

@@ -91,6 +91,10 @@ static_assert(sizeof(Emit) == 56, "Emit layout");
 // whose emitter equals the tick's entry bit for bit takes its rays from the table instead
 // of computing them (an Architect batch's cameras share one fan, and their headings advance
 // in lockstep); any other group computes its own.  n_uniq < 0: no table for the tick.
+// The table covers kFanTicks ticks from the launch that fills it and serves the following
+// launches at their offset (fan_base) until it runs out or the handle's cameras change
+// other than by K-tick launches (set_layout, reset, single ticks); an entry that no longer
+// matches a group's emitter is simply not used, so staleness costs time, never results.
 constexpr int kFanRays = 256;   // rays 0 .. num_rays with num_rays < kFanRays
 constexpr int kFanTicks = 1024;  // the K-tick launch's K limit
 struct FanTick {
@@ -137,6 +141,8 @@ struct EnvParams {
   int ray_mode;               // 0: fp32 fast path with exact fp64 re-cast of near-tie rays; 1: exact fp64 only
   FanTick* fan;               // [kFanTicks] shared camera fan of the current K-tick launch (fan_kernel)
   int fan_on;                 // 1 (default): the K-tick kernel uses the shared fan (HEIST_SHARED_FAN)
+  int fan_base;               // table entry of the launch's tick 0 (heist_step_multi)
+  int fan_fill;               // 1: the launch first refills the table from the cameras' current headings
   int probe_mode;             // profiling only (HEIST_PROBE_MODE): 0 normal, 1 no rays, 2 angles+sin/cos only,
                               // 3 marches with a fixed direction (no sin/cos), 4 no observation write,
                               // 5 neither rays nor observation, 6 return at entry, 7 return after the

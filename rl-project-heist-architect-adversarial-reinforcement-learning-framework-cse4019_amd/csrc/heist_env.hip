@@ -1463,14 +1463,16 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
 // K ticks per launch (heist_step_multi)
 // ---------------------------------------------------------------------------
 
-// The launch's shared camera fan (FanTick), block k = tick k: env 0's first camera after
-// k + 1 rotations (security.py:49-51, every tick of the launch acting), its emitter as
+// The shared camera fan table (FanTick), block k = table entry k: env 0's first camera after
+// k + 1 rotations from its heading when the filling launch starts (security.py:49-51, every
+// tick acting; heist_step_multi fills kFanTicks entries and later launches read them at
+// their offset fan_base), its emitter as
 // cam_emit forms it, and rays 0 .. num_rays through the same fast-path functions as
 // cast_rays (fast_dir, near_tie_key): the near-tie rays, and one ray per run of equal dedup
 // keys (a ray is kept when its key differs from the previous ray's, as cast_rays keeps it
 // when it differs from the previous lane's).  Runs on the launch's stream before the K-tick
-// kernel; a tick without a table (no camera in env 0, range > 6, too many rays, exact-only
-// mode) gets n_uniq = -1.
+// kernel of a filling launch; a tick without a table (no camera in env 0, range > 6, too
+// many rays, exact-only mode) gets n_uniq = -1.
 __global__ __launch_bounds__(kFanRays) void fan_kernel(EnvParams p) {
   FanTick* F = p.fan + blockIdx.x;
   const int t = threadIdx.x;
@@ -1863,7 +1865,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
   while (k < K) {
     __syncthreads();  // the previous pass's readers of vis / em / meta / cones are done
     HEIST_MULTI_STAMP(8);  // 8: end of the previous tick -> through the top barrier
-    if (p.fan_on && PROBE == 0 && !reset_pass) fhdr = fan_hdr(p.fan + k);  // lands during phase A
+    if (p.fan_on && PROBE == 0 && !reset_pass) fhdr = fan_hdr(p.fan + p.fan_base + k);  // lands during phase A
     Emit E;
     E.kind = -1;
     if (!reset_pass) {
@@ -1956,7 +1958,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     // 3. visibility (environment.py:257-258)
     if (live_guard && E.kind == 1) L.vis[L.at(E.row, E.col)] = 1;  // visibility.py:59
     if (!(PROBE & 1))
-      cast_rays<NT, U, D, false, true>(smem, L, p.ray_mode, (PROBE & 4) ? 2 : 0, p.half_deg, tb, uq, p.fan + k, fhdr);
+      cast_rays<NT, U, D, false, true>(smem, L, p.ray_mode, (PROBE & 4) ? 2 : 0, p.half_deg, tb, uq,
+                                       p.fan + p.fan_base + k, fhdr);
     if (SOLO && cached && !reset_pass) take_entry();  // loaded a tick ago; the raycast covered its latency
     if (!(PROBE & 1)) stamp_guard_cones<NT>(L, gvis, mc, mg, 0);
     HEIST_MULTI_STAMP(4);  // 4: raycast, cone stamps
@@ -2699,7 +2702,7 @@ hipError_t launch_step_multi(const EnvParams& p, const EnvParams* pg, int K, con
 #define HEIST_MULTI_CASE(W, U, O, D)                                                                        \
   if (p.multi_waves == W && p.ray_chunk == U && p.multi_occ == O && p.vis_gap == D && p.probe_mode == 0 && \
       !p.sample_counter && !p.redo_counter && (p.C & 3) == 0) {                                            \
-    if (p.fan_on) hipLaunchKernelGGL(fan_kernel, dim3(K), dim3(kFanRays), 0, st, p);                        \
+    if (p.fan_on && p.fan_fill) hipLaunchKernelGGL(fan_kernel, dim3(kFanTicks), dim3(kFanRays), 0, st, p);   \
     if (p.stamps)                                                                                            \
       hipLaunchKernelGGL((step_multi_kernel<W, U, O, D, true>), dim3(p.n_envs), dim3(64 * W), lds, st, p, K,  \
                          actions, obs, rew, rew64, done_out, status_out, auto_reset);                         \

@@ -1,9 +1,12 @@
 """Headline benchmark: Solver env-steps/sec at 20x20, 4096 envs/GPU (BASELINE.json metric).
 
-One "step" = one heist_step launch over all envs of the rank: move, camera/guard
-update, raycast visibility, reward/termination, in-kernel auto-reset, and the
-[N,3,20,20] float32 observation write.  Inputs (layouts, per-step actions) are
-resident in HBM before the timed region.  The headline layouts are BASELINE config 2's:
+One "step" = one env tick over all envs of the rank: move, camera/guard update, raycast
+visibility, reward/termination, in-kernel auto-reset, and the [N,3,20,20] float32
+observation write, reward, done and status of that tick to HBM.  The timed ticks run in
+heist_step_multi launches of K = --ticks-per-launch ticks each (default 20; named in
+config.workload), K = 1 being one heist_step launch per tick (also reported as the
+secondary env_only_single_tick).  Inputs (layouts, per-tick actions) are resident in HBM
+before the timed region, and every launch's arguments are resolved before it.  The headline layouts are BASELINE config 2's:
 sampled at temperature 1.0 and budget 15 from the fixed Architect checkpoint
 (checkpoints/architect_c2_fixed.pt, tools/mint_architect_checkpoint.py), resampled until
 BFS-valid; the round-1 synthetic mix (SURVEY 8d generator (ii)) is a secondary line.

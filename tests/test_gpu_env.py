@@ -727,3 +727,35 @@ def test_step_multi_shared_fan(gpu_device, monkeypatch, waves, auto_reset):
         for k in range(kk):
             o, r, d, s = b.step(acts[k0 + k], auto_reset=auto_reset)
             assert torch.equal(oa[0][k], o) and torch.equal(oa[2][k], d) and torch.equal(oa[3][k], s), (k0 + k)
+
+
+def test_step_multi_shared_fan_across_layout_changes(gpu_device):
+    """The shared fan table across heist_set_layout / single ticks between K-tick launches:
+    new Architect cameras (a second checkpoint draw) and headings advanced by single ticks
+    make the table stale; results stay equal to single ticks throughout."""
+    import os
+    from heist_amd.layouts import architect_checkpoint_layouts
+    ckpt = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "checkpoints",
+                        "architect_c2_fixed.pt")
+    n, budget = 512, 15
+    cfg = EnvironmentConfig(architect_budget=budget, max_steps=30)
+    a, b = (HeistEnv(n, cfg, max_cams=5, max_guards=3, max_path=16, device=gpu_device) for _ in range(2))
+    g = torch.Generator(device="cpu").manual_seed(72)
+    acts = torch.randint(0, 5, (90, n), generator=g).to(gpu_device)
+    t = 0
+    for seed, kk, single in ((1234, 25, 3), (99, 30, 2), (99, 20, 0)):
+        if seed != 99 or kk == 30:
+            for env in (a, b):
+                _, ok = architect_checkpoint_layouts(env, budget, seed=seed, ckpt=ckpt)
+                assert ok
+                env.reset()
+        oa = a.step_multi(acts[t:t + kk])
+        for k in range(kk):
+            o, r, d, s = b.step(acts[t + k])
+            assert torch.equal(oa[0][k], o) and torch.equal(oa[2][k], d) and torch.equal(oa[3][k], s), (t + k)
+        t += kk
+        for k in range(single):  # single ticks on both: headings move outside the launches
+            oa1 = a.step(acts[t])
+            ob1 = b.step(acts[t])
+            assert torch.equal(oa1[0], ob1[0])
+            t += 1

@@ -114,6 +114,57 @@ def architect_layouts(env, budget, seed, ckpt=None):
     return architect_checkpoint_layouts(env, budget, seed, path)
 
 
+def shared_fan_fraction(cam_params, n_cams):
+    """Share of the envs with cameras whose cameras all cast the shared fan (heist_env.hip
+    fan_kernel: the K-tick kernel takes a camera direction group's rays from the table when
+    its emitter equals the table's, i.e. every camera has the (fov, heading, speed, range) of
+    the first env's first camera, range <= 6).  Architect batches share one camera parameter
+    set per forward (reference networks.py:283-322); the synthetic mix draws its own per
+    camera.  cam_params [N, max_cams, 6] (row, col, fov, heading, speed, range), n_cams [N]."""
+    cp, nc = np.asarray(cam_params, np.float64), np.asarray(n_cams)
+    has = nc > 0
+    if not has.any():
+        return 0.0
+    e0 = int(np.nonzero(has)[0][0])
+    ref = cp[e0, 0, 2:6]
+    if ref[3] > 6:
+        return 0.0
+    served = [bool(np.all(cp[e, :nc[e], 2:6] == ref)) for e in np.nonzero(has)[0]]
+    return float(np.mean(served))
+
+
+def synthetic_fan_fraction(layouts, env, budget):
+    """shared_fan_fraction of layouts in the reference's list format."""
+    from heist_amd.vec_env import LayoutBatch
+    lb = LayoutBatch.from_lists(layouts, budget, env.max_cams, env.max_guards, env.max_path, "cpu", env.rows, env.cols)
+    return shared_fan_fraction(lb.cam_params.numpy(), lb.n_cams.numpy())
+
+
+def measure_fan_fill(env, actions, K, bufs, reps=5):
+    """The shared fan table's fill (fan_kernel: kFanTicks = 1,024 entries, run on the launch's
+    stream before a K-tick launch that finds the table stale) priced by HIP events: a K-tick
+    launch after the table was marked stale minus the same launch reading the table.  The
+    timed ticks read a table an earlier launch filled; amortised over the 1,024 ticks one fill
+    serves, its cost per tick is fill / 1,024."""
+    stream = torch.cuda.current_stream(env.device)
+    acts = actions[:K]
+
+    def one(stale):
+        if stale:
+            env.set_ray_mode(env.kernel_config()["ray_mode"])  # marks the table stale (heist_set_ray_mode)
+        launch = env.step_multi_launcher(K, acts, *bufs)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        launch()
+        b.record(stream)
+        torch.cuda.synchronize(env.device)
+        return a.elapsed_time(b)
+    one(False)
+    fill = [one(True) for _ in range(reps)]
+    plain = [one(False) for _ in range(reps)]
+    return max(0.0, float(np.median(fill) - np.median(plain)))
+
+
 def time_env(env, actions, warmup, steps, K, world):
     """Time `steps` env ticks over all envs after `warmup` untimed ones: K = 1 one heist_step
     launch per tick, K > 1 heist_step_multi launches of K ticks (the last one shorter), every
@@ -139,6 +190,8 @@ def time_env(env, actions, warmup, steps, K, world):
                 launch()
             return len(ls)
     else:
+        bufs = None
+
         def prepare(k0, n):
             return None
 
@@ -164,10 +217,15 @@ def time_env(env, actions, warmup, steps, K, world):
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / steps
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    per_rank = [(elapsed, kern_ms)]
+    if world > 1:  # every rank's wall time and kernel time per tick; the line's time is the max
+        t = torch.zeros((world, 2), dtype=torch.float64, device=dev)
+        t[dist.get_rank()] = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
+        dist.all_reduce(t)
+        per_rank = [tuple(r) for r in t.tolist()]
+        elapsed = max(r[0] for r in per_rank)
+    time_env.last_bufs = bufs if K > 1 else None
+    time_env.per_rank = per_rank
     return elapsed, kern_ms, issue_s, launches
 
 
@@ -207,9 +265,10 @@ def measure_env_config(dev, R, n, budget, steps=100, warmup=10, K=1, **kw):
     env = HeistEnv(n, cfg, max_cams=max(1, budget // 3), max_guards=max(1, budget // 5), max_path=16, device=dev,
                    auto_reset=True)
     if kw.pop("architect", False):
-        architect_layouts(env, budget, seed=99)
+        lb, _ = architect_layouts(env, budget, seed=99)
+        fan = shared_fan_fraction(lb.cam_params.cpu().numpy(), lb.n_cams.cpu().numpy())
     else:
-        valid_synthetic_layouts(env, budget, seed=99, **kw)
+        fan = synthetic_fan_fraction(valid_synthetic_layouts(env, budget, seed=99, **kw), env, budget)
     env.reset()
     acts = torch.randint(0, 5, (warmup + steps, n), device=dev, dtype=torch.int64)
     K = max(1, min(K, steps))
@@ -221,6 +280,7 @@ def measure_env_config(dev, R, n, budget, steps=100, warmup=10, K=1, **kw):
     env.close()
     return {"value": n / (ms * 1e-3), "unit": "env-steps/s", "kernel_ms": ms, "envs": n, "grid": "%dx%d" % (R, R),
             "budget": budget, "mean_cameras": ncam, "mean_guards": ngu, "ticks_per_launch": K,
+            "shared_fan_frac": fan,
             "kernel": "heist::step_multi_kernel" if K > 1 else "heist::step_kernel",
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_env_step": b}}
@@ -316,6 +376,31 @@ def measure_train(cfg, dev, n_envs, rollout_len=32, minibatch=16384, update_prec
                          else "")}
 
 
+def measure_allreduce_grads(dev, iters=20, warmup=3):
+    """Mean microseconds of dist_utils.allreduce_grads (the training path's ONE exchange per
+    optimizer step: a flat all-reduce of the Solver's 550,150 gradient floats plus its weight,
+    reference agents/solver.py:191-199) on this process group, max over ranks."""
+    from heist_amd import dist_utils
+    from heist_amd.networks import SolverNetwork
+    net = SolverNetwork(20, 20).to(dev)
+    for p in net.parameters():
+        p.grad = torch.randn_like(p)
+    params = list(net.parameters())
+    dist = torch.distributed
+    for _ in range(warmup):
+        dist_utils.allreduce_grads(params, weight=1.0)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist_utils.allreduce_grads(params, weight=1.0)
+    torch.cuda.synchronize(dev)
+    us = (time.perf_counter() - t0) / iters * 1e6
+    t = torch.tensor([us], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def _spawned_rank(rank, world, port, argv):
     """Body of a rank started by `bench.py --gpus N` (torch.multiprocessing spawn)."""
     os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
@@ -400,6 +485,18 @@ def main():
     actions = torch.randint(0, 5, (args.warmup + args.steps, N), device=dev, generator=gen, dtype=torch.int64)
     K = max(1, min(args.ticks_per_launch, args.steps))
     elapsed, kern_ms, issue_s, launches = time_env(env, actions, args.warmup, args.steps, K, world)
+    per_rank = time_env.per_rank
+    fan_fill_ms = 0.0
+    if K > 1 and kcfg["fan_on"]:  # the table fill the timed launches did not pay (read from an earlier fill)
+        fan_fill_ms = measure_fan_fill(env, actions, K, time_env.last_bufs)
+    # the rollout's form (the policy needs each observation before the next action): one
+    # heist_step launch per tick, timed the same way at every N (collective at N > 1)
+    e1, k1, i1, _ = time_env(env, actions, args.warmup, args.steps, 1, world) if K > 1 else (elapsed, kern_ms,
+                                                                                               issue_s, launches)
+    per_rank_1 = time_env.per_rank
+    allreduce_us = None
+    if world > 1:  # the training path's one exchange step: a flat Solver-gradient all-reduce per optimizer step
+        allreduce_us = measure_allreduce_grads(dev)
 
     # ALU work figure: ray samples evaluated per env-step, counted by the
     # kernel on extra steps after the timed region
@@ -422,6 +519,12 @@ def main():
     achieved = b_step * N / (kern_ms * 1e-3) / 1e9  # GB/s: algorithmic bytes per tick / mean tick duration
     total_steps = args.steps * N * world
     value = total_steps / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    fan_ms_tick = fan_fill_ms / 1024.0  # one fill serves kFanTicks = 1,024 ticks
+    achieved_fan = b_step * N / ((kern_ms + fan_ms_tick) * 1e-3) / 1e9
+    achieved_wall = b_step * N / (ms_per_step * 1e-3) / 1e9
+    fan_frac = shared_fan_fraction(lb.cam_params.cpu().numpy(), lb.n_cams.cpu().numpy()) if layouts is None else \
+        synthetic_fan_fraction(layouts, env, args.budget)
 
     if rank == 0:
         traffic, traffic_src = None, None
@@ -435,9 +538,10 @@ def main():
                               "MI355X_MICROARCH.md, per tick: profiles/%s" % (tj.get("profile", "?"), os.path.basename(tf))
         line = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": "env-only %s, 20x20 grid, %d envs/GPU, %s budget-%d layouts "
+            "config": {"workload": "env-only action replay (the K ticks' actions known up front) %s, 20x20 grid, "
+                                   "%d envs/GPU, %s budget-%d layouts "
                                    "(mean %.2f cameras, %.2f guards/env accepted), uniform random actions pre-generated "
                                    "in HBM, auto-reset, every tick's [N,3,20,20] f32 observation, reward, done and "
                                    "status written to HBM"
@@ -450,31 +554,46 @@ def main():
                        "parallelism": "env-sharded x%d" % world, "kernel_config": kcfg, "env_knobs": knobs,
                        "backend": args.backend if world > 1 else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "frac_wall": achieved_wall / HBM_PEAK_GBS,
+                         "frac_with_fan_fill": achieved_fan / HBM_PEAK_GBS,
+                         "fan_fill_ms_per_fill": fan_fill_ms, "fan_fill_ms_per_tick_amortised": fan_ms_tick,
+                         "shared_fan_frac": fan_frac,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "heist::step_multi_kernel" if K > 1 else "heist::step_kernel",
                          "kernel_ms": kern_ms, "kernel_ms_per_launch": kern_ms * K, "launches": launches,
                          "algorithmic_bytes_per_env_step": b_step,
                          "ray_samples_per_env_step": samples_per_step,
                          "exact_path_rays_per_env_step": exact_rays_per_step,
                          "host_issue_us_per_step": issue_s / args.steps * 1e6,
-                         "note": "achieved = algorithmic bytes per env-step (SURVEY 8d) x envs / mean tick duration; "
-                                 "with K > 1 the per-env state stays on chip between ticks, so the kernel moves "
-                                 "fewer bytes than the formula counts (see traffic)"},
+                         "note": "achieved = algorithmic bytes per env-step (SURVEY 8d) x envs / mean tick duration "
+                                 "(kernel_ms: HIP events around the timed launches); frac_wall uses ms_per_step (the "
+                                 "wall clock between the barriers), frac_with_fan_fill adds the shared fan table's "
+                                 "fill amortised over the 1,024 ticks it serves (the timed launches read a table "
+                                 "an earlier launch filled); shared_fan_frac = share of the envs with cameras whose "
+                                 "camera group the table serves; with K > 1 the per-env state stays on chip between "
+                                 "ticks, so the kernel moves fewer bytes than the formula counts (see traffic)"},
+            # the rollout cannot replay K known actions (the policy needs each
+            # observation), so its env figure -- one heist_step launch per tick -- sits beside
+            # the headline at every N
+            "env_only_single_tick": {
+                "value": args.steps * N * world / e1, "unit": "env-steps/s", "kernel_ms": k1,
+                "ms_per_step": e1 / args.steps * 1e3, "host_issue_us_per_step": i1 / args.steps * 1e6,
+                "kernel": "heist::step_kernel", "workload": "one heist_step launch per tick (the rollout's form)",
+                "roofline": {"bound": "hbm", "achieved": b_step * N / (k1 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                             "unit": "GB/s", "frac": b_step * N / (k1 * 1e-3) / 1e9 / HBM_PEAK_GBS}},
             "cpu_baseline": None,
         }
         log("env-only: %.1f M env-steps/s, %.2f us per tick (K=%d)" % (value / 1e6, kern_ms * 1e3, K))
         # single-GPU figures: the secondary numbers and the CPU baseline run on rank 0 at N=1
         # only (at N>1 the other ranks would idle at the closing barrier meanwhile)
+        if world > 1:  # attribution for a 1 -> N curve: every rank's env-only time, the exchange step's cost
+            line["per_rank"] = {"elapsed_s": [r[0] for r in per_rank], "kernel_ms_per_tick": [r[1] for r in per_rank],
+                                "single_tick_elapsed_s": [r[0] for r in per_rank_1],
+                                "single_tick_kernel_ms": [r[1] for r in per_rank_1]}
+            line["allreduce_grads_us_per_optimizer_step"] = allreduce_us
         if not args.no_secondary and world == 1:
             sec = {}
-            if K > 1:  # the rollout's kernel: one tick per launch (the policy needs each observation)
-                log("env-only, one tick per launch (heist_step)")
-                e1, k1, i1, _ = time_env(env, actions, args.warmup, args.steps, 1, 1)
-                sec["env_only_single_tick"] = {
-                    "value": args.steps * N / e1, "unit": "env-steps/s", "kernel_ms": k1,
-                    "host_issue_us_per_step": i1 / args.steps * 1e6, "kernel": "heist::step_kernel",
-                    "roofline": {"bound": "hbm", "achieved": b_step * N / (k1 * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                                 "unit": "GB/s", "frac": b_step * N / (k1 * 1e-3) / 1e9 / HBM_PEAK_GBS}}
             log("env-only at the other BASELINE configs / layout sources")
             other = "synthetic" if args.layouts == "architect" else "architect"
             sec["env_only_%s_layouts" % other] = measure_env_config(dev, 20, N, args.budget, K=K,

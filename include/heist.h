@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define HEIST_ABI_VERSION 1
+#define HEIST_ABI_VERSION 2  /* 2: heist_step_stamps takes the buffer size; heist_stamp_words */
 #define HEIST_EINVAL 100000
 
 /* status_out codes of heist_step (environment.py:236-297 info["status"]). */
@@ -117,12 +117,18 @@ int heist_count_redo(heist_t h, uint64_t* counter);
 
 /* Instrumentation, no reference counterpart: later heist_step calls on h record the shader
  * clock (s_memtime) at 8 phase boundaries of every wavefront into buf[env][wave][10] (waves
- * per env: heist_step_waves(h)): 0 entry, 1 prefetch landed, 2 emitter
- * table published, 3 raycast done, 4 reward done, 5 auto-reset done, 6 observation written,
- * 7 exit.  NULL switches stamping off (default). */
-int heist_step_stamps(heist_t h, uint64_t* buf);
-/* (heist_step_multi with stamps armed writes buf[env][multi_waves][16] instead: clock
- * cycles summed per tick segment 0..8 over the launch, lifetime, start clock, HW_ID, XCC_ID.) */
+ * per env: heist_step_waves(h); slots 8 and 9 hold HW_ID and XCC_ID): 0 entry, 1 prefetch
+ * landed, 2 emitter table published, 3 raycast done, 4 reward done, 5 auto-reset done, 6
+ * observation written, 7 exit.  heist_step_multi writes buf[env][multi_waves][16] instead:
+ * clock cycles summed per tick segment 0..8 over the launch, lifetime, start clock, HW_ID,
+ * XCC_ID.  n_words is buf's size in uint64 words: a call whose kernel needs more
+ * (n_envs * 10 * step_waves, resp. n_envs * 16 * multi_waves; heist_stamp_words reports both)
+ * fails with HEIST_EINVAL instead of writing past it.  NULL switches stamping off (default). */
+int heist_step_stamps(heist_t h, uint64_t* buf, int64_t n_words);
+
+/* uint64 words of a stamp buffer for heist_step (which = 0) or heist_step_multi (which = 1)
+ * on h; no reference counterpart. */
+int64_t heist_stamp_words(heist_t h, int which);
 
 /* Wavefronts per env of h's step / reset kernels (2 unless HEIST_STEP_WAVES chose 1 or 4
  * at heist_create); no reference counterpart. */

@@ -1,4 +1,5 @@
 // heist_capi.hip -- extern "C" entry points of libheist_hip.so (declared in include/heist.h).
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -22,7 +23,7 @@ hipError_t launch_set_layout(const EnvParams& p, int max_walls, const int32_t* w
 hipError_t launch_reset(const EnvParams& p, const uint8_t* mask, float* obs, hipStream_t st);
 hipError_t launch_step(const EnvParams& p, const int64_t* actions, float* obs, float* rew, double* rew64,
                        uint8_t* done_out, int8_t* status_out, int auto_reset, hipStream_t st);
-hipError_t launch_step_multi(const EnvParams& p, const EnvParams* pg, int K, const int64_t* actions, float* obs,
+hipError_t launch_step_multi(const EnvParams& p, int K, const int64_t* actions, float* obs,
                              float* rew, double* rew64, uint8_t* done_out, int8_t* status_out, int auto_reset,
                              hipStream_t st);
 hipError_t launch_export(const EnvParams& p, int32_t* scalars, int8_t* grid, double* cam_heading, int32_t* guard_idx,
@@ -70,12 +71,13 @@ using heist::EnvParams;
 struct heist_env {
   int device;
   EnvParams p;
-  void* allocs[13];
+  void* allocs[12];
   int n_allocs;
-  EnvParams* dev_p;  // device copy of p for the K-tick kernel (read through a pointer, not as kernel arguments)
-  int fan_pos;       // next entry of the shared fan table (FanTick) for a K-tick launch; -1: refill first
-  EnvParams dev_p_host;  // what dev_p holds
-  bool dev_p_valid;
+  int fan_pos;             // next entry of the shared fan table (FanTick) for a K-tick launch; -1: refill first
+  hipStream_t fan_stream;  // stream of the K-tick launch that last used the table (a refill on another stream
+                           // could overwrite entries a launch still in flight on this one reads)
+  bool fan_used;           // a K-tick launch has been issued on fan_stream
+  int64_t stamp_words;     // size of the stamp buffer armed by heist_step_stamps (uint64 words)
 };
 
 namespace {
@@ -256,9 +258,10 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
       (size_t)heist::stop_map_bytes(R, C) * n,
       // guard cone cache: 64 B per (guard, patrol index, heading slot)
       sizeof(uint16_t) * heist::kConeEntry * n * (max_guards > 0 ? max_guards : 1) * heist::kConePath * heist::kConeSlots,
-      sizeof(EnvParams),
       sizeof(heist::FanTick) * heist::kFanTicks,
   };
+  static_assert(sizeof(sizes) / sizeof(sizes[0]) <= sizeof(((heist_env*)nullptr)->allocs) / sizeof(void*),
+                "heist_env::allocs too small");
   h->n_allocs = 0;
   for (size_t k = 0; k < sizeof(sizes) / sizeof(sizes[0]); ++k) {
     void* ptr = nullptr;
@@ -283,14 +286,15 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   p.stop = (uint8_t*)h->allocs[9];
   p.stop_bytes = heist::stop_map_bytes(R, C);
   p.cones = (uint16_t*)h->allocs[10];
-  h->dev_p = (EnvParams*)h->allocs[11];
-  p.fan = (heist::FanTick*)h->allocs[12];
+  p.fan = (heist::FanTick*)h->allocs[11];
   h->fan_pos = -1;
+  h->fan_stream = nullptr;
+  h->fan_used = false;
+  h->stamp_words = 0;
   p.fan_base = 0;
   p.fan_fill = 0;
   p.fan_on = 1;
   if (const char* f = getenv("HEIST_SHARED_FAN")) p.fan_on = atoi(f) ? 1 : 0;
-  h->dev_p_valid = false;
   p.guard_cones = 1;
   if (const char* gc = getenv("HEIST_GUARD_CONES")) p.guard_cones = atoi(gc) ? 1 : 0;
   std::vector<double> hrad(heist::kHalfDegN);
@@ -300,7 +304,7 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   if (!rc) rc = check_hip(hipMemcpy(h->allocs[6], planes.data(), sizes[6], hipMemcpyHostToDevice), "heist_create: upload");
   if (!rc) rc = check_hip(hipMemset(h->allocs[2], 0, sizes[2]), "heist_create: memset");
   // fan table: all 0xFF = NaN emitters and n_uniq = -1, an entry no group can match
-  if (!rc) rc = check_hip(hipMemset(h->allocs[12], 0xFF, sizes[12]), "heist_create: memset");
+  if (!rc) rc = check_hip(hipMemset(h->allocs[11], 0xFF, sizes[11]), "heist_create: memset");
   if (!rc) rc = check_hip(hipMemset(h->allocs[3], 0, sizes[3]), "heist_create: memset");
   if (!rc) rc = check_hip(hipMemset(h->allocs[4], 0, sizes[4]), "heist_create: memset");
   if (!rc) rc = check_hip(hipMemcpy((double*)h->allocs[8] + 2 * heist::kHalfDegN, hrad.data(),
@@ -359,6 +363,7 @@ int heist_step(heist_t h, const int64_t* actions, float* obs_out, float* reward_
                uint8_t* done_out, int8_t* status_out, int auto_reset, heist_stream_t stream) {
   if (int rc = check_handle(h)) return rc;
   HEIST_REQUIRE(actions && obs_out && reward_out && done_out && status_out, "heist_step: null output/input");
+  HEIST_REQUIRE(!h->p.stamps || h->stamp_words >= heist_stamp_words(h, 0), "heist_step: stamp buffer too small");
   h->fan_pos = -1;  // headings advanced outside the K-tick launches' accounting
   return check_hip(heist::launch_step(h->p, actions, obs_out, reward_out, reward64_out, done_out, status_out,
                                       auto_reset, (hipStream_t)stream),
@@ -371,35 +376,42 @@ int heist_step_multi(heist_t h, int K, const int64_t* actions, float* obs_out, f
   if (int rc = check_handle(h)) return rc;
   HEIST_REQUIRE(K >= 1 && K <= 1024, "heist_step_multi: need 1 <= K <= 1024");
   HEIST_REQUIRE(actions && obs_out && reward_out && done_out && status_out, "heist_step_multi: null output/input");
+  // (without a K-tick variant the launch runs K single ticks: either kernel's size may apply)
+  HEIST_REQUIRE(!h->p.stamps || h->stamp_words >= std::max(heist_stamp_words(h, 1), heist_stamp_words(h, 0)),
+                "heist_step_multi: stamp buffer too small");
   hipStream_t st = (hipStream_t)stream;
-  if (!h->dev_p_valid || std::memcmp(&h->dev_p_host, &h->p, sizeof(EnvParams)) != 0) {  // set_* changed it
-    h->dev_p_host = h->p;
-    if (int rc = check_hip(hipMemcpyAsync(h->dev_p, &h->dev_p_host, sizeof(EnvParams), hipMemcpyHostToDevice, st),
-                           "heist_step_multi: params upload"))
-      return rc;
-    if (int rc = check_hip(hipStreamSynchronize(st), "heist_step_multi: params upload")) return rc;
-    h->dev_p_valid = true;
-  }
-  // the shared fan table (FanTick): refilled when stale or used up, else read at the launch's
-  // offset -- only when the K-tick kernel runs (otherwise K single ticks advance the headings)
+  // the shared fan table (FanTick): refilled when stale, used up, or last used by a launch on
+  // another stream (streams do not order a refill against a launch still reading the table:
+  // that stream is drained first, a host wait paid only when the caller switches streams),
+  // else read at the launch's offset -- only when the K-tick kernel runs (otherwise K single
+  // ticks advance the headings)
   EnvParams q = h->p;
   const bool kt = heist::multi_variant_exists(q.multi_waves, q.ray_chunk, q.multi_occ, q.vis_gap) && (q.C & 3) == 0 &&
                   q.probe_mode == 0 && !q.sample_counter && !q.redo_counter;
   q.fan_fill = 0;
   q.fan_base = 0;
+  int next_pos = -1;
   if (kt && q.fan_on) {
-    if (h->fan_pos < 0 || h->fan_pos + K > heist::kFanTicks) {
+    int pos = h->fan_pos;
+    if (pos < 0 || pos + K > heist::kFanTicks || st != h->fan_stream) {
+      if (h->fan_used && st != h->fan_stream)  // the refill must not overtake a launch still reading the table
+        if (int rc = check_hip(hipStreamSynchronize(h->fan_stream), "heist_step_multi: previous stream")) return rc;
       q.fan_fill = 1;
-      h->fan_pos = 0;
+      pos = 0;
     }
-    q.fan_base = h->fan_pos;
-    h->fan_pos += K;
-  } else {
-    h->fan_pos = -1;
+    q.fan_base = pos;
+    next_pos = pos + K;
   }
-  return check_hip(heist::launch_step_multi(q, h->dev_p, K, actions, obs_out, reward_out, reward64_out, done_out,
-                                            status_out, auto_reset, st),
-                   "heist_step_multi");
+  const int rc = check_hip(heist::launch_step_multi(q, K, actions, obs_out, reward_out, reward64_out, done_out,
+                                                    status_out, auto_reset, st),
+                           "heist_step_multi");
+  // the table position advances only with a launch that was issued
+  h->fan_pos = rc ? -1 : next_pos;
+  if (!rc) {
+    h->fan_stream = st;
+    h->fan_used = true;
+  }
+  return rc;
 }
 
 int heist_export(heist_t h, int32_t* scalars, int8_t* grid, double* cam_heading, int32_t* guard_idx,
@@ -421,10 +433,17 @@ int heist_count_redo(heist_t h, uint64_t* counter) {
   return 0;
 }
 
-int heist_step_stamps(heist_t h, uint64_t* buf) {
+int heist_step_stamps(heist_t h, uint64_t* buf, int64_t n_words) {
   if (int rc = check_handle(h)) return rc;
+  HEIST_REQUIRE(buf == nullptr || n_words >= 0, "heist_step_stamps: n_words < 0");
   h->p.stamps = reinterpret_cast<unsigned long long*>(buf);
+  h->stamp_words = buf ? n_words : 0;
   return 0;
+}
+
+int64_t heist_stamp_words(heist_t h, int which) {
+  if (check_handle(h)) return -1;
+  return (int64_t)h->p.n_envs * (which ? 16 * h->p.multi_waves : 10 * h->p.step_waves);
 }
 
 int heist_step_waves(heist_t h) {

@@ -2683,7 +2683,7 @@ size_t step_multi_lds(const EnvParams& p, int K) {
          align16(sizeof(TieBuckets)) + 1024 * (size_t)p.multi_waves + (p.stamps ? 80 * (size_t)p.multi_waves : 0);
 }
 
-hipError_t launch_step_multi(const EnvParams& p, const EnvParams* pg, int K, const int64_t* actions, float* obs,
+hipError_t launch_step_multi(const EnvParams& p, int K, const int64_t* actions, float* obs,
                              float* rew, double* rew64, uint8_t* done_out, int8_t* status_out, int auto_reset,
                              hipStream_t st) {
   const size_t lds = step_multi_lds(p, K);

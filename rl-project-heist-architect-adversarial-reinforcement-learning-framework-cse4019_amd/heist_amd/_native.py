@@ -38,7 +38,8 @@ SIGNATURES = {
     "heist_set_guard_cones": (_i, [_vp, _i]),
     "heist_step_waves": (_i, [_vp]),
     "heist_get_config": (_i, [_vp, _vp, _i]),
-    "heist_step_stamps": (_i, [_vp, _vp]),
+    "heist_step_stamps": (_i, [_vp, _vp, _i64]),
+    "heist_stamp_words": (_i64, [_vp, _i]),
     "heist_bfs_valid": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "heist_cones": (_i, [_i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     "heist_cones_mode": (_i, [_i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp]),

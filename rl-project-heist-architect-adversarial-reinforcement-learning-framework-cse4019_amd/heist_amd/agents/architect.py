@@ -255,12 +255,33 @@ class ArchitectAgent:  # agents/architect.py:16-170
         self.values.clear()
         self.rewards.clear()
 
+    def optimizer_state_dict(self) -> dict:
+        """The optimizer state as the reference's eager Adam keeps it: `capturable` off and
+        the step counters as CPU scalars, whatever the graph replay (_capture) switched on,
+        so a checkpoint loads into the reference's agent on any device
+        (agents/architect.py:165-170: map_location=DEVICE, then Adam.step)."""
+        sd = self.optimizer.state_dict()
+        groups = [dict(g, capturable=False) for g in sd["param_groups"]]
+        state = {}
+        for k, st in sd["state"].items():
+            st = dict(st)
+            if torch.is_tensor(st.get("step")):
+                st["step"] = st["step"].detach().to("cpu", torch.float32).reshape(())
+            state[k] = st
+        return {"state": state, "param_groups": groups}
+
     def save(self, path: str):  # agents/architect.py:157-163
-        torch.save({"network": self.network.state_dict(), "optimizer": self.optimizer.state_dict(),
+        torch.save({"network": self.network.state_dict(), "optimizer": self.optimizer_state_dict(),
                     "episode_count": self.episode_count}, path)
+
+    def _drop_graph(self):
+        """Forget the captured update step (it holds the old optimizer state tensors)."""
+        for k in ("_graph", "_g_r", "_g_vl", "_g_i", "_g_s"):
+            self.__dict__.pop(k, None)
 
     def load(self, path: str):
         ck = torch.load(path, map_location=self.device, weights_only=True)
         self.network.load_state_dict(ck["network"])
         self.optimizer.load_state_dict(ck["optimizer"])
+        self._drop_graph()  # replays would update the replaced exp_avg / exp_avg_sq / step tensors
         self.episode_count = ck.get("episode_count", 0)

@@ -124,3 +124,41 @@ def test_architect_update_sequence_cpu():
 def test_architect_update_sequence_gpu_graph(gpu_device):
     # 40: the first capture (1,024 slots); 5: eager only; 1500: past the slots, captured again
     _sequence_vs_updates(gpu_device, ks=(40, 5, 1500))
+
+
+def _checkpoint_after_sequence_loads_on_cpu(device, tmp_path):
+    """A checkpoint written after update_sequence (graph replay: capturable Adam on the
+    device) loads into a CPU agent, as the reference's load does (map_location=DEVICE,
+    agents/architect.py:165-170), and that agent's update() steps (Adam's capturable-device
+    check would fail on a saved capturable=True); the saved state is the live one."""
+    torch.manual_seed(3)
+    a = ArchitectAgent(grid_rows=12, grid_cols=12, device=device)
+    g = torch.Generator().manual_seed(4)
+    lp, v, r = (torch.randn(30, generator=g, dtype=torch.float64) for _ in range(3))
+    a.update_sequence(lp, v, r)
+    path = str(tmp_path / "architect_ep1.pt")
+    a.save(path)
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    assert all(not grp.get("capturable", False) for grp in ck["optimizer"]["param_groups"])
+    cpu = ArchitectAgent(grid_rows=12, grid_cols=12, device=torch.device("cpu"))
+    cpu.load(path)
+    for (n, p), q in zip(cpu.network.state_dict().items(), a.network.state_dict().values()):
+        assert torch.equal(p, q.cpu()), n
+    before = [p.detach().clone() for p in cpu.network.parameters()]
+    cpu.log_probs, cpu.values = [torch.tensor(0.1)], [torch.tensor(0.2)]
+    cpu.store_reward(0.5)
+    cpu.update(collective=False)
+    assert any(not torch.equal(p, q) for p, q in zip(cpu.network.parameters(), before))
+    # the source agent keeps replaying after a load (its graph dropped and re-captured)
+    a.load(path)
+    assert getattr(a, "_graph", None) is None
+    a.update_sequence(lp[:12], v[:12], r[:12])
+
+
+def test_architect_checkpoint_after_sequence_cpu(tmp_path):
+    _checkpoint_after_sequence_loads_on_cpu(torch.device("cpu"), tmp_path)
+
+
+@pytest.mark.gpu
+def test_architect_checkpoint_after_sequence_gpu(gpu_device, tmp_path):
+    _checkpoint_after_sequence_loads_on_cpu(gpu_device, tmp_path)

@@ -35,6 +35,11 @@ def test_bench_driver_command_line(gpu_device):
     rf = out["roofline"]
     assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["achieved"] > 0
     assert out["config"]["kernel_config"]["probe_mode"] == 0
+    # the amortised fan fill, the wall-clock fraction and the fan's reach
+    assert 0 < rf["frac_wall"] <= rf["frac"] * 1.0001 and 0 < rf["frac_with_fan_fill"] <= rf["frac"]
+    assert rf["fan_fill_ms_per_fill"] >= 0 and rf["shared_fan_frac"] == 1.0  # Architect batch: one camera fan
+    st = out["env_only_single_tick"]  # the rollout's one-tick-per-launch figure beside it
+    assert st["value"] > 0 and st["kernel"] == "heist::step_kernel"
 
 
 def test_bench_refuses_profiling_kernel(gpu_device):
@@ -51,5 +56,7 @@ def test_bench_two_ranks_gloo(gpu_device):
                 "--train-envs", "256", "--no-cpu-baseline"], 900)
     assert out["n_gpus"] == 2 and out["config"]["backend"] == "gloo"
     assert out["value"] > 0 and math.isfinite(out["value"])
+    assert len(out["per_rank"]["elapsed_s"]) == 2 and len(out["per_rank"]["single_tick_kernel_ms"]) == 2
+    assert out["allreduce_grads_us_per_optimizer_step"] > 0 and out["env_only_single_tick"]["value"] > 0
     tr = out["full_train_c4_multi_gpu"]
     assert tr["n_gpus"] == 2 and tr["value"] > 0 and math.isfinite(tr["value"])

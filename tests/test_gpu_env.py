@@ -263,9 +263,9 @@ def test_step_stamps_instrumentation(gpu_device):
     g = torch.Generator(device="cpu").manual_seed(3)
     for t in range(20):
         a = torch.randint(0, 5, (n,), generator=g)
-        nat.check(nat.lib().heist_step_stamps(envs[0]._h, nat.ptr(buf)), "heist_step_stamps")
+        nat.check(nat.lib().heist_step_stamps(envs[0]._h, nat.ptr(buf), buf.numel()), "heist_step_stamps")
         r0 = envs[0].step(a)
-        nat.check(nat.lib().heist_step_stamps(envs[0]._h, None), "heist_step_stamps")
+        nat.check(nat.lib().heist_step_stamps(envs[0]._h, None, 0), "heist_step_stamps")
         r1 = envs[1].step(a)
         for x, y in zip(r0, r1):
             assert torch.equal(x, y), t
@@ -273,6 +273,19 @@ def test_step_stamps_instrumentation(gpu_device):
     assert (s[:, :, :8] > 0).all()
     assert (np.diff(s[:, :, :8], axis=2) >= 0).all()
     assert (s[:, :, 8] != 0).any()
+    # a buffer too small for the kernel a call runs is refused, not overrun
+    L = nat.lib()
+    need0, need1 = L.heist_stamp_words(envs[0]._h, 0), L.heist_stamp_words(envs[0]._h, 1)
+    assert need0 == n * 10 * w and need1 == n * 16 * envs[0].kernel_config()["multi_waves"]
+    small = torch.zeros(min(need0, need1) - 1, dtype=torch.int64, device=gpu_device)
+    nat.check(L.heist_step_stamps(envs[0]._h, nat.ptr(small), small.numel()), "heist_step_stamps")
+    acts = torch.zeros((2, n), dtype=torch.int64, device=gpu_device)
+    with pytest.raises(nat.HeistError):
+        envs[0].step_multi(acts)
+    with pytest.raises(nat.HeistError):
+        envs[0].step(acts[0])
+    nat.check(L.heist_step_stamps(envs[0]._h, None, 0), "heist_step_stamps")
+    envs[0].step_multi(acts)
 
 
 @pytest.mark.parametrize("cones", [False, True], ids=["live_guards", "guard_cones"])
@@ -644,6 +657,67 @@ def test_step_multi_c2_checkpoint_layouts(gpu_device):
     for k in range(80):
         o, r, d, s = b.step(acts[k])
         assert torch.equal(obs[k], o) and torch.equal(done[k], d) and torch.equal(status[k], s), k
+
+
+def test_step_multi_bench_launch_sequence_with_fan_refill(gpu_device):
+    """The headline launch sequence exactly as bench.py issues it (4096 C2-checkpoint envs,
+    a 5-tick warm-up launch, then 20-tick launches read the shared fan table at offsets 5,
+    25, ...), continued for 1,045 ticks so that the table is refilled once (the 51st 20-tick
+    launch, ticks 1005-1024: fan_pos 1005 + 20 > kFanTicks, heist_capi.hip heist_step_multi)
+    and read again after the refill.  Every tick of every env == single ticks bit for bit,
+    and 32 envs == the C oracle on every tick's reward/done/status, with their observation
+    rows compared byte for byte on the ticks around the refill (reference
+    environment.py:216-299, security.py:49-101)."""
+    import os
+    from heist_amd.layouts import architect_checkpoint_layouts
+    from heist_amd.training import _lb_rows
+    ckpt = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "checkpoints",
+                        "architect_c2_fixed.pt")
+    n, budget = 4096, 15
+    cfg = EnvironmentConfig(architect_budget=budget)
+    envs = []
+    for _ in range(2):  # the bench's handle shape (bench.py: max_cams = budget // 3, max_guards = budget // 5)
+        env = HeistEnv(n, cfg, max_cams=5, max_guards=3, max_path=16, device=gpu_device)
+        lb, ok = architect_checkpoint_layouts(env, budget, seed=1234, ckpt=ckpt)
+        assert ok
+        env.reset()
+        envs.append(env)
+    a, b = envs
+    assert a.kernel_config()["multi_waves"] == 1 and a.kernel_config()["fan_on"] == 1
+    chunks = [5] + [20] * 52
+    T = sum(chunks)
+    assert T >= 1040
+    g = torch.Generator(device=gpu_device).manual_seed(4321)
+    acts = torch.randint(0, 5, (T, n), device=gpu_device, generator=g, dtype=torch.int64)
+    pick = np.random.default_rng(67).choice(n, 32, replace=False)
+    pick_t = torch.from_numpy(pick).to(gpu_device)
+    oracles = _oracle_envs(cfg, _lb_rows(lb, pick).to_lists(), budget)
+    acts_p = acts[:, pick_t].cpu().numpy()
+    window = range(985, 1045)  # the refill launch is ticks 1005-1024
+    k0 = 0
+    for K in chunks:
+        obs, rew, done, status, r64 = a.step_multi(acts[k0:k0 + K], reward64=True)
+        for k in range(K):
+            o, r, d, s = b.step(acts[k0 + k])
+            ctx = "tick %d" % (k0 + k)
+            assert torch.equal(obs[k], o), ctx
+            assert torch.equal(r64[k], b.reward64), ctx
+            assert torch.equal(rew[k], r) and torch.equal(done[k], d) and torch.equal(status[k], s), ctx
+        r64p, dp, sp = (x[:, pick_t].cpu().numpy() for x in (r64, done, status))
+        need_obs = any(k0 + k in window for k in range(K))
+        obs_p = obs[:, pick_t].cpu().numpy() if need_obs else None
+        for k in range(K):
+            for j in range(len(pick)):
+                r, d, s = oracles[j].step(int(acts_p[k0 + k, j]))
+                if d:
+                    oracles[j].reset()
+                assert (r64p[k, j], bool(dp[k, j]), int(sp[k, j])) == (r, d, s), "env %d t %d" % (pick[j], k0 + k)
+                if need_obs and k0 + k in window:
+                    assert obs_p[k, j].tobytes() == oracles[j].state_tensor().tobytes(), "env %d t %d" % (pick[j], k0 + k)
+        k0 += K
+    sa, sb = a.export(grid=True), b.export(grid=True)
+    for key in sb:
+        assert torch.equal(sa[key], sb[key]), key
 
 
 @pytest.mark.parametrize("waves", [1, 2])

@@ -36,12 +36,12 @@ def main():
     buf = torch.zeros((n, W, 16), dtype=torch.int64, device="cuda")
     out = {"n": n, "K": K, "waves": W, "launches": []}
     for j in range(2, 4):
-        nat.check(nat.lib().heist_step_stamps(env._h, nat.ptr(buf)), "heist_step_stamps")
+        nat.check(nat.lib().heist_step_stamps(env._h, nat.ptr(buf), buf.numel()), "heist_step_stamps")
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
         env.step_multi(acts[j * K:(j + 1) * K])
         ev1.record()
-        nat.check(nat.lib().heist_step_stamps(env._h, None), "heist_step_stamps")
+        nat.check(nat.lib().heist_step_stamps(env._h, None, 0), "heist_step_stamps")
         torch.cuda.synchronize()
         s = buf.cpu().numpy().astype(np.int64)
         rec = {"launch_ms": ev0.elapsed_time(ev1)}

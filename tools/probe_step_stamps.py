@@ -48,9 +48,9 @@ def main():
     buf = torch.zeros((n, waves, 10), dtype=torch.int64, device="cuda")
     out = {"n": n, "waves": waves, "steps": []}
     for k in range(3):
-        nat.check(nat.lib().heist_step_stamps(env._h, nat.ptr(buf)), "heist_step_stamps")
+        nat.check(nat.lib().heist_step_stamps(env._h, nat.ptr(buf), buf.numel()), "heist_step_stamps")
         _, _, done, _ = env.step(acts[10 + k])
-        nat.check(nat.lib().heist_step_stamps(env._h, None), "heist_step_stamps")
+        nat.check(nat.lib().heist_step_stamps(env._h, None, 0), "heist_step_stamps")
         torch.cuda.synchronize()
         s = buf.cpu().numpy().astype(np.int64)
         d = done.cpu().numpy().astype(bool)

@@ -135,9 +135,9 @@ int64_t heist_stamp_words(heist_t h, int which);
 int heist_step_waves(heist_t h);
 
 /* The handle's effective kernel configuration, no reference counterpart (what a benchmark
- * records next to its numbers): out[0..n) with n <= 12 receives step_waves, ray_chunk,
+ * records next to its numbers): out[0..n) with n <= 13 receives step_waves, ray_chunk,
  * step_occ, vis_gap, obs_store, ray_mode, probe_mode, dispatch_order, split_obs,
- * guard_cones, multi_waves, fan_on (the HEIST_* environment knobs as heist_create resolved them,
+ * guard_cones, multi_waves, fan_on, lean (the HEIST_* environment knobs as heist_create resolved them,
  * then any heist_set_* calls).  probe_mode != 0 selects the profiling step kernel, whose results are
  * wrong by design (phases skipped). */
 int heist_get_config(heist_t h, int32_t* out, int n);

@@ -295,6 +295,8 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   p.fan_fill = 0;
   p.fan_on = 1;
   if (const char* f = getenv("HEIST_SHARED_FAN")) p.fan_on = atoi(f) ? 1 : 0;
+  p.lean = 1;
+  if (const char* f = getenv("HEIST_LEAN")) p.lean = atoi(f) ? 1 : 0;
   p.guard_cones = 1;
   if (const char* gc = getenv("HEIST_GUARD_CONES")) p.guard_cones = atoi(gc) ? 1 : 0;
   std::vector<double> hrad(heist::kHalfDegN);
@@ -453,10 +455,11 @@ int heist_step_waves(heist_t h) {
 
 int heist_get_config(heist_t h, int32_t* out, int n) {
   if (int rc = check_handle(h)) return rc;
-  HEIST_REQUIRE(out != nullptr && n >= 0 && n <= 12, "heist_get_config: need out != NULL and 0 <= n <= 12");
+  HEIST_REQUIRE(out != nullptr && n >= 0 && n <= 13, "heist_get_config: need out != NULL and 0 <= n <= 13");
   const EnvParams& p = h->p;
-  const int32_t v[12] = {p.step_waves, p.ray_chunk,  p.step_occ,       p.vis_gap,   p.obs_store,  p.ray_mode,
-                         p.probe_mode, p.dispatch_order, p.split_obs, p.guard_cones, p.multi_waves, p.fan_on};
+  const int32_t v[13] = {p.step_waves, p.ray_chunk,  p.step_occ,       p.vis_gap,   p.obs_store,  p.ray_mode,
+                         p.probe_mode, p.dispatch_order, p.split_obs, p.guard_cones, p.multi_waves, p.fan_on,
+                         p.lean};
   for (int k = 0; k < n; ++k) out[k] = v[k];
   return 0;
 }

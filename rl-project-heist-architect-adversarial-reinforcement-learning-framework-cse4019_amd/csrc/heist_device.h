@@ -85,7 +85,7 @@ struct Emit {
 static_assert(sizeof(Emit) == 56, "Emit layout");
 
 // The K-tick kernel's shared camera fan (fan_kernel, heist_env.hip): for tick k of a
-// launch, the fast-path fan of env 0's first camera as that tick casts it -- the emitter
+// launch, the fast-path fan of the source camera (the first env's first camera) as that tick casts it -- the emitter
 // (heading - fov / 2, fov, rays, range) and, computed once for the whole batch, its rays'
 // unique fp32 directions (one per dedup key) and its near-tie rays.  A direction group
 // whose emitter equals the tick's entry bit for bit takes its rays from the table instead
@@ -100,8 +100,17 @@ constexpr int kFanTicks = 1024;  // the K-tick launch's K limit
 struct FanTick {
   double hmh, fov;
   int num_rays, range, n_uniq, n_tie;
+  double heading, speed;     // the source camera's heading at this tick (after its rotation) and speed
   float uniq[2 * kFanRays];  // (dxs, dys) of the unique directions
   uint16_t tie[kFanRays];    // ray indices of the near-tie rays (exact path)
+  // The unique directions' sample tiles for the lean K-tick kernel: direction j's sample k
+  // (k = 1 .. 12, dist k / 2) lands on tile (row + dr, col + dc) with dc = rint(k * dxs), dr =
+  // rint(k * dys) -- exactly the fast path's march, which rounds col + k * dxs once and, the
+  // direction screened off every .5 tie, equals col + rint(k * dxs) -- stored as the index of
+  // that tile in the padded plane counted from the tile (row - kRing, col - kRing):
+  // (dr + kRing) * (C + 2 kRing) + dc + kRing, u16 pairs, samples 1-8 in off4, 9-12 in off2.
+  uint4 off4[kFanRays];
+  uint2 off2[kFanRays];
 };
 
 struct EnvParams {
@@ -141,6 +150,7 @@ struct EnvParams {
   int ray_mode;               // 0: fp32 fast path with exact fp64 re-cast of near-tie rays; 1: exact fp64 only
   FanTick* fan;               // [kFanTicks] shared camera fan of the current K-tick launch (fan_kernel)
   int fan_on;                 // 1 (default): the K-tick kernel uses the shared fan (HEIST_SHARED_FAN)
+  int lean;                   // 1 (default): one-wave 20 x 20 K-tick launches run step_lean_kernel (HEIST_LEAN)
   int fan_base;               // table entry of the launch's tick 0 (heist_step_multi)
   int fan_fill;               // 1: the launch first refills the table from the cameras' current headings
   int probe_mode;             // profiling only (HEIST_PROBE_MODE): 0 normal, 1 no rays, 2 angles+sin/cos only,

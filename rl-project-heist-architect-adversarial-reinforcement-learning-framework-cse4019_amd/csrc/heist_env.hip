@@ -1060,6 +1060,7 @@ __device__ __forceinline__ void patch4(float4& v, int m, float val) {
 // + dirty bytes / 6 TB/s per dependent launch).  Measured per 4096-env step (C2 layouts,
 // profiles/r02ba_probe_obs_store.log): plain 16.66 us, sc1 16.22, nt 15.44, sc1 nt 16.10.
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void obs_put(__amdgpu_buffer_rsrc_t rs, int pol, int off, float4 v) {
   const u32x4_t u = __builtin_bit_cast(u32x4_t, v);
   if (pol == 1) __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, 16);       // sc1
@@ -1463,7 +1464,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
 // K ticks per launch (heist_step_multi)
 // ---------------------------------------------------------------------------
 
-// The shared camera fan table (FanTick), block k = table entry k: env 0's first camera after
+// The shared camera fan table (FanTick), block k = table entry k: the first camera of the
+// first env with a camera (env 0's, in practice) after
 // k + 1 rotations from its heading when the filling launch starts (security.py:49-51, every
 // tick acting; heist_step_multi fills kFanTicks entries and later launches read them at
 // their offset fan_base), its emitter as
@@ -1476,9 +1478,19 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
 __global__ __launch_bounds__(kFanRays) void fan_kernel(EnvParams p) {
   FanTick* F = p.fan + blockIdx.x;
   const int t = threadIdx.x;
-  Cam cm = p.cams[0];
-  const bool ok = p.max_cams > 0 && p.scal[0].n_cams > 0 && p.ray_mode == 0 && cm.range <= kTieMaxRange &&
-                  cm.num_rays >= 0 && cm.num_rays < kFanRays;
+  // the source camera: the first camera of the first env that has one
+  __shared__ int src;
+  if (t == 0) src = 0x7fffffff;
+  __syncthreads();
+  for (int b0 = 0; b0 < p.n_envs; b0 += kFanRays) {
+    const int e = b0 + t;
+    if (e < p.n_envs && p.max_cams > 0 && p.scal[e].n_cams > 0) atomicMin(&src, e);
+    __syncthreads();
+    if (src != 0x7fffffff) break;
+  }
+  const bool found = src != 0x7fffffff;
+  Cam cm = p.cams[found ? (size_t)src * p.max_cams : 0];
+  const bool ok = found && p.ray_mode == 0 && cm.range <= kTieMaxRange && cm.num_rays >= 0 && cm.num_rays < kFanRays;
   if (!ok) {
     if (t == 0) F->n_uniq = -1;
     return;
@@ -1519,12 +1531,32 @@ __global__ __launch_bounds__(kFanRays) void fan_kernel(EnvParams p) {
   of += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bf >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bf, 0u));
   ot += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bt >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bt, 0u));
   if (fresh) {
-    F->uniq[2 * of] = below_one(cf) * 0.5f;  // camera sample stride: half tiles (cast_rays)
-    F->uniq[2 * of + 1] = -below_one(sf) * 0.5f;
+    const float dxs = below_one(cf) * 0.5f, dys = -below_one(sf) * 0.5f;  // camera sample stride: half tiles
+    F->uniq[2 * of] = dxs;
+    F->uniq[2 * of + 1] = dys;
+    // the march's tiles relative to the emitter (FanTick::off4/off2): k * d is exact in fp64 and
+    // no sample is a .5 tie (the screen), so rint here is the fma's rounding in march_fast
+    const int PCf = p.C + 2 * kRing;
+    uint32_t w[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      uint32_t pair = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const double kk = (double)(2 * i + h + 1);
+        const int dc = (int)__builtin_rint(kk * (double)dxs), dr = (int)__builtin_rint(kk * (double)dys);
+        pair |= (uint32_t)((dr + kRing) * PCf + dc + kRing) << (16 * h);
+      }
+      w[i] = pair;
+    }
+    F->off4[of] = make_uint4(w[0], w[1], w[2], w[3]);
+    F->off2[of] = make_uint2(w[4], w[5]);
   }
   if (tie) F->tie[ot] = (uint16_t)t;
   if (t == 0) {
     F->hmh = E.hmh;
+    F->heading = cm.heading;
+    F->speed = cm.speed;
     F->fov = E.fov;
     F->num_rays = E.num_rays;
     F->range = E.range;
@@ -1760,13 +1792,12 @@ __device__ __forceinline__ void stamp_guard_cones(const EnvLds& L, uint8_t* gvis
 // bit 0 skips the raycast and the cone stamps, bit 1 the observation stores, bit 2 the
 // rays' marches (directions and tie screens only).
 template <int W, int U, int O, int D, bool STAMP = false, int PROBE = 0>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) void step_multi_kernel(
-    EnvParams p, int K, const int64_t* __restrict__ actions, float* __restrict__ obs, float* __restrict__ rew,
-    double* __restrict__ rew64, uint8_t* __restrict__ done_out, int8_t* __restrict__ status_out, int auto_reset) {
+__device__ __forceinline__ void step_multi_body(
+    const EnvParams& p, int K, const int64_t* __restrict__ actions, float* __restrict__ obs, float* __restrict__ rew,
+    double* __restrict__ rew64, uint8_t* __restrict__ done_out, int8_t* __restrict__ status_out, int auto_reset,
+    unsigned char* smem, int e) {
   constexpr int NT = 64 * W;
   constexpr bool SOLO = W == 1;  // one wave does every role
-  extern __shared__ __align__(16) unsigned char smem[];
-  const int e = p.dispatch_order ? p.order[blockIdx.x] : (int)blockIdx.x;
   const int t = threadIdx.x;
   const bool w0 = (t >> 6) == 0;
   const int RC = p.RC, N = p.n_envs;
@@ -2076,6 +2107,545 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     gp->pos = gd.pos;
     gp->hslot = gd.hslot;
     gp->nslot = gd.nslot;
+  }
+}
+
+template <int W, int U, int O, int D, bool STAMP = false, int PROBE = 0>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) void step_multi_kernel(
+    EnvParams p, int K, const int64_t* __restrict__ actions, float* __restrict__ obs, float* __restrict__ rew,
+    double* __restrict__ rew64, uint8_t* __restrict__ done_out, int8_t* __restrict__ status_out, int auto_reset) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int e = p.dispatch_order ? p.order[blockIdx.x] : (int)blockIdx.x;
+  step_multi_body<W, U, O, D, STAMP, PROBE>(p, K, actions, obs, rew, rew64, done_out, status_out, auto_reset, smem, e);
+}
+
+// ---------------------------------------------------------------------------
+// Lean K-tick kernel (heist_step_multi, one wave per env, grids up to 20 x 20)
+// ---------------------------------------------------------------------------
+//
+// The same K ticks as step_multi_kernel, bit for bit, laid out for the one-wave case so
+// that a tick is a short chain of register and LDS work with no wait on global memory:
+//   * every per-launch constant in registers: the lane's camera / guard record, the
+//     observation's static channels 0 and 2 and its LDS offsets (two quads per lane), the
+//     stop map's rows as bit masks (lane r = row r: the solver's wall test is a readlane);
+//   * the data the next tick needs from HBM -- the shared fan's header and its unique
+//     directions' sample tiles (FanTick::off4/off2), the cached guards' cone entries -- is
+//     loaded at the end of the previous tick, BEFORE that tick's channel-1 stores: vmcnt
+//     counts loads and stores in issue order, so waiting for a load issued after the stores
+//     would wait for the stores to reach memory;
+//   * one visibility plane for cameras and guards (the cached cones ORed in with ds_or_b32);
+//     detection reads the solver's byte from the channel-1 quads the observation loads
+//     anyway; a finishing env whose guards stood off their start re-casts from the reset
+//     poses (rare: the reset observation needs the guards at patrol point 0);
+//   * a camera group the shared fan serves (every live camera's emitter equals the tick's
+//     table entry, no near-tie ray, range 6) marches the table's unique directions from
+//     each camera's tile, one address add per sample: the table holds each sample's tile as
+//     an offset from the camera's corner tile;
+//   * near-tie rays of the fan (rare) are cast on the exact path from each camera;
+//   * an env the lean loop cannot serve for the whole launch -- a camera that is not the fan's
+//     (heading, speed, fov, rays, range 6 at the launch's first tick: then every tick's
+//     camera equals the table's), a live-raycast guard, exact-only mode, an env already
+//     finished at the launch's start -- runs the generic K-tick body (step_multi_body) in the
+//     same launch, before any lean register is live;
+//   * an env that finished without auto-reset is frozen (environment.py:232-233): its plane
+//     is kept and only its outputs are written.
+
+// LDS-DMA of 16 bytes per active lane (global_load_lds_dwordx4: lane i's bytes land at
+// lds_dst + 16 i), issued as inline asm so that the compiler's vmcnt bookkeeping does not
+// see it: the lean kernel waits for these with its own counted s_waitcnt (kLeanStores).  M0
+// (the LDS destination base) is set and restored inside the statement.
+__device__ __forceinline__ void lds_dma16(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+
+// The exact path (exact_ray) for a shared fan's near-tie rays (FanTick::tie), from every
+// camera of the env (camera m's tile in lane m of cam_rc): a call, so that the glibc sin/cos
+// restatement's registers stay out of the lean loop (near-tie rays are rare).
+template <int D, int PC>
+__device__ __noinline__ void lean_tie_rays(unsigned char* smem, const FanTick* f, int n_tie, uint32_t cam_rc, int n_cams,
+                                           const double* hd) {
+  const int lane = threadIdx.x;
+  for (int b0 = 0; b0 < n_tie; b0 += 64) {
+    const int tr = b0 + lane < n_tie ? (int)f->tie[b0 + lane] : -1;
+    for (int m = 0; m < n_cams; ++m) {
+      Emit E;
+      E.hmh = f->hmh;
+      E.fov = f->fov;
+      E.step = 0.0;
+      E.range = f->range;
+      E.num_rays = f->num_rays;
+      const uint32_t rcm = (uint32_t)__builtin_amdgcn_readlane((int)cam_rc, m);
+      E.row = (int)(rcm & 0xffu);
+      E.col = (int)(rcm >> 8);
+      E.first = 0;
+      E.kind = 0;
+      E.members = 1;
+      if (tr >= 0) exact_ray<4, D>(smem, E, tr, PC, 0, hd);
+    }
+  }
+}
+
+// The lean kernel's LDS: the three padded planes (stop map, visibility, sink; the step
+// kernels' geometry, so exact_ray works on them), the tile grid, the patrol paths, the
+// launch's K actions, the LDS-DMA staging of the next tick's HBM data (LeanStage), the
+// cached guards' cone rows [tick parity][rows 0-7 | 8-15][max_guards] x 16 B, and the static
+// position plane (channel 2 with the vault patched) -- or step_multi_body's, if larger, for
+// the envs that take it.
+size_t step_multi_lds(const EnvParams& p, int K);
+struct LeanStage {
+  uint4 off4[128];  // the fan's unique directions 0 .. 127, samples 1-8 (FanTick::off4)
+  uint2 off2[128];  // samples 9-12 (FanTick::off2)
+  int hdr[4];       // FanTick num_rays, range, n_uniq, n_tie
+};
+struct LeanLds {
+  uint8_t* grid;
+  uint16_t* path;
+  uint8_t* act;
+  LeanStage* stg;
+  uint16_t* cone;
+  float4* plane2;
+};
+__host__ __device__ inline size_t lean_carve(unsigned char* smem, int R, int C, int mg, int mp, int K, LeanLds* L) {
+  size_t o = 3 * 1024;
+  if (L) L->grid = smem + o;
+  o += align16((size_t)R * C);
+  if (L) L->path = reinterpret_cast<uint16_t*>(smem + o);
+  o += align16(2 * (size_t)mg * mp);
+  if (L) L->act = smem + o;
+  o += align16((size_t)K);
+  if (L) L->stg = reinterpret_cast<LeanStage*>(smem + o);
+  o += sizeof(LeanStage);
+  if (L) L->cone = reinterpret_cast<uint16_t*>(smem + o);
+  o += 64 * (size_t)(mg > 0 ? mg : 1);
+  if (L) L->plane2 = reinterpret_cast<float4*>(smem + o);
+  o += 4 * (size_t)R * C;
+  return o;
+}
+static size_t lean_lds_bytes(const EnvParams& p, int K) {
+  const size_t lean = lean_carve(nullptr, p.R, p.C, p.max_guards, p.max_path, K, nullptr);
+  const size_t generic = step_multi_lds(p, K);  // the envs that take step_multi_body
+  return lean > generic ? lean : generic;
+}
+
+// Stores the lean tick issues, every tick, after the LDS-DMA of the next tick's data:
+// observation channels 0, 1, 2 for two quads per lane (6), the solver's quad of channel 2,
+// reward, reward64, done, status.  The next tick's `s_waitcnt vmcnt(kLeanStores)` therefore
+// retires the DMA and never waits for a store.
+constexpr int kLeanStores = 11;
+
+// A cached guard's per-tick state packed in two registers: patrol index | step << 8 | len
+// << 16 | heading slot << 24, and position | position 0 << 16 (row | col << 8 each); the slot
+// after its next move rides in a third.
+struct LeanGuard {
+  uint32_t a, b, nslot;
+  __device__ int idx() const { return (int)(a & 0xffu); }
+  __device__ int step() const { return (int)((a >> 8) & 0xffu); }
+  __device__ int len() const { return (int)((a >> 16) & 0xffu); }
+  __device__ int hslot() const { return (int)(a >> 24); }
+  __device__ uint32_t pos() const { return b & 0xffffu; }
+  __device__ uint32_t pos0() const { return b >> 16; }
+};
+
+template <int R_, int C_>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void step_lean_kernel(
+    EnvParams p, int K, const int64_t* __restrict__ actions, float* __restrict__ obs, float* __restrict__ rew,
+    double* __restrict__ rew64, uint8_t* __restrict__ done_out, int8_t* __restrict__ status_out, int auto_reset) {
+  constexpr int D = 1024;
+  constexpr int PC = C_ + 2 * kRing;
+  constexpr int RC = R_ * C_;
+  constexpr int N4 = RC / 4;
+  constexpr int C4 = C_ / 4;
+  constexpr int OFF0 = kRing * PC + kRing;  // padded index of tile (0, 0); also a sample's offset on its own tile
+  static_assert((R_ + 2 * kRing) * PC <= D, "the padded planes fit the 1024-byte gap");
+  static_assert(C_ % 4 == 0 && N4 <= 64 * kObsQ && R_ <= 64 && C_ <= 32, "lean kernel geometry");
+  extern __shared__ __align__(16) unsigned char smem[];
+  const int e = p.dispatch_order ? p.order[blockIdx.x] : (int)blockIdx.x;
+  const int lane = threadIdx.x;
+  const int N = p.n_envs;
+  const int mc = p.max_cams, mg = p.max_guards, n_slot = mc + mg, mp = p.max_path;
+  const EnvBase eb = env_base(p, e);
+  const FanTick* fan0 = p.fan + p.fan_base;
+
+  // ---- which kernel body serves this env for the launch: the lean loop needs every live
+  // camera to BE the shared fan's source camera (same heading after this launch's first
+  // rotation, same speed, fov, rays and range 6: then the table's entry k is this camera's
+  // fan at tick k, the same functions on the same inputs), every live guard cached, and the
+  // env acting at the first tick
+  EnvScalars s = p.scal[e];
+  const int g = lane - mc;
+  double heading = 0.0, speed = 0.0;  // camera lanes
+  uint32_t cam_rc = 0;                // camera lanes: row | col << 8
+  LeanGuard gd{0u, 0u, 0u};           // guard lanes
+  const bool live_cam = lane < s.n_cams, live_guard = g >= 0 && g < s.n_guards;
+  bool cached = false;
+  {
+    EmitterRaw rec;
+    rec.a = make_uint4(0u, 0u, 0u, 0u);
+    rec.b = rec.a;
+    if (lane < n_slot) {
+      const uint4* rs = lane < mc ? reinterpret_cast<const uint4*>(eb.cams + (uint32_t)lane)
+                                  : reinterpret_cast<const uint4*>(eb.guards + (uint32_t)g);
+      rec.a = rs[0];
+      rec.b = rs[1];
+    }
+    const Cam cm = as_cam(rec);
+    const Guard gr = as_guard(rec);
+    heading = cm.heading;
+    speed = cm.speed;
+    cam_rc = (uint32_t)cm.row | ((uint32_t)cm.col << 8);
+    cached = live_guard && gr.hslot != kUncached;
+    gd.a = (uint32_t)(uint8_t)gr.idx | ((uint32_t)(uint8_t)gr.step << 8) | ((uint32_t)(uint8_t)gr.len << 16) |
+           ((uint32_t)gr.hslot << 24);
+    gd.b = (uint32_t)gr.pos | ((uint32_t)gr.pos0 << 16);
+    gd.nslot = gr.nslot;
+    const double f_heading = fan0->heading, f_speed = fan0->speed, f_fov = fan0->fov;
+    const int f_rays = fan0->num_rays, f_range = fan0->range, f_uniq = fan0->n_uniq;
+    const bool cam_ok = !live_cam || (py_mod360(cm.heading + cm.speed * 1.0) == f_heading && cm.speed == f_speed &&
+                                      cm.fov == f_fov && cm.num_rays == f_rays && cm.range == f_range);
+    // patrol index, step and length fit the packed bytes: a cached guard has <= kConePath points
+    const bool ok = p.fan_on && p.ray_mode == 0 && !s.done && f_uniq >= 0 && f_range == kTieMaxRange &&
+                    __ballot(!cam_ok || (live_guard && !cached)) == 0ull;
+    if (!ok) {
+      step_multi_body<1, 4, 4, D, false, 0>(p, K, actions, obs, rew, rew64, done_out, status_out, auto_reset, smem, e);
+      return;
+    }
+  }
+
+  // ---- prologue: the env's layout and state, once per launch
+  LeanLds L;
+  lean_carve(smem, R_, C_, mg, mp, K, &L);
+  uint8_t* const wall = smem;          // [0, D): the padded stop map
+  uint8_t* const vis = smem + D;       // [D, 2D): the visibility plane; [2D, 3D): the sink
+  const uint32_t base = (uint32_t)(uintptr_t)smem;  // LDS address of the stop map
+  const uint32_t stg_a = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)L.stg);
+  const uint32_t stc_a = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)L.cone);
+  {
+    // grid (static observation channel 0) and the padded stop map, as prefetch does
+    const uint32_t* g4 = reinterpret_cast<const uint32_t*>(p.grid + (size_t)e * RC);
+    for (int i = lane; i < N4; i += 64) reinterpret_cast<uint32_t*>(L.grid)[i] = g4[i];
+    const uint8_t* ss = p.stop + (size_t)e * p.stop_bytes;
+    for (int i = lane; i < p.stop_bytes; i += 64) expand_stop(wall, i, ss[i]);
+    const int vault = p.vr * C_ + p.vc, qv = vault >> 2;
+    for (int q = lane; q < N4; q += 64) {  // channel 2's static plane with the vault patched
+      float4 v = reinterpret_cast<const float4*>(p.plane0)[q];
+      if (q == qv) patch4(v, vault & 3, p.vault_val);
+      L.plane2[q] = v;
+    }
+  }
+  for (int i = lane; i < mg * mp; i += 64) L.path[i] = eb.paths[i];
+  for (int k = lane; k < K; k += 64) {
+    const int64_t a = actions[(size_t)k * N + e];
+    L.act[k] = (uint8_t)((a < 0 || a > 4) ? 0 : a);  // unknown actions do not move (environment.py:239)
+  }
+  __syncthreads();  // LDS filled
+  uint32_t vwall = 0;  // lane r < R: bit c = stop byte of tile (r, c) (a wall)
+  if (lane < R_)
+    for (int c = 0; c < C_; ++c) vwall |= (uint32_t)wall[OFF0 + lane * PC + c] << c;
+
+  // HBM data a tick needs -- its shared fan entry (FanTick: the unique directions' sample
+  // tiles, n_uniq, n_tie) and its cached guards' cone entries -- comes by LDS-DMA issued a
+  // tick ahead: the fan entry once the tick has marched its own (the staging is then free),
+  // a cone entry once the guard's move is known (the pose after the next move; a finishing
+  // env re-issues it for its reset pose; double-buffered by tick parity).  The tick's stores
+  // go last, so the next tick's counted wait for the DMA (kLeanStores younger operations)
+  // never waits for a store to reach memory.
+  auto dma_fan = [&](int k, bool wide) {  // k < K
+    const FanTick* f = fan0 + k;
+    lds_dma16(f->off4 + lane, stg_a + (uint32_t)offsetof(LeanStage, off4));
+    if (wide) lds_dma16(f->off4 + 64 + lane, stg_a + (uint32_t)offsetof(LeanStage, off4) + 1024u);
+    lds_dma16(f->off2 + 2 * lane, stg_a + (uint32_t)offsetof(LeanStage, off2));
+    if (lane == 0) lds_dma16(&f->num_rays, stg_a + (uint32_t)offsetof(LeanStage, hdr));
+  };
+  // the cone entry (rows 0-15, 32 B) of cached guard g at (idx, slot) into cone staging
+  // `par`: lane mc + g writes at the base it is given minus 16 mc
+  auto dma_cone = [&](int idx, int slot, int par) {
+    if (cached) {
+      const uint16_t* src = eb.cones + cone_off((uint32_t)g, (uint32_t)idx, (uint32_t)slot);
+      const uint32_t dst = stc_a + (uint32_t)(par * 32 * mg) - 16u * (uint32_t)mc;
+      lds_dma16(src, dst);
+      lds_dma16(src + 8, dst + 16u * (uint32_t)mg);
+    }
+  };
+  // the entry of the pose after a move from the guard's current one (idx + step, nslot)
+  auto dma_next_cone = [&](int par) {
+    int idx = gd.idx(), slot = gd.hslot();
+    if (gd.len() >= 2) {
+      idx += gd.step();
+      if (idx >= gd.len()) idx -= gd.len();
+      slot = (int)gd.nslot;
+    }
+    dma_cone(idx, slot, par);
+  };
+  dma_next_cone(0);
+  dma_fan(0, true);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // the cached guards' cone rows (staging parity par) ORed into the plane: lane 15 i + j
+  // takes row j of guard slot 4 pass + i; bit dc + 7 of row dr + 7 is tile (gr + dr, gc + dc);
+  // the aligned dwords a row spans get its bits as 0/1 bytes (ds_or_b32)
+  const uint64_t cmask = __ballot(cached);
+  auto stamp_cones = [&](int par) {
+    const uint32_t gposv = gd.pos();
+    for (int pass = 0; pass * 4 < mg; ++pass) {
+      const int i = lane / 15, j = lane - 15 * i;
+      const int gs = 4 * pass + i;
+      const uint32_t gp = (uint32_t)__shfl((int)gposv, mc + (gs < mg ? gs : 0), 64);
+      if (lane < 60 && gs < mg && ((cmask >> (mc + gs)) & 1u)) {
+        const uint32_t bits = L.cone[par * 16 * mg + (j >> 3) * 8 * mg + 8 * gs + (j & 7)] & 0x7fffu;
+        if (bits) {
+          const uint32_t a0 = base + D + OFF0 + (unpack_r((uint16_t)gp) + j - kConeRange) * PC +
+                              (unpack_c((uint16_t)gp) - kConeRange);
+          const uint32_t m = bits << (a0 & 3u);
+          const uint32_t a = a0 & ~3u;
+#pragma unroll
+          for (int w = 0; w < 5; ++w) {
+            const uint32_t nib = (m >> (4 * w)) & 15u;
+            if (nib)
+              __hip_atomic_fetch_or(reinterpret_cast<__attribute__((address_space(3))) uint32_t*>(a + 4 * w),
+                                    __umul24(nib, 0x204081u) & 0x01010101u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+        }
+      }
+    }
+  };
+  // one fast-path march: this lane's unique direction from the camera whose corner tile
+  // (row - 6, col - 6) is at LDS address `corner`; all 12 stop bytes read before any is used,
+  // a running stop flag (and the own tile, only reachable by samples 1 and 2) sends a
+  // sample's visibility store to the sink plane (march_fast)
+  auto march = [&](uint32_t corner, uint4 o4, uint2 o2) {
+    const uint32_t ow[6] = {o4.x, o4.y, o4.z, o4.w, o2.x, o2.y};
+    uint32_t a[12], w[12];
+#pragma unroll
+    for (int u = 0; u < 12; ++u) a[u] = corner + ((u & 1) ? (ow[u >> 1] >> 16) : (ow[u >> 1] & 0xffffu));
+#pragma unroll
+    for (int u = 0; u < 12; ++u) w[u] = lds_ld(a[u]);
+    const uint32_t own0 = (ow[0] & 0xffffu) == (uint32_t)OFF0, own1 = (ow[0] >> 16) == (uint32_t)OFF0;
+    uint32_t stop = 0;
+#pragma unroll
+    for (int u = 0; u < 12; ++u) {
+      stop = u == 0 ? w[0] : or_b32(stop, w[u]);
+      const uint32_t skip = u == 0 ? or_b32(stop, own0) : (u == 1 ? or_b32(stop, own1) : stop);
+      lds_st(__umul24(skip, (uint32_t)D) + a[u] + D, 1);
+    }
+  };
+  // this tick's visibility into the cleared plane: every camera marches the shared fan's
+  // unique directions -- from the staging, or (the reset pass, after the next tick's DMA
+  // took the staging) from the table -- with the table's near-tie rays on the exact path,
+  // then the cached cones
+  auto cast = [&](int k, int n_uniq, int n_tie, int par, bool staged, bool staged_wide) {
+    reinterpret_cast<uint4*>(vis)[lane] = make_uint4(0u, 0u, 0u, 0u);  // 64 x 16 B = the plane
+    if (s.n_cams > 0) {
+      const FanTick* f = fan0 + k;
+      uint4 o4a = make_uint4(0u, 0u, 0u, 0u), o4b = o4a;
+      uint2 o2a = make_uint2(0u, 0u), o2b = o2a;
+      const bool want_b = n_uniq > 64;
+      if (staged) {
+        o4a = L.stg->off4[lane];
+        o2a = L.stg->off2[lane];
+        if (want_b && staged_wide) {
+          o4b = L.stg->off4[64 + lane];
+          o2b = L.stg->off2[64 + lane];
+        }
+      }
+      if (!staged || (want_b && !staged_wide)) {  // from the table (rare): waited for here, not after the join
+        if (!staged) {
+          o4a = f->off4[lane];
+          o2a = f->off2[lane];
+        }
+        if (want_b) {
+          o4b = f->off4[64 + lane];
+          o2b = f->off2[64 + lane];
+        }
+        asm volatile("" ::"v"(__builtin_bit_cast(u32x4_t, o4a)), "v"(__builtin_bit_cast(u32x2_t, o2a)),
+                     "v"(__builtin_bit_cast(u32x4_t, o4b)), "v"(__builtin_bit_cast(u32x2_t, o2b)));
+      }
+      for (int m = 0; m < s.n_cams; ++m) {
+        const uint32_t rcm = (uint32_t)__builtin_amdgcn_readlane((int)cam_rc, m);
+        const uint32_t corner = base + (rcm & 0xffu) * PC + (rcm >> 8);
+        if (lane < n_uniq) march(corner, o4a, o2a);
+        if (lane + 64 < n_uniq) march(corner, o4b, o2b);
+        for (int c0 = 128; c0 < n_uniq; c0 += 64)  // fans wider than 128 unique directions (fov > ~150)
+          if (lane + c0 < n_uniq) march(corner, f->off4[lane + c0], f->off2[lane + c0]);
+      }
+      if (n_tie > 0) lean_tie_rays<D, PC>(smem, f, n_tie, cam_rc, s.n_cams, p.half_deg);
+    }
+    stamp_cones(par);
+  };
+
+  constexpr uint32_t kOOB = 0x40000000u;  // a store offset past every buffer descriptor below
+  uint32_t vact = 0;  // lane j: the action of tick 64 c + j (the current 64-tick chunk)
+  bool wide = true;   // the DMA staged directions 64 .. 127 for this tick
+  for (int k = 0; k < K; ++k) {
+    const int par = k & 1;
+    if ((k & 63) == 0) vact = k + lane < K ? L.act[k + lane] : 0u;
+    // the DMA issued a tick ago (older than the previous tick's kLeanStores stores) has landed
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLeanStores) : "memory");
+    const int n_uniq = __builtin_amdgcn_readfirstlane(L.stg->hdr[2]);
+    const int n_tie = __builtin_amdgcn_readfirstlane(L.stg->hdr[3]);
+    const bool staged_wide = wide;
+    const bool frozen = s.done != 0;  // finished, no auto-reset: environment.py:232-233
+    double reward = 0.0;
+    int status = kAlreadyDone, curr = 0;
+    if (!frozen) {
+      // 1. move (environment.py:239-246) and the reward terms that precede detection (:235, :261-269)
+      const int a = __builtin_amdgcn_readlane((int)vact, k & 63);
+      const int nr = s.pos_r + (a == 1 ? -1 : (a == 2 ? 1 : 0)), nc = s.pos_c + (a == 3 ? -1 : (a == 4 ? 1 : 0));
+      if (nr >= 0 && nr < R_ && nc >= 0 && nc < C_ && !((__builtin_amdgcn_readlane((int)vwall, nr) >> nc) & 1)) {
+        s.pos_r = nr;
+        s.pos_c = nc;
+      }
+      status = kRunning;
+      curr = iabs_(s.pos_r - p.vr) + iabs_(s.pos_c - p.vc);
+      reward = p.r_step;
+      reward += (double)(s.prev_dist - curr) * 0.1;
+      if (curr <= 3 && s.initial_dist > 3) reward += 0.05 * (double)(3 - curr);
+      s.prev_dist = curr;
+      // 2. cameras rotate, guards patrol (security.py:49-51, :145-159; every live guard is
+      // cached here: its heading is its slot's)
+      if (live_cam) heading = py_mod360(heading + speed * 1.0);
+      if (live_guard && gd.len() >= 2) {
+        int nidx = gd.idx() + gd.step();
+        if (nidx >= gd.len()) nidx -= gd.len();
+        const uint32_t np = L.path[__umul24((uint32_t)g, (uint32_t)mp) + (uint32_t)nidx];
+        gd.a = (uint32_t)nidx | (gd.a & 0x00ffff00u) | (gd.nslot << 24);
+        gd.b = np | (gd.b & 0xffff0000u);
+      }
+      // the slot after the guard's next move: row 15 of this tick's entry (staged a tick ago)
+      if (cached) gd.nslot = L.cone[par * 16 * mg + 8 * mg + 8 * g + 7];
+      if (k + 1 < K) dma_next_cone(par ^ 1);  // tick k + 1's entry if the env still acts then
+      // 3. visibility (environment.py:257-258)
+      cast(k, n_uniq, n_tie, par, true, staged_wide);
+    }
+    // the staging is free: tick k + 1's fan entry (a frozen env keeps its plane and skips it)
+    if (k + 1 < K && !frozen) dma_fan(k + 1, n_uniq > 64);
+    wide = n_uniq > 64;
+    // the plane's channel-1 quads (also the detection test's byte)
+    uint32_t v1[kObsQ];
+#pragma unroll
+    for (int j = 0; j < kObsQ; ++j) {
+      const int q = lane + 64 * j, qc = q < N4 ? q : N4 - 1, r = qc / C4;
+      v1[j] = *reinterpret_cast<const uint32_t*>(vis + OFF0 + r * PC + 4 * (qc - r * C4));
+    }
+    int done_now = s.done;
+    if (!frozen) {
+      // 4. detection, vault, timeout (environment.py:271-297), in the reference's order
+      const int sol = s.pos_r * C_ + s.pos_c, qs = sol >> 2;
+      const uint32_t qv = (uint32_t)__builtin_amdgcn_readlane((int)((qs >> 6) ? v1[1] : v1[0]), qs & 63);
+      if ((qv >> (8 * (sol & 3))) & 0xffu) {
+        s.detected = 1;
+        reward += p.r_detect;
+        s.done = 1;
+        status = kDetected;
+      }
+      if (s.pos_r == p.vr && s.pos_c == p.vc) {
+        s.vault_reached = 1;
+        reward += p.r_vault;
+        s.done = 1;
+        status = kVaultReached;
+      }
+      s.tick += 1;
+      if (s.tick >= p.max_steps) {
+        s.done = 1;
+        status = kTimeout;
+        double frac = 1.0 - (double)curr / (double)(s.initial_dist > 1 ? s.initial_dist : 1);
+        if (frac < 0.0) frac = 0.0;
+        reward += frac * 2.0;
+      }
+      done_now = s.done;
+    }
+    if (auto_reset && done_now) {
+      // 5. auto-reset (environment.py:183-214): headings kept, guards back to patrol point 0;
+      // this row's observation is the next attempt's first one
+      const bool moved = __ballot(live_guard && gd.pos() != gd.pos0()) != 0ull;
+      reset_solver(p, s);
+      if (live_guard) {
+        gd.a &= ~0xffu;                        // idx 0
+        gd.b = (gd.b & 0xffff0000u) | gd.pos0();  // the patrol start
+      }
+      if (cached) {  // the cone of (patrol point 0, this slot), loaded now: only finishing envs pay for it
+        const uint4* rsrc = reinterpret_cast<const uint4*>(eb.cones + cone_off(g, 0, gd.hslot()));
+        const uint4 ra = rsrc[0], rb = rsrc[1];
+        if (moved) {
+          *reinterpret_cast<uint4*>(L.cone + par * 16 * mg + 8 * g) = ra;
+          *reinterpret_cast<uint4*>(L.cone + par * 16 * mg + 8 * mg + 8 * g) = rb;
+        }
+        gd.nslot = rb.w >> 16;
+      }
+      if (moved) {  // the plane again from the reset poses (the staging holds tick k + 1's fan now)
+        cast(k, n_uniq, n_tie, par, false, false);
+#pragma unroll
+        for (int j = 0; j < kObsQ; ++j) {
+          const int q = lane + 64 * j, qc = q < N4 ? q : N4 - 1, r = qc / C4;
+          v1[j] = *reinterpret_cast<const uint32_t*>(vis + OFF0 + r * PC + 4 * (qc - r * C4));
+        }
+      }
+      if (k + 1 < K) dma_next_cone(par ^ 1);  // tick k + 1's entry from the reset pose
+    }
+    // 6. tick k's stores (kLeanStores, unconditional; lanes with nothing to store pass an
+    // offset past their buffer descriptor, which the hardware drops): observation channels
+    // 0, 1, 2, the solver's quad of channel 2 again (same lane, program order: it lands
+    // last), reward, reward64, done, status
+    asm volatile("" ::: "memory");
+    float* o = obs + ((size_t)k * N + e) * 3 * RC;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(o, (short)0, 12 * RC, 0x00020000);
+    const int sol = s.pos_r * C_ + s.pos_c, qs = sol >> 2;
+    const int vault = p.vr * C_ + p.vc;
+#pragma unroll
+    for (int j = 0; j < kObsQ; ++j) {
+      const int q = lane + 64 * j;
+      const bool in = q < N4;
+      const int qc = in ? q : N4 - 1;
+      const uint32_t b = *reinterpret_cast<const uint32_t*>(L.grid + 4 * qc);
+      // float32(tile) / 5 == float32(tile) * 0.2f for every tile type (environment.py:319)
+      obs_put(rs, 2, in ? 16 * q : (int)kOOB,
+              make_float4((float)(b & 0xff) * 0.2f, (float)((b >> 8) & 0xff) * 0.2f,
+                          (float)((b >> 16) & 0xff) * 0.2f, (float)(b >> 24) * 0.2f));
+      const uint32_t v = v1[j];
+      obs_put(rs, 2, in ? 16 * (N4 + q) : (int)kOOB,
+              make_float4((float)(v & 0xff), (float)((v >> 8) & 0xff), (float)((v >> 16) & 0xff), (float)(v >> 24)));
+      float4 c2 = L.plane2[qc];
+      obs_put(rs, 2, in ? 16 * (2 * N4 + q) : (int)kOOB, c2);
+      if (j == (qs >> 6)) {
+        // the solver's cell of channel 2 is fl32(1 + g) for its static value g (heist_create's
+        // second plane), unless it is the vault, whose value wins
+        const int m = sol & 3;
+        const float g0 = m == 0 ? c2.x : (m == 1 ? c2.y : (m == 2 ? c2.z : c2.w));
+        if (sol != vault) patch4(c2, m, 1.0f + g0);
+        obs_put(rs, 2, (qs & 63) == lane ? 16 * (2 * N4 + qs) : (int)kOOB, c2);
+      }
+    }
+    const uint32_t ko = (uint32_t)((size_t)k * N + e);
+    const int l0 = lane == 0 ? 0 : (int)kOOB;
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, (float)reward),
+                                          __builtin_amdgcn_make_buffer_rsrc(rew + ko, (short)0, 4, 0x00020000), l0, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, __builtin_bit_cast(uint64_t, reward)),
+                                          __builtin_amdgcn_make_buffer_rsrc(rew64 ? rew64 + ko : rew64, (short)0,
+                                                                            rew64 ? 8 : 0, 0x00020000),
+                                          l0, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)done_now,
+                                         __builtin_amdgcn_make_buffer_rsrc(done_out + ko, (short)0, 1, 0x00020000), l0,
+                                         0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(int8_t)status,
+                                         __builtin_amdgcn_make_buffer_rsrc(status_out + ko, (short)0, 1, 0x00020000),
+                                         l0, 0, 0);
+  }
+  // epilogue: the state the next launch (or heist_export) starts from
+  if (lane == 0) p.scal[e] = s;
+  if (live_cam) eb.cams[(uint32_t)lane].heading = heading;
+  if (live_guard) {
+    // the heading its slot names (u16 16..19 of any entry with that slot)
+    const uint4 c2 = reinterpret_cast<const uint4*>(eb.cones + cone_off(g, gd.idx(), gd.hslot()))[2];
+    Guard* gp = eb.guards + (uint32_t)g;
+    gp->heading = __builtin_bit_cast(double, ((uint64_t)c2.y << 32) | c2.x);
+    gp->idx = (int16_t)gd.idx();
+    gp->pos = (uint16_t)gd.pos();
+    gp->hslot = (uint8_t)gd.hslot();
+    gp->nslot = (uint8_t)gd.nslot;
   }
 }
 
@@ -2697,6 +3267,14 @@ hipError_t launch_step_multi(const EnvParams& p, int K, const int64_t* actions, 
     HEIST_PROBE_CASE(2, 8, 1) HEIST_PROBE_CASE(2, 8, 2) HEIST_PROBE_CASE(2, 8, 3) HEIST_PROBE_CASE(2, 8, 4)
     HEIST_PROBE_CASE(1, 4, 1) HEIST_PROBE_CASE(1, 4, 2) HEIST_PROBE_CASE(1, 4, 3) HEIST_PROBE_CASE(1, 4, 4)
 #undef HEIST_PROBE_CASE
+    return hipGetLastError();
+  }
+  // the lean one-wave kernel (step_lean_kernel): the default for 20 x 20 grids at one wave per env
+  if (p.lean && p.multi_waves == 1 && p.R == 20 && p.C == 20 && p.vis_gap == 1024 && p.probe_mode == 0 && !p.stamps &&
+      !p.sample_counter && !p.redo_counter && p.max_cams + p.max_guards <= kMaxEmitters) {
+    if (p.fan_on && p.fan_fill) hipLaunchKernelGGL(fan_kernel, dim3(kFanTicks), dim3(kFanRays), 0, st, p);
+    hipLaunchKernelGGL((step_lean_kernel<20, 20>), dim3(p.n_envs), dim3(64), lean_lds_bytes(p, K), st, p, K, actions,
+                       obs, rew, rew64, done_out, status_out, auto_reset);
     return hipGetLastError();
   }
 #define HEIST_MULTI_CASE(W, U, O, D)                                                                        \

@@ -45,6 +45,14 @@ def log(msg):
     print("[bench %s] %s" % (time.strftime("%H:%M:%S"), msg), file=sys.stderr, flush=True)
 
 
+def multi_kernel_name(kcfg, R, C):
+    """The K-tick launch's kernel: the lean one-wave kernel for 20 x 20 grids at one wave per env
+    (heist_env.hip step_lean_kernel; envs it cannot serve take the generic body inside the same
+    launch), else step_multi_kernel."""
+    lean = kcfg.get("lean", 0) and kcfg.get("multi_waves") == 1 and R == 20 and C == 20
+    return "heist::step_lean_kernel" if lean else "heist::step_multi_kernel"
+
+
 def algorithmic_bytes_per_env_step(R, C, ncam, nguard):
     """obs f32 write + grid u8 read + action i64 + reward f32 + done + status
     + read and write of the dynamic per-env state (24 + 8*ncam + 12*nguard bytes)."""
@@ -277,11 +285,12 @@ def measure_env_config(dev, R, n, budget, steps=100, warmup=10, K=1, **kw):
     ncam, ngu = float(st["n_cams"].double().mean()), float(st["n_guards"].double().mean())
     b = algorithmic_bytes_per_env_step(R, R, ncam, ngu)
     gbs = b * n / (ms * 1e-3) / 1e9
+    kname = multi_kernel_name(env.kernel_config(), R, R) if K > 1 else "heist::step_kernel"
     env.close()
     return {"value": n / (ms * 1e-3), "unit": "env-steps/s", "kernel_ms": ms, "envs": n, "grid": "%dx%d" % (R, R),
             "budget": budget, "mean_cameras": ncam, "mean_guards": ngu, "ticks_per_launch": K,
             "shared_fan_frac": fan,
-            "kernel": "heist::step_multi_kernel" if K > 1 else "heist::step_kernel",
+            "kernel": kname,
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_env_step": b}}
 
@@ -560,7 +569,7 @@ def main():
                          "fan_fill_ms_per_fill": fan_fill_ms, "fan_fill_ms_per_tick_amortised": fan_ms_tick,
                          "shared_fan_frac": fan_frac,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "heist::step_multi_kernel" if K > 1 else "heist::step_kernel",
+                         "kernel": multi_kernel_name(kcfg, 20, 20) if K > 1 else "heist::step_kernel",
                          "kernel_ms": kern_ms, "kernel_ms_per_launch": kern_ms * K, "launches": launches,
                          "algorithmic_bytes_per_env_step": b_step,
                          "ray_samples_per_env_step": samples_per_step,

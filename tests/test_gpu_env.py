@@ -720,6 +720,62 @@ def test_step_multi_bench_launch_sequence_with_fan_refill(gpu_device):
         assert torch.equal(sa[key], sb[key]), key
 
 
+def _shared_camera_layouts(n, R, budget, seed, fov, speed, heading, **kw):
+    """Synthetic layouts whose cameras all share one (fov, speed, heading), as an Architect
+    batch's do (reference networks.py:283-322): the lean K-tick kernel's fan-served form."""
+    lays = synthetic_layouts(n, R, R, budget, seed=seed, **kw)
+    out = []
+    for walls, cams, guards in lays:
+        cams = [dict(c, fov_angle=fov, rotation_speed=speed, heading=heading) for c in cams]
+        out.append((walls, cams, guards))
+    return out
+
+
+@pytest.mark.parametrize("auto_reset", [True, False], ids=["auto_reset", "no_reset"])
+@pytest.mark.parametrize("fov", [120.0, 126.5, 33.25], ids=["fov120", "fov126", "fov33"])
+def test_step_lean_wide_fans_and_many_guards(gpu_device, monkeypatch, fov, auto_reset):
+    """The lean one-wave K-tick kernel (step_lean_kernel) on shared-camera layouts with wide
+    fans (more than 64 unique directions: the second staged chunk, and the chunk the
+    previous tick did not stage), budget 40 (up to 13 cameras, 8 guards: two cone-stamp
+    passes), short episodes, launches of 1, 63, 70 and 66 ticks (the 64-tick action chunk
+    and the table's refill) == single ticks and == the generic K-tick body (HEIST_LEAN=0),
+    bit for bit."""
+    n, R, budget = 512, 20, 40
+    cfg = EnvironmentConfig(max_steps=30, architect_budget=budget)
+    f32 = lambda x: float(np.float32(x))  # noqa: E731
+    lays = _shared_camera_layouts(n, R, budget, 77, f32(fov), f32(23.7), f32(301.3))
+    envs = []
+    monkeypatch.setenv("HEIST_MULTI_WAVES", "1")  # one wave per env at n = 512, as at the bench's 4,096
+    for lean in ("1", "0", "1"):
+        monkeypatch.setenv("HEIST_LEAN", lean)
+        env = HeistEnv(n, cfg, max_cams=13, max_guards=8, max_path=16, device=gpu_device)
+        monkeypatch.delenv("HEIST_LEAN")
+        v = env.set_layouts(lays, budget=budget)
+        env.reset()
+        envs.append((env, v))
+    (a, va), (c, vc), (b, vb) = envs
+    assert torch.equal(va, vb) and torch.equal(va, vc)
+    assert a.kernel_config()["lean"] == 1 and c.kernel_config()["lean"] == 0
+    assert a.kernel_config()["multi_waves"] == 1
+    g = torch.Generator(device="cpu").manual_seed(78)
+    acts = torch.randint(0, 5, (200, n), generator=g).to(gpu_device)
+    k0 = 0
+    for kk in (1, 63, 70, 66):
+        oa = a.step_multi(acts[k0:k0 + kk], auto_reset=auto_reset, reward64=True)
+        oc = c.step_multi(acts[k0:k0 + kk], auto_reset=auto_reset, reward64=True)
+        for x, y in zip(oa, oc):
+            assert torch.equal(x, y), k0
+        for k in range(kk):
+            o, r, d, s = b.step(acts[k0 + k], auto_reset=auto_reset)
+            ctx = "tick %d" % (k0 + k)
+            assert torch.equal(oa[0][k], o), ctx
+            assert torch.equal(oa[4][k], b.reward64) and torch.equal(oa[2][k], d) and torch.equal(oa[3][k], s), ctx
+        k0 += kk
+    sa, sb = a.export(grid=True), b.export(grid=True)
+    for key in sb:
+        assert torch.equal(sa[key], sb[key]), key
+
+
 @pytest.mark.parametrize("waves", [1, 2])
 @pytest.mark.parametrize("cones", [True, False], ids=["guard_cones", "live_guards"])
 def test_step_multi_one_wave_per_env(gpu_device, monkeypatch, cones, waves):

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define HEIST_ABI_VERSION 2  /* 2: heist_step_stamps takes the buffer size; heist_stamp_words */
+#define HEIST_ABI_VERSION 3  /* 2: heist_step_stamps takes the buffer size; heist_stamp_words; 3: heist_arch_update_* */
 #define HEIST_EINVAL 100000
 
 /* status_out codes of heist_step (environment.py:236-297 info["status"]). */
@@ -204,6 +204,41 @@ int heist_architect_decode(const int64_t* asset_map, int n, int rows, int cols, 
  * evaluates them: glibc 2.35's dbl-64 algorithm, bit-exact to the host libm for
  * |x| < 105414350.  x, sin_out, cos_out [n] float64 (parity checks and tooling). */
 int heist_sincos(const double* x, int64_t n, double* sin_out, double* cos_out, heist_stream_t stream);
+
+/* Replaces the Architect's per-layout update cadence (training.py:479-480 / :558-559:
+ * ArchitectAgent.update after every layout with ONE transition, agents/architect.py:91-155)
+ * for k consecutive rewards, as one persistent launch (64 workgroups, one per CU, grid
+ * barriers between phases).  With one transition update i is an Adam step on
+ * value_coeff * (V(s0) - rewards[i])^2, V = ArchitectNetwork's value path (encoder ->
+ * adaptive pool -> fc_global -> value_head, networks.py:159-188) on the constant grid s0,
+ * after clip_grad_norm_(max_norm) over the 12 value-path tensors.
+ *   params / exp_avg / exp_avg_sq: HOST arrays of 12 device pointers each, in
+ *     ArchitectNetwork.parameters() order restricted to the value path: encoder.0.weight
+ *     [32][1][3][3], encoder.0.bias, encoder.2.weight [64][32][3][3], encoder.2.bias,
+ *     encoder.4.weight [64][64][3][3], encoder.4.bias, fc_global.weight [256][1024],
+ *     fc_global.bias, value_head.0.weight [128][256], value_head.0.bias,
+ *     value_head.2.weight [1][128], value_head.2.bias; float32, contiguous; the weights of
+ *     encoder.2 / encoder.4 / value_head.0 128-byte aligned.  Updated in place.
+ *   grid [rows][cols] float32 = s0;  rewards [k] float32;  value_loss [k] float32 out
+ *     (mse of each step, before its update).
+ *   step = Adam's step count of these tensors before the first update (torch keeps one per
+ *     tensor; they must agree); lr, beta1, beta2, eps as torch.optim.Adam (amsgrad,
+ *     weight_decay, maximize off; the foreach arithmetic, bias corrections in float64).
+ *   workspace: heist_arch_update_workspace_bytes() device bytes, not shared by launches in
+ *     flight.  rows x cols in {8, 12, 16, 20} squared (heist_arch_update_supported). */
+int64_t heist_arch_update_workspace_bytes(void);
+int heist_arch_update_supported(int rows, int cols);
+int heist_arch_update_sequence(float* const* params, float* const* exp_avg, float* const* exp_avg_sq,
+                               const float* grid, int rows, int cols, const float* rewards, int k, double step,
+                               double lr, double beta1, double beta2, double eps, double max_norm,
+                               double value_coeff, float* value_loss, void* workspace, heist_stream_t stream);
+/* 1 in *timed_out if a grid barrier of the last launch on `workspace` gave up waiting
+ * (workgroups not co-resident; its results are then invalid).  Synchronises `stream`. */
+int heist_arch_update_timed_out(const void* workspace, int* timed_out, heist_stream_t stream);
+/* Instrumentation, no reference counterpart: with buf a device array of 2 * 16 * 32 uint64,
+ * later heist_arch_update_sequence launches record s_memrealtime (100 MHz) at up to 32 phase points
+ * of steps 0..15 in workgroups 0 and 63 (tools/probe_arch_update.py); NULL: off (default). */
+int heist_arch_update_stamps(uint64_t* buf);
 
 /* Replaces SolverAgent._compute_gae + returns (agents/solver.py:142-143, :228-244) on a
  * [T][N] rollout (column e = env e's concatenated episodes).  dones [T][N] uint8.

@@ -17,7 +17,7 @@ INCLUDE = os.path.join(REPO_ROOT, "include")
 LIB_PATH = os.environ.get("HEIST_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libheist_hip.so")
 BUILD_DIR = os.path.join(PKG_ROOT, "build")
 ARCH = os.environ.get("HEIST_OFFLOAD_ARCH", "gfx950")
-SOURCES = ["heist_env.hip", "heist_arch.hip", "heist_ppo.hip", "heist_policy.hip", "heist_capi.hip"]
+SOURCES = ["heist_env.hip", "heist_arch.hip", "heist_arch_update.hip", "heist_ppo.hip", "heist_policy.hip", "heist_capi.hip"]
 HEADERS = ["heist_device.h", "heist_trig.h", "heist_sincos_table.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # heist_env.hip: no SLP vectorization -- ROCm 7.2 clang miscompiles the packed-fp32
@@ -29,7 +29,10 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # single-tick step kernel drops from 64 VGPRs + 3 spilled to 53 with none.
 # HEIST_ENV_FLAGS replaces this list (A/B builds).
 FILE_FLAGS = {"heist_env.hip": os.environ.get("HEIST_ENV_FLAGS", "-fno-slp-vectorize -mllvm -disable-machine-licm").split(),
-              "heist_policy.hip": os.environ.get("HEIST_POLICY_FLAGS", "").split()}  # A/B builds of the policy kernels
+              "heist_policy.hip": os.environ.get("HEIST_POLICY_FLAGS", "").split(),  # A/B builds of the policy kernels
+              # the persistent Architect update: machine LICM would keep loop-invariant scalars of
+              # every phase live across the whole step loop (SGPR spills 267 -> 132 without it)
+              "heist_arch_update.hip": ["-mllvm", "-disable-machine-licm"]}
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function",
           "--offload-arch=" + ARCH, "-I", INCLUDE, "-I", CSRC]
 

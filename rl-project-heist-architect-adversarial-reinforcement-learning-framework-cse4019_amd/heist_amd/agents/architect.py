@@ -178,10 +178,13 @@ class ArchitectAgent:  # agents/architect.py:16-170
         training.py:479-480 / :558-559).  With one reward the value target is the raw
         reward and the policy term is a constant, so update i is one Adam step on
         value_coeff * (V(s0) - r_i)^2 (V on the constant grid state, grad-norm clipped to
-        0.5).  On a HIP device the step is captured once in a HIP graph (forward, backward,
-        clip, capturable Adam, the reward index advanced on the device) and replayed k
-        times with no host synchronisation; the first steps run eagerly as the capture's
-        warm-up.  Returns update()'s metrics for the last transition."""
+        0.5).  On a HIP device all k steps run as ONE persistent kernel
+        (heist_arch_update_sequence: forward, fp32 backward, clip and Adam per step with the
+        weights and moments on chip).  HEIST_ARCH_UPDATE=graph (A/B) or a grid size the
+        kernel is not compiled for takes the HIP-graph path instead: the step captured once
+        (forward, backward, clip, capturable Adam, the reward index advanced on the device)
+        and replayed k times, the first steps eager as the capture's warm-up.  Returns
+        update()'s metrics for the last transition."""
         k = int(rewards.numel())
         if k == 0:
             return {"architect_loss": 0.0}
@@ -190,18 +193,87 @@ class ArchitectAgent:  # agents/architect.py:16-170
         lp = log_probs.to(device=d, dtype=torch.float32).reshape(-1)
         v = values.to(device=d, dtype=torch.float32).reshape(-1)
         self.network.train()
-        n_eager = k if d.type != "cuda" or k < 8 else 3
-        vlast = None
-        for i in range(n_eager):
-            vlast = self._value_step(r32[i])
-        if n_eager < k:
-            vl = self._replay_steps(r32[n_eager:])
-            vlast = vl[-1]
+        if self._kernel_ok():
+            vlast = self._kernel_steps(r32)[-1]
+        else:
+            n_eager = k if d.type != "cuda" or k < 8 else 3
+            vlast = None
+            for i in range(n_eager):
+                vlast = self._value_step(r32[i])
+            if n_eager < k:
+                vl = self._replay_steps(r32[n_eager:])
+                vlast = vl[-1]
         policy_loss = -(lp[k - 1] * (r32[k - 1] - v[k - 1]))
         total = policy_loss + self.value_coeff * vlast
         return {"architect_policy_loss": float(policy_loss), "architect_value_loss": float(vlast),
                 "architect_total_loss": float(total), "architect_layouts": 1,
                 "architect_avg_reward": self.total_reward / max(self.episode_count, 1)}
+
+    def value_parameters(self) -> List[torch.Tensor]:
+        """The 12 tensors the value loss reaches (encoder, fc_global, value_head), in
+        parameters() order: the ones update() steps (the decoder and camera heads get no
+        gradient, so Adam skips them)."""
+        n = self.network
+        return [n.encoder[0].weight, n.encoder[0].bias, n.encoder[2].weight, n.encoder[2].bias, n.encoder[4].weight,
+                n.encoder[4].bias, n.fc_global.weight, n.fc_global.bias, n.value_head[0].weight, n.value_head[0].bias,
+                n.value_head[2].weight, n.value_head[2].bias]
+
+    def _kernel_ok(self) -> bool:
+        """The persistent update kernel applies: a HIP device, a compiled grid size, the
+        default Adam configuration (one group, no weight decay / amsgrad / maximize), equal
+        step counts on the value tensors, 128-byte aligned weights."""
+        if self.device.type != "cuda" or os.environ.get("HEIST_ARCH_UPDATE", "kernel") != "kernel":
+            return False
+        from .. import _native
+        if not _native.lib().heist_arch_update_supported(self.grid_rows, self.grid_cols):
+            return False
+        if len(self.optimizer.param_groups) != 1:
+            return False
+        grp = self.optimizer.param_groups[0]
+        if grp.get("weight_decay", 0) != 0 or grp.get("amsgrad") or grp.get("maximize") or grp.get("differentiable"):
+            return False
+        ps = self.value_parameters()
+        if any(p.data_ptr() % 128 for p in (ps[2], ps[4], ps[8])) or not all(p.is_contiguous() for p in ps):
+            return False
+        steps = {float(self.optimizer.state[p]["step"]) for p in ps if "step" in self.optimizer.state[p]}
+        return len(steps) <= 1 and (not steps or all("step" in self.optimizer.state[p] for p in ps))
+
+    def _kernel_steps(self, r32: torch.Tensor) -> torch.Tensor:
+        """value steps for every reward of r32 [k] in one heist_arch_update_sequence launch;
+        returns the k value losses.  Adam's state is created as torch does on a first step
+        (zero moments, step 0) and its step counters advance by k."""
+        from .. import _native
+        d = self.device
+        k = int(r32.numel())
+        ps = self.value_parameters()
+        grp = self.optimizer.param_groups[0]
+        for p in ps:
+            st = self.optimizer.state[p]
+            if "step" not in st:
+                st["step"] = (torch.zeros((), dtype=torch.float32, device=d) if grp.get("capturable")
+                              else torch.tensor(0.0, dtype=torch.float32))
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        step0 = float(self.optimizer.state[ps[0]]["step"])
+        ws = getattr(self, "_au_ws", None)
+        nb = int(_native.lib().heist_arch_update_workspace_bytes())
+        if ws is None or ws.device != d:
+            ws = self._au_ws = torch.empty((nb + 3) // 4, dtype=torch.float32, device=d)
+        vl = torch.empty(k, dtype=torch.float32, device=d)
+        r = r32.to(device=d, dtype=torch.float32).contiguous()
+        grid = self.grid_state().contiguous()
+        arr = lambda ts: (_native._vp * 12)(*[t.data_ptr() for t in ts])  # noqa: E731
+        self.optimizer.zero_grad(set_to_none=True)
+        beta1, beta2 = grp["betas"]
+        _native.check(_native.lib().heist_arch_update_sequence(
+            arr(ps), arr([self.optimizer.state[p]["exp_avg"] for p in ps]),
+            arr([self.optimizer.state[p]["exp_avg_sq"] for p in ps]), _native.ptr(grid), self.grid_rows,
+            self.grid_cols, _native.ptr(r), k, step0, float(grp["lr"]), float(beta1), float(beta2), float(grp["eps"]),
+            0.5, float(self.value_coeff), _native.ptr(vl), _native.ptr(ws), _native.stream(d)),
+            "heist_arch_update_sequence")
+        for p in ps:
+            self.optimizer.state[p]["step"].add_(float(k))
+        return vl
 
     def _value_step(self, r: torch.Tensor) -> torch.Tensor:
         """One eager single-reward step (update() with len(rewards) == 1); returns the value loss."""

@@ -10,6 +10,8 @@ different device and library); parameters whose gradient is cancellation noise (
 noise, get only Adam's lr bound on their step.  kat.json's architect_reward table pins
 calculate_architect_reward (rewards.py:43-73).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -121,8 +123,11 @@ def test_architect_update_sequence_cpu():
 
 
 @pytest.mark.gpu
-def test_architect_update_sequence_gpu_graph(gpu_device):
-    # 40: the first capture (1,024 slots); 5: eager only; 1500: past the slots, captured again
+@pytest.mark.parametrize("mode", ["kernel", "graph"])
+def test_architect_update_sequence_gpu(gpu_device, monkeypatch, mode):
+    # kernel: one persistent launch per sequence; graph: 40 = the first capture (1,024
+    # slots), 5 = eager only, 1500 = past the slots, captured again
+    monkeypatch.setenv("HEIST_ARCH_UPDATE", mode)
     _sequence_vs_updates(gpu_device, ks=(40, 5, 1500))
 
 
@@ -162,3 +167,132 @@ def test_architect_checkpoint_after_sequence_cpu(tmp_path):
 @pytest.mark.gpu
 def test_architect_checkpoint_after_sequence_gpu(gpu_device, tmp_path):
     _checkpoint_after_sequence_loads_on_cpu(gpu_device, tmp_path)
+
+
+def _single_transition_runs(z):
+    """(case, [update indices]) of arch_update.npz's leading single-transition updates: the
+    ones the per-layout cadence produces (update() with one reward)."""
+    out = []
+    for ci in range(int(z["n_cases"])):
+        us = []
+        for ui in range(int(z["c%d_n" % ci])):
+            if len(z["c%d_u%d_r" % (ci, ui)]) != 1:
+                break
+            us.append(ui)
+        if us:
+            out.append((ci, us))
+    return out
+
+
+@pytest.mark.gpu
+def test_architect_update_kernel_golden(gpu_device, monkeypatch):
+    """The persistent update kernel (heist_arch_update_sequence, via update_sequence) on
+    arch_update.npz's single-transition updates, run by the Python reference from the
+    nets.npz weights: losses to 1e-4, each update's parameter step (norm and fixed random
+    projections) to 1e-3 of its size, as the eager path is held (_check_cases).  Case 3's
+    two consecutive updates also run as ONE k = 2 launch, equal to the two k = 1 launches."""
+    monkeypatch.setenv("HEIST_ARCH_UPDATE", "kernel")
+    z = gd.load("arch_update.npz")
+    n_sd = gd.load("nets.npz")
+    sd = {k[len("architect/"):]: torch.from_numpy(n_sd[k]) for k in n_sd.files if k.startswith("architect/")}
+    runs = _single_transition_runs(z)
+    assert [ci for ci, _ in runs] == [0, 1, 3] and runs[-1][1] == [0, 1]
+    for ci, us in runs:
+        ag = ArchitectAgent(grid_rows=20, grid_cols=20, budget=15, device=gpu_device)
+        ag.network.load_state_dict(sd)
+        assert ag._kernel_ok()
+        for ui in us:
+            key = "c%d_u%d_" % (ci, ui)
+            p0 = [p.detach().clone() for p in ag.network.parameters()]
+            lp, v, r = (torch.tensor(np.asarray(z[key + x], dtype=np.float64).reshape(-1)) for x in ("lp", "v", "r"))
+            ag.store_rewards([float(r[0])])
+            m = ag.update_sequence(lp, v, r)
+            got = [m["architect_policy_loss"], m["architect_value_loss"], m["architect_total_loss"]]
+            np.testing.assert_allclose(got, z[key + "loss"], rtol=1e-4, atol=1e-4, err_msg=key)
+            gmax = float(np.max(z[key + "gnorm"]))
+            for i, (p, q) in enumerate(zip(ag.network.parameters(), p0)):
+                d = (p.detach() - q).double().reshape(-1).cpu().numpy()
+                if float(z[key + "gnorm"][i]) == 0.0:  # decoder / camera heads: no gradient, no step
+                    assert not d.any(), (key, i)
+                    continue
+                if float(z[key + "gnorm"][i]) < 1e-6 * gmax:
+                    assert np.abs(d).max() <= ag.optimizer.param_groups[0]["lr"] * 3.17, (key, i)
+                    continue
+                P = proj_vectors(i, d.size)
+                dscale = max(float(z[key + "dnorm"][i]), 1e-12)
+                np.testing.assert_allclose(np.linalg.norm(d), z[key + "dnorm"][i], rtol=1e-3, atol=1e-9,
+                                           err_msg="%s step norm %d" % (key, i))
+                np.testing.assert_allclose(P @ d, z[key + "dproj"][i], rtol=0, atol=1e-3 * dscale + 1e-9,
+                                           err_msg="%s step proj %d" % (key, i))
+        if ci == 3:  # the same two updates as one launch
+            b = ArchitectAgent(grid_rows=20, grid_cols=20, budget=15, device=gpu_device)
+            b.network.load_state_dict(sd)
+            lp, v, r = (torch.tensor([float(np.asarray(z["c3_u%d_" % u + x]).reshape(-1)[0]) for u in (0, 1)],
+                                     dtype=torch.float64) for x in ("lp", "v", "r"))
+            b.update_sequence(lp, v, r)
+            for (n, p), q in zip(b.network.state_dict().items(), ag.network.state_dict().values()):
+                assert torch.equal(p, q), n
+            for p, q in zip(b.value_parameters(), ag.value_parameters()):
+                for key in ("exp_avg", "exp_avg_sq", "step"):
+                    assert torch.equal(b.optimizer.state[p][key], ag.optimizer.state[q][key]), key
+
+
+@pytest.mark.gpu
+def test_architect_update_long_sequence_drift(gpu_device, monkeypatch):
+    """A full iteration's Architect sequence (3,841 single-reward updates, the count of
+    profiles/r03l_probe_train.log) from the nets.npz weights, through the persistent kernel
+    and through the HIP-graph replay, against the same sequence of eager update() calls
+    (agents/architect.py:91-155).  Rewards come from the table the training loop produces
+    (kat.json architect_reward values and the invalid-layout -1, rewards.py:43-73).
+
+    What holds (measured, profiles/r04h_probe_arch_drift.log): the kernel is bit-for-bit
+    deterministic; over the first 200 updates every parameter stays within 2e-6 of eager
+    (8.7e-7 measured); later, fp32 rounding differences get amplified where Adam meets a
+    unit crossing its ReLU boundary at a different step, a few weights part by up to ~60 lr
+    (0.017) and stay there, while the function the network computes does not drift: V(s0)
+    and the value loss track eager to 1.7e-5 at the end (1.4e-4 worst checkpoint).  The same
+    bounds hold for the graph replay."""
+    n_sd = gd.load("nets.npz")
+    sd = {k[len("architect/"):]: torch.from_numpy(n_sd[k]) for k in n_sd.files if k.startswith("architect/")}
+    table = sorted(set(float(v) for v in gd.load_json("kat.json")["architect_reward"].values())) + [-1.0]
+    g = torch.Generator().manual_seed(31)
+    k, k0 = 3841, 200
+    r = torch.tensor(table, dtype=torch.float64)[torch.randint(0, len(table), (k,), generator=g)]
+    lp, v = torch.randn(k, generator=g, dtype=torch.float64), torch.randn(k, generator=g, dtype=torch.float64)
+
+    def agent():
+        a = ArchitectAgent(grid_rows=20, grid_cols=20, budget=15, device=gpu_device)
+        a.network.load_state_dict(sd)
+        return a
+
+    def vs0(a):
+        with torch.no_grad():
+            return float(a.network.value(a.grid_state()))
+
+    e = agent()
+    e_first = None
+    for i in range(k):
+        e.log_probs, e.values = [torch.tensor(float(lp[i]), device=gpu_device)], [torch.tensor(float(v[i]), device=gpu_device)]
+        e.rewards = [float(r[i])]
+        me = e.update(collective=False)
+        if i == k0 - 1:
+            e_first = [p.detach().clone() for p in e.network.parameters()]
+    for mode in ("kernel", "graph"):
+        monkeypatch.setenv("HEIST_ARCH_UPDATE", mode)
+        ag = agent()
+        ag.update_sequence(lp[:k0], v[:k0], r[:k0])
+        first = max(float((p - q).abs().max()) for p, q in zip(ag.network.parameters(), e_first))
+        m = ag.update_sequence(lp[k0:], v[k0:], r[k0:])
+        worst = max(float((p - q).abs().max()) for p, q in zip(ag.network.parameters(), e.network.parameters()))
+        dv = abs(vs0(ag) - vs0(e))
+        print("%s vs eager: max |param diff| %.3g after %d updates, %.3g after %d; |V(s0) diff| %.3g; value loss %.9g vs %.9g"
+              % (mode, first, k0, worst, k, dv, m["architect_value_loss"], me["architect_value_loss"]))
+        assert first <= 2e-6, (mode, first)
+        assert dv <= 5e-4, (mode, dv)
+        assert abs(m["architect_value_loss"] - me["architect_value_loss"]) <= 5e-4 * max(1.0, me["architect_value_loss"])
+        if mode == "kernel":  # bit-for-bit deterministic
+            b = agent()
+            b.update_sequence(lp[:k0], v[:k0], r[:k0])
+            b.update_sequence(lp[k0:], v[k0:], r[k0:])
+            for p, q in zip(b.network.parameters(), ag.network.parameters()):
+                assert torch.equal(p, q)

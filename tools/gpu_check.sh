@@ -14,6 +14,7 @@ elif [ -z "$NO_PYTEST" ]; then
   run pytest_gpu 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
 fi
 [ -z "$NO_SMOKE" ] && run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-run bench_driver 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
+[ -n "$PROBE" ] && run probe 300 python3 $PROBE
+[ -z "$NO_BENCH" ] && run bench_driver 600 python3 bench.py --gpus 1 --steps 20 --warmup 5
 [ -n "$BENCH_QUICK" ] && run bench_quick 600 python3 bench.py --steps 300 --warmup 30 --no-cpu-baseline --no-secondary
 echo "== all done"

@@ -211,7 +211,8 @@ int heist_sincos(const double* x, int64_t n, double* sin_out, double* cos_out, h
  * barriers between phases).  With one transition update i is an Adam step on
  * value_coeff * (V(s0) - rewards[i])^2, V = ArchitectNetwork's value path (encoder ->
  * adaptive pool -> fc_global -> value_head, networks.py:159-188) on the constant grid s0,
- * after clip_grad_norm_(max_norm) over the 12 value-path tensors.
+ * after clip_grad_norm_(max_norm) over the 12 value-path tensors.  Workgroup w owns conv2 /
+ * conv3 channels 4(w/4)..+3 on pool-cell row band w%4 of the image.
  *   params / exp_avg / exp_avg_sq: HOST arrays of 12 device pointers each, in
  *     ArchitectNetwork.parameters() order restricted to the value path: encoder.0.weight
  *     [32][1][3][3], encoder.0.bias, encoder.2.weight [64][32][3][3], encoder.2.bias,
@@ -219,18 +220,20 @@ int heist_sincos(const double* x, int64_t n, double* sin_out, double* cos_out, h
  *     fc_global.bias, value_head.0.weight [128][256], value_head.0.bias,
  *     value_head.2.weight [1][128], value_head.2.bias; float32, contiguous; the weights of
  *     encoder.2 / encoder.4 / value_head.0 128-byte aligned.  Updated in place.
- *   grid [rows][cols] float32 = s0;  rewards [k] float32;  value_loss [k] float32 out
+ *   grid [rows][cols] float32 = s0 with at most 64 nonzero pixels (the Architect's state
+ *     has 2);  rewards [k] float32;  value_loss [k] float32 out
  *     (mse of each step, before its update).
- *   step = Adam's step count of these tensors before the first update (torch keeps one per
- *     tensor; they must agree); lr, beta1, beta2, eps as torch.optim.Adam (amsgrad,
- *     weight_decay, maximize off; the foreach arithmetic, bias corrections in float64).
+ *   step_scalars [k][2] float32 (device): per update, the two scalars torch.optim.Adam forms
+ *     in float64 from the step count and casts to float: -lr / (1 - beta1^step) and
+ *     sqrt(1 - beta2^step); beta1, beta2, eps as torch.optim.Adam (amsgrad, weight_decay,
+ *     maximize off; the foreach arithmetic).
  *   workspace: heist_arch_update_workspace_bytes() device bytes, not shared by launches in
  *     flight.  rows x cols in {8, 12, 16, 20} squared (heist_arch_update_supported). */
 int64_t heist_arch_update_workspace_bytes(void);
 int heist_arch_update_supported(int rows, int cols);
 int heist_arch_update_sequence(float* const* params, float* const* exp_avg, float* const* exp_avg_sq,
-                               const float* grid, int rows, int cols, const float* rewards, int k, double step,
-                               double lr, double beta1, double beta2, double eps, double max_norm,
+                               const float* grid, int rows, int cols, const float* rewards, int k,
+                               const float* step_scalars, double beta1, double beta2, double eps, double max_norm,
                                double value_coeff, float* value_loss, void* workspace, heist_stream_t stream);
 /* 1 in *timed_out if a grid barrier of the last launch on `workspace` gave up waiting
  * (workgroups not co-resident; its results are then invalid).  Synchronises `stream`. */

@@ -61,7 +61,7 @@ bool arch_update_supported(int R, int C);
 void set_arch_stamps(unsigned long long* p);
 int64_t arch_update_workspace_bytes();
 hipError_t launch_arch_update(float* const* p, float* const* m, float* const* v, const float* grid, int R, int C,
-                              const float* target, int k, float* vloss, void* ws, double step0, double lr, double beta1,
+                              const float* target, int k, const float* adam_sc, float* vloss, void* ws, double beta1,
                               double beta2, double eps, double max_norm, double value_coeff, hipStream_t st);
 hipError_t launch_gae(const float* r, const float* v, const uint8_t* d, const float* last_value, int T, int N,
                       double gamma, double lam, float* adv, float* ret, hipStream_t st);
@@ -568,24 +568,24 @@ int64_t heist_arch_update_workspace_bytes(void) { return heist::arch_update_work
 int heist_arch_update_supported(int rows, int cols) { return heist::arch_update_supported(rows, cols) ? 1 : 0; }
 
 int heist_arch_update_sequence(float* const* params, float* const* exp_avg, float* const* exp_avg_sq,
-                               const float* grid, int rows, int cols, const float* rewards, int k, double step,
-                               double lr, double beta1, double beta2, double eps, double max_norm,
+                               const float* grid, int rows, int cols, const float* rewards, int k,
+                               const float* step_scalars, double beta1, double beta2, double eps, double max_norm,
                                double value_coeff, float* value_loss, void* workspace, heist_stream_t stream) {
   HEIST_REQUIRE(params && exp_avg && exp_avg_sq && grid && workspace, "heist_arch_update_sequence: null pointer");
   HEIST_REQUIRE(heist::arch_update_supported(rows, cols),
                 "heist_arch_update_sequence: rows x cols must be 8x8, 12x12, 16x16 or 20x20");
   HEIST_REQUIRE(k >= 0, "heist_arch_update_sequence: negative k");
   if (k == 0) return 0;
-  HEIST_REQUIRE(rewards && value_loss, "heist_arch_update_sequence: null rewards / value_loss");
+  HEIST_REQUIRE(rewards && value_loss && step_scalars, "heist_arch_update_sequence: null rewards / step_scalars / value_loss");
   for (int i = 0; i < 12; ++i)
     HEIST_REQUIRE(params[i] && exp_avg[i] && exp_avg_sq[i], "heist_arch_update_sequence: null tensor pointer");
   for (int i : {2, 4, 8})  // rows handed between workgroups are stored as whole 128-B lines
     HEIST_REQUIRE(((uintptr_t)params[i] & 127) == 0, "heist_arch_update_sequence: weights must be 128-byte aligned");
   HEIST_REQUIRE(((uintptr_t)workspace & 127) == 0, "heist_arch_update_sequence: workspace must be 128-byte aligned");
-  HEIST_REQUIRE(step >= 0 && lr >= 0 && beta1 >= 0 && beta1 < 1 && beta2 >= 0 && beta2 < 1 && eps >= 0,
+  HEIST_REQUIRE(beta1 >= 0 && beta1 < 1 && beta2 >= 0 && beta2 < 1 && eps >= 0,
                 "heist_arch_update_sequence: bad Adam hyperparameters");
-  return check_hip(heist::launch_arch_update(params, exp_avg, exp_avg_sq, grid, rows, cols, rewards, k, value_loss,
-                                             workspace, step, lr, beta1, beta2, eps, max_norm, value_coeff,
+  return check_hip(heist::launch_arch_update(params, exp_avg, exp_avg_sq, grid, rows, cols, rewards, k, step_scalars,
+                                             value_loss, workspace, beta1, beta2, eps, max_norm, value_coeff,
                                              (hipStream_t)stream),
                    "heist_arch_update_sequence");
 }

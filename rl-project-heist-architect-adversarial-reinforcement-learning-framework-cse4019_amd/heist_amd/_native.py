@@ -51,7 +51,7 @@ SIGNATURES = {
     "heist_arch_update_workspace_bytes": (_i64, []),
     "heist_arch_update_supported": (_i, [_i, _i]),
     "heist_arch_update_sequence": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp, _i, _i,
-                                        _vp, _i, _d, _d, _d, _d, _d, _d, _d, _vp, _vp, _vp]),
+                                        _vp, _i, _vp, _d, _d, _d, _d, _d, _vp, _vp, _vp]),
     "heist_arch_update_timed_out": (_i, [_vp, ctypes.POINTER(_i), _vp]),
     "heist_arch_update_stamps": (_i, [_vp]),
     "heist_gae": (_i, [_vp, _vp, _vp, _vp, _i, _i, _d, _d, _vp, _vp, _vp]),

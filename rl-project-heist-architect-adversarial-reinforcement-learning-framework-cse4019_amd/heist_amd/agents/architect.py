@@ -172,7 +172,20 @@ class ArchitectAgent:  # agents/architect.py:16-170
         self._clear()
         return metrics
 
-    def update_sequence(self, log_probs: torch.Tensor, values: torch.Tensor, rewards: torch.Tensor) -> Dict[str, float]:
+    def side_stream(self):
+        """The stream the training loop runs this agent's deferred update on (None off a HIP device)."""
+        if self.device.type != "cuda":
+            return None
+        st = getattr(self, "_side", None)
+        if st is None:
+            # high priority: the persistent update kernel needs 64 whole CUs (its LDS), and the
+            # dispatcher hands CUs freed by the Solver's short kernels to this queue first
+            lo, hi = torch.cuda.Stream.priority_range()
+            st = self._side = torch.cuda.Stream(device=self.device, priority=min(lo, hi))
+        return st
+
+    def update_sequence(self, log_probs: torch.Tensor, values: torch.Tensor, rewards: torch.Tensor,
+                        defer: bool = False, join=None):
         """k single-transition updates in order: update() called after each layout with one
         (log_prob, value, reward) in its buffer, k times (the reference's cadence,
         training.py:479-480 / :558-559).  With one reward the value target is the raw
@@ -184,16 +197,40 @@ class ArchitectAgent:  # agents/architect.py:16-170
         kernel is not compiled for takes the HIP-graph path instead: the step captured once
         (forward, backward, clip, capturable Adam, the reward index advanced on the device)
         and replayed k times, the first steps eager as the capture's warm-up.  Returns
-        update()'s metrics for the last transition."""
+        update()'s metrics for the last transition.
+
+        defer=True returns instead a callable that produces those metrics, and nothing here
+        waits for the GPU on the kernel path: run it with a side stream current (the training
+        loop uses side_stream()) so other work (the Solver's PPO update) runs beside it; the
+        callable first makes `join` (a stream, e.g. the main one) wait for the launch."""
         k = int(rewards.numel())
         if k == 0:
-            return {"architect_loss": 0.0}
+            m0 = {"architect_loss": 0.0}
+            return (lambda: m0) if defer else m0
         d = self.device
         r32 = rewards.to(device=d, dtype=torch.float32).reshape(-1)
         lp = log_probs.to(device=d, dtype=torch.float32).reshape(-1)
         v = values.to(device=d, dtype=torch.float32).reshape(-1)
         self.network.train()
+
+        def metrics(vlast):
+            policy_loss = -(lp[k - 1] * (r32[k - 1] - v[k - 1]))
+            total = policy_loss + self.value_coeff * vlast
+            return {"architect_policy_loss": float(policy_loss), "architect_value_loss": float(vlast),
+                    "architect_total_loss": float(total), "architect_layouts": 1,
+                    "architect_avg_reward": self.total_reward / max(self.episode_count, 1)}
+
         if self._kernel_ok():
+            if defer:
+                vl = self._kernel_steps(r32)
+                done = torch.cuda.Event()
+                done.record(torch.cuda.current_stream(d))
+
+                def finish():
+                    if join is not None:
+                        join.wait_event(done)
+                    return metrics(vl[-1])
+                return finish
             vlast = self._kernel_steps(r32)[-1]
         else:
             n_eager = k if d.type != "cuda" or k < 8 else 3
@@ -203,11 +240,10 @@ class ArchitectAgent:  # agents/architect.py:16-170
             if n_eager < k:
                 vl = self._replay_steps(r32[n_eager:])
                 vlast = vl[-1]
-        policy_loss = -(lp[k - 1] * (r32[k - 1] - v[k - 1]))
-        total = policy_loss + self.value_coeff * vlast
-        return {"architect_policy_loss": float(policy_loss), "architect_value_loss": float(vlast),
-                "architect_total_loss": float(total), "architect_layouts": 1,
-                "architect_avg_reward": self.total_reward / max(self.episode_count, 1)}
+        m = metrics(vlast)
+        if defer and join is not None and d.type == "cuda":
+            join.wait_stream(torch.cuda.current_stream(d))
+        return (lambda: m) if defer else m
 
     def value_parameters(self) -> List[torch.Tensor]:
         """The 12 tensors the value loss reaches (encoder, fc_global, value_head), in
@@ -235,6 +271,10 @@ class ArchitectAgent:  # agents/architect.py:16-170
         ps = self.value_parameters()
         if any(p.data_ptr() % 128 for p in (ps[2], ps[4], ps[8])) or not all(p.is_contiguous() for p in ps):
             return False
+        if getattr(self, "_grid_nnz", None) is None:
+            self._grid_nnz = int((self.grid_state() != 0).sum())
+        if self._grid_nnz > 64:  # the kernel's conv1 walks the input's nonzeros (the state has 2)
+            return False
         steps = {float(self.optimizer.state[p]["step"]) for p in ps if "step" in self.optimizer.state[p]}
         return len(steps) <= 1 and (not steps or all("step" in self.optimizer.state[p] for p in ps))
 
@@ -255,20 +295,28 @@ class ArchitectAgent:  # agents/architect.py:16-170
                 st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
         step0 = float(self.optimizer.state[ps[0]]["step"])
+        beta1, beta2 = grp["betas"]
+        # the per-step scalars as _multi_tensor_adam forms them: Python floats from the step
+        # count (numpy's float64 power is C pow, as Python's **), then float32
+        steps = step0 + np.arange(1, k + 1, dtype=np.float64)
+        bc1, bc2 = 1.0 - np.power(float(beta1), steps), 1.0 - np.power(float(beta2), steps)
+        sc = torch.from_numpy(np.stack([(float(grp["lr"]) / bc1) * -1.0, np.sqrt(bc2)], axis=1).astype(np.float32))
+        sc = sc.pin_memory().to(d, non_blocking=True)  # pageable copies would wait for an idle device
         ws = getattr(self, "_au_ws", None)
         nb = int(_native.lib().heist_arch_update_workspace_bytes())
         if ws is None or ws.device != d:
             ws = self._au_ws = torch.empty((nb + 3) // 4, dtype=torch.float32, device=d)
         vl = torch.empty(k, dtype=torch.float32, device=d)
         r = r32.to(device=d, dtype=torch.float32).contiguous()
-        grid = self.grid_state().contiguous()
+        grid = getattr(self, "_grid_dev", None)
+        if grid is None or grid.device != d:
+            grid = self._grid_dev = self.grid_state().contiguous()  # the constant input, made once
         arr = lambda ts: (_native._vp * 12)(*[t.data_ptr() for t in ts])  # noqa: E731
         self.optimizer.zero_grad(set_to_none=True)
-        beta1, beta2 = grp["betas"]
         _native.check(_native.lib().heist_arch_update_sequence(
             arr(ps), arr([self.optimizer.state[p]["exp_avg"] for p in ps]),
             arr([self.optimizer.state[p]["exp_avg_sq"] for p in ps]), _native.ptr(grid), self.grid_rows,
-            self.grid_cols, _native.ptr(r), k, step0, float(grp["lr"]), float(beta1), float(beta2), float(grp["eps"]),
+            self.grid_cols, _native.ptr(r), k, _native.ptr(sc), float(beta1), float(beta2), float(grp["eps"]),
             0.5, float(self.value_coeff), _native.ptr(vl), _native.ptr(ws), _native.stream(d)),
             "heist_arch_update_sequence")
         for p in ps:

@@ -150,14 +150,17 @@ class SolverAgent:  # agents/solver.py:18-259
         return m
 
     def _ppo_epochs(self, states, actions, old_logp, adv, ret, n, perm_fn, minibatch=None,
-                    collective: bool = True) -> Dict[str, float]:
+                    collective: bool = True, defer: bool = False):
         """agents/solver.py:157-204: epochs x shuffled minibatches, zero-hidden re-forward.
 
         collective (batched data-parallel training): every rank runs the same number of
         optimizer steps, max over ranks of ceil(n / minibatch) per epoch.  A rank that has
         run out of samples takes part with an empty minibatch (zero gradient, weight 0);
         the one flat all-reduce per step forms the sample-weighted mean gradient, so all
-        ranks clip and step identically and their parameters stay equal."""
+        ranks clip and step identically and their parameters stay equal.
+
+        defer=True returns a callable that produces the metrics: the steps are only enqueued
+        (nothing in the loop waits for the GPU), so the host can do other work meanwhile."""
         self.network.train()
         bs = minibatch or self.batch_size
         tot = torch.zeros(3, device=self.device)
@@ -195,9 +198,11 @@ class SolverAgent:  # agents/solver.py:18-259
                     continue
                 nn.utils.clip_grad_norm_(params, self.max_grad_norm)
                 self.optimizer.step()
-        t = (tot / max(updates, 1)).cpu().numpy()
-        return {"solver_policy_loss": float(t[0]), "solver_value_loss": float(t[1]), "solver_entropy": float(t[2]),
-                "solver_updates": n_mb * self.ppo_epochs}
+        def metrics():
+            t = (tot / max(updates, 1)).cpu().numpy()
+            return {"solver_policy_loss": float(t[0]), "solver_value_loss": float(t[1]), "solver_entropy": float(t[2]),
+                    "solver_updates": n_mb * self.ppo_epochs}
+        return metrics if defer else metrics()
 
     # -- batched API ------------------------------------------------------------------
     @torch.no_grad()
@@ -250,10 +255,23 @@ class SolverAgent:  # agents/solver.py:18-259
         last tick ended an episode masks it (done), as the reference's buffer-end 0 does."""
         return compute_gae(ro.rewards, ro.values, ro.dones, ro.last_value, self.gamma, self.gae_lambda)
 
-    def update_rollout(self, ro: Rollout, minibatch: int = 4096) -> Dict[str, float]:
+    @staticmethod
+    def _finish(m, n, defer):
+        if not defer:
+            m["solver_samples"] = n
+            return m
+
+        def done():
+            out = m()
+            out["solver_samples"] = n
+            return out
+        return done
+
+    def update_rollout(self, ro: Rollout, minibatch: int = 4096, defer: bool = False):
         """One PPO update on a [T, N] rollout (GAE per env column, global advantage norm).
         Collective-safe: with torch.distributed initialised every rank enters the
-        normalisation and the same number of optimizer steps, whatever its sample count."""
+        normalisation and the same number of optimizer steps, whatever its sample count.
+        defer=True: enqueue only, return a callable giving the metrics (_ppo_epochs)."""
         T, N = ro.rewards.shape
         adv, ret = self.rollout_advantages(ro)
         sel = None if ro.mask is None else ro.mask.reshape(1, N).expand(T, N).reshape(-1)
@@ -263,14 +281,14 @@ class SolverAgent:  # agents/solver.py:18-259
             states, actions, old_logp, adv, ret = (x[sel] for x in (states, actions, old_logp, adv, ret))
         n = adv.shape[0]
         if n == 0 and not dist_utils.is_multi():
-            return {"solver_loss": 0.0}
+            m0 = {"solver_loss": 0.0}
+            return (lambda: m0) if defer else m0
         adv = normalize_advantages(adv)
         gen = torch.Generator(device=self.device)
         gen.manual_seed(int(torch.randint(0, 2 ** 31, (1,)).item()))
         perm = lambda k: torch.randperm(k, device=self.device, generator=gen)  # noqa: E731
-        m = self._ppo_epochs(states, actions, old_logp, adv, ret, n, perm, minibatch=minibatch)
-        m["solver_samples"] = n
-        return m
+        m = self._ppo_epochs(states, actions, old_logp, adv, ret, n, perm, minibatch=minibatch, defer=defer)
+        return self._finish(m, n, defer)
 
     def layout_batch_advantages(self, ro: Rollout, sel: torch.Tensor):
         """The reference's per-layout buffer statistics for a layout-batch rollout
@@ -298,7 +316,7 @@ class SolverAgent:  # agents/solver.py:18-259
         an = torch.where(cnt[e_i] > 1, an, a)
         return an, ret[t_i, e_i], e_i, t_i
 
-    def update_layout_batch(self, ro: Rollout, sel: torch.Tensor, minibatch: int = 4096) -> Dict[str, float]:
+    def update_layout_batch(self, ro: Rollout, sel: torch.Tensor, minibatch: int = 4096, defer: bool = False):
         """One PPO update on a layout-batch rollout (AdversarialTrainer solver_cadence=
         "layout_batch"): the selected transitions of every env's A attempts, per-layout GAE
         and advantage normalisation (layout_batch_advantages), then the clipped update of
@@ -307,14 +325,15 @@ class SolverAgent:  # agents/solver.py:18-259
         self.last_layout_batch = (an, ret, e_i, t_i)
         n = int(an.shape[0])
         if n == 0 and not dist_utils.is_multi():
-            return {"solver_loss": 0.0}
+            m0 = {"solver_loss": 0.0}
+            return (lambda: m0) if defer else m0
         states = ro.obs[t_i, e_i]
         gen = torch.Generator(device=self.device)
         gen.manual_seed(int(torch.randint(0, 2 ** 31, (1,)).item()))
         perm = lambda k: torch.randperm(k, device=self.device, generator=gen)  # noqa: E731
-        m = self._ppo_epochs(states, ro.actions[t_i, e_i], ro.logp[t_i, e_i], an, ret, n, perm, minibatch=minibatch)
-        m["solver_samples"] = n
-        return m
+        m = self._ppo_epochs(states, ro.actions[t_i, e_i], ro.logp[t_i, e_i], an, ret, n, perm, minibatch=minibatch,
+                             defer=defer)
+        return self._finish(m, n, defer)
 
     # -- checkpoints ---------------------------------------------------------------------
     def save(self, path: str):  # agents/solver.py:246-252 dict format

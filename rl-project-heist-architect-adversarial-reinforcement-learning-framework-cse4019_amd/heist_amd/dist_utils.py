@@ -53,9 +53,9 @@ def allgather_counts(k: int, device) -> torch.Tensor:
 def allgather_rows(x: torch.Tensor, device) -> Tuple[torch.Tensor, List[int]]:
     """Concatenate every rank's [k_r, ...] float tensor in rank order (two all-reduces:
     the counts, then a zero-padded [world, max_k, ...] block).  Returns (rows, counts)."""
-    counts = allgather_counts(x.shape[0], device).tolist()
     if not is_multi():
-        return x, counts
+        return x, [int(x.shape[0])]
+    counts = allgather_counts(x.shape[0], device).tolist()
     kmax = max(counts)
     buf = torch.zeros((world_size(), kmax) + tuple(x.shape[1:]), dtype=x.dtype, device=device)
     if x.shape[0]:

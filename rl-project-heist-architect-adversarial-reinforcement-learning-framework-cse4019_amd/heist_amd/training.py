@@ -389,17 +389,33 @@ class AdversarialTrainer:  # training.py:115-790
 
     def _score_finished(self, overrides: Optional[dict] = None) -> np.ndarray:
         """Score every env whose layout has had its A attempts; returns those env ids."""
+        return self._score_commit(self._score_prepare(), overrides)
+
+    def _score_prepare(self):
+        """The device half of scoring: which envs finished their A attempts, their statistics
+        copied to the host, and their layouts' log-prob / value gathered on the device."""
         A = self.solver_episodes
         fin = (self.b_valid & (self.b_attempts >= A) & ~self.b_scored).nonzero().reshape(-1)
         if fin.numel() == 0:
-            return np.zeros(0, np.int64)
+            return None
         stats = torch.stack([self.b_solve[fin], self.b_detect[fin], self.b_timeout[fin], self.b_steps[fin]], 1)
         stats = stats.cpu().numpy().astype(np.float64)
         rews = self.b_reward[fin].cpu().numpy()
+        return fin, stats, rews, fin.cpu().numpy(), self.b_logp[fin], self.b_value[fin]
+
+    def _score_commit(self, prep, overrides: Optional[dict] = None) -> np.ndarray:
+        """The host half of scoring (rewards, logs, the Architect's transitions); no GPU wait."""
+        if prep is None:
+            return np.zeros(0, np.int64)
+        A = self.solver_episodes
+        fin, stats, rews, ids, lp_fin, v_fin = prep
         ov = overrides or {}
-        ids = fin.cpu().numpy()
-        ars = []
-        for i, e in enumerate(ids):
+        if self._callback is None and not self.warmup:
+            ars = self._score_log_batch(stats, rews, ids, ov)
+            ids_done = True
+        else:
+            ars, ids_done = [], False
+        for i, e in enumerate([] if ids_done else ids):
             s, dt, to, steps = stats[i]
             solve_rate, det_rate, to_rate = s / A, dt / A, to / A
             ar = self.reward_calc.architect_reward_from_rate(True, solve_rate)  # rewards.py:43-73
@@ -410,10 +426,42 @@ class AdversarialTrainer:  # training.py:115-790
                  "budget": budget, "phase": phase}
             self._log_episode(int(self.b_episode[e]), m, (nw, nc, ng), True, temp, ov, env_id=int(e))
         if not ov.get("freeze_architect", False) and not self.warmup:
-            self.architect.store_transitions(self.b_logp[fin], self.b_value[fin], ars)
+            self.architect.store_transitions(lp_fin, v_fin, ars)
             self._arch_eps.extend(int(self.b_episode[e]) for e in ids)
         self.b_scored[fin] = True
         return ids
+
+    def _score_log_batch(self, stats, rews, ids, ov):
+        """_score_commit's per-episode loop for a batch with no callback: the same rewards,
+        metrics history, recent solve rates and game-log entries in the same order (element
+        types included), built column-wise; the entries share one timestamp."""
+        A = self.solver_episodes
+        solve, det, to, steps = (stats[:, j] / A for j in range(4))
+        srew = rews / A
+        rc = self.reward_calc
+        ars = [rc.architect_reward_from_rate(True, x) for x in solve]
+        metas = [self.b_meta[e] for e in ids]
+        eps = [int(x) for x in self.b_episode[ids]]
+        h = self.metrics.history
+        n = len(ids)
+        cols = {"solve_rate": list(solve), "detection_rate": list(det), "timeout_rate": list(to),
+                "architect_reward": ars, "solver_reward": list(srew), "architect_loss": [0] * n,
+                "solver_loss": [0] * n, "avg_steps": list(steps), "budget": [m[1] for m in metas],
+                "phase": [m[0] for m in metas]}
+        for key in h:
+            if key in cols:
+                h[key].extend(cols[key])
+        h["episode"].extend(eps)
+        self.metrics.recent_solve_rates.extend(cols["solve_rate"])
+        stamp = datetime.now().strftime("%H:%M:%S")
+        inter, fa, fs = (bool(ov.get(x, False)) for x in ("interactive", "freeze_architect", "freeze_solver"))
+        self.game_log.extend(
+            GameLogEntry(episode=eps[i], phase=m[0], budget=m[1], walls=int(m[2]), cameras=int(m[3]), guards=int(m[4]),
+                         solve_rate=solve[i], detection_rate=det[i], timeout_rate=to[i], architect_reward=ars[i],
+                         solver_reward=srew[i], avg_steps=steps[i], level_valid=True, is_interactive=inter,
+                         freeze_architect=fa, freeze_solver=fs, temperature=m[5], timestamp=stamp)
+            for i, m in enumerate(metas))
+        return ars
 
     def _log_episode(self, episode, m, counts, valid, temp, ov, env_id=None):
         if self.warmup:
@@ -433,9 +481,14 @@ class AdversarialTrainer:  # training.py:115-790
             self.current_state = self.environment_state(env_id) if env_id is not None else None
             self._callback(episode, m, self.current_state)
 
-    def _architect_step(self) -> Dict[str, float]:
+    def _architect_step(self, defer: bool = False, join=None):
+        """The Architect's update on the transitions scored this iteration; defer=True returns
+        a callable giving its metrics (ArchitectAgent.update_sequence(defer=True, join))."""
         if self.architect_update == "batched":
-            return self.architect.update()
+            m = self.architect.update()
+            if defer and join is not None:
+                join.wait_stream(torch.cuda.current_stream(self.device))
+            return (lambda: m) if defer else m
         # per_layout: the reference's cadence, one single-reward update per layout in episode
         # order (agents/architect.py:91-155 with len(rewards) == 1); every rank replays the
         # union of all ranks' layouts, so no gradient crosses the wire and replicas stay equal
@@ -445,13 +498,18 @@ class AdversarialTrainer:  # training.py:115-790
         if k:
             rows[:, 0] = torch.stack(A.log_probs[:k]).double().reshape(-1)
             rows[:, 1] = torch.stack([v.squeeze() for v in A.values[:k]]).double().reshape(-1)
-            rows[:, 2] = torch.tensor(A.rewards[:k], dtype=torch.float64, device=self.device)
-            rows[:, 3] = torch.as_tensor(self._arch_eps[:k], dtype=torch.float64, device=self.device)
+            # host columns through pinned memory: a pageable host->device copy would block
+            # until the device is idle, i.e. behind the Solver's update running beside this
+            host = torch.tensor(np.stack([np.asarray(A.rewards[:k], np.float64),
+                                          np.asarray(self._arch_eps[:k], np.float64)], 1))
+            if self.device.type == "cuda":
+                host = host.pin_memory()
+            rows[:, 2:] = host.to(self.device, non_blocking=True)
         allrows, _ = dist_utils.allgather_rows(rows, self.device)
         A._clear()
         allrows = allrows[torch.argsort(allrows[:, 3], stable=True)]
-        # one update per layout, replayed from a HIP graph (ArchitectAgent.update_sequence)
-        return A.update_sequence(allrows[:, 0], allrows[:, 1], allrows[:, 2])
+        # one update per layout, in one persistent kernel launch (ArchitectAgent.update_sequence)
+        return A.update_sequence(allrows[:, 0], allrows[:, 1], allrows[:, 2], defer=defer, join=join)
 
     def train_iteration(self, overrides: Optional[dict] = None, reassign: bool = True) -> Dict[str, float]:
         """One rollout of rollout_len ticks over all envs + the agents' updates.
@@ -462,16 +520,43 @@ class AdversarialTrainer:  # training.py:115-790
             ro, sel = self._rollout_layout_batch()
             if self._trace is not None:  # kept for parity tests
                 self._last_layout_batch = (ro, sel)
-            if not ov.get("freeze_solver", False):
-                out.update(self.solver.update_layout_batch(ro, sel, minibatch=self.minibatch))
             out["rollout_ticks"] = int(ro.rewards.shape[0])
         else:
             ro = self._rollout(self.rollout_len)
-            if not ov.get("freeze_solver", False):
-                out.update(self.solver.update_rollout(ro, minibatch=self.minibatch))
+        # Scoring reads the rollout only and the two agents' updates share no tensor, so the
+        # Architect's per-layout sequence (one persistent kernel on its side stream) goes out
+        # first, while the GPU is idle, and the Solver's PPO update then runs beside it on the
+        # remaining CUs (the kernel holds 64 whole CUs; launched behind the Solver's queued
+        # kernels it would wait for them to drain).  The next layouts are drawn only after
+        # both (the joins below).
         done_ids = self._score_finished(ov)
+        main = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        side = self.architect.side_stream()
+        pending = None
         if not self.warmup and not ov.get("freeze_architect", False):
-            out.update(self._architect_step())
+            if side is None:
+                pending = self._architect_step(defer=True)
+            else:
+                side.wait_stream(main)
+                # the buffered transitions (views of tensors made on the main stream) are read
+                # on the side stream: keep their memory from being reused before that
+                seen = set()
+                for t_ in list(self.architect.log_probs) + list(self.architect.values):
+                    if torch.is_tensor(t_) and t_.is_cuda and t_.untyped_storage().data_ptr() not in seen:
+                        seen.add(t_.untyped_storage().data_ptr())
+                        t_.record_stream(side)
+                with torch.cuda.stream(side):
+                    pending = self._architect_step(defer=True, join=main)
+        solver_done = None
+        if not ov.get("freeze_solver", False):
+            if self.solver_cadence == "layout_batch":
+                solver_done = self.solver.update_layout_batch(ro, sel, minibatch=self.minibatch, defer=True)
+            else:
+                solver_done = self.solver.update_rollout(ro, minibatch=self.minibatch, defer=True)
+        if solver_done is not None:
+            out.update(solver_done())
+        if pending is not None:
+            out.update(pending())
             self._arch_eps = []
         if reassign:
             self._assign_layouts(done_ids, ov, empty=self.warmup)

@@ -250,8 +250,9 @@ def test_architect_update_long_sequence_drift(gpu_device, monkeypatch):
     (8.7e-7 measured); later, fp32 rounding differences get amplified where Adam meets a
     unit crossing its ReLU boundary at a different step, a few weights part by up to ~60 lr
     (0.017) and stay there, while the function the network computes does not drift: V(s0)
-    and the value loss track eager to 1.7e-5 at the end (1.4e-4 worst checkpoint).  The same
-    bounds hold for the graph replay."""
+    and the value loss track eager to 1.7e-5 at the end (1.4e-4 worst checkpoint).  The graph
+    replay (capturable Adam: fp32 bias corrections) is 2e-4 .. 4e-3 off after 200 updates
+    (it varies run to run); its function-level bounds are the kernel's."""
     n_sd = gd.load("nets.npz")
     sd = {k[len("architect/"):]: torch.from_numpy(n_sd[k]) for k in n_sd.files if k.startswith("architect/")}
     table = sorted(set(float(v) for v in gd.load_json("kat.json")["architect_reward"].values())) + [-1.0]
@@ -287,7 +288,8 @@ def test_architect_update_long_sequence_drift(gpu_device, monkeypatch):
         dv = abs(vs0(ag) - vs0(e))
         print("%s vs eager: max |param diff| %.3g after %d updates, %.3g after %d; |V(s0) diff| %.3g; value loss %.9g vs %.9g"
               % (mode, first, k0, worst, k, dv, m["architect_value_loss"], me["architect_value_loss"]))
-        assert first <= 2e-6, (mode, first)
+        # the graph replay's capturable Adam forms the bias corrections in fp32: 2e-4 measured
+        assert first <= (2e-6 if mode == "kernel" else 1e-2), (mode, first)
         assert dv <= 5e-4, (mode, dv)
         assert abs(m["architect_value_loss"] - me["architect_value_loss"]) <= 5e-4 * max(1.0, me["architect_value_loss"])
         if mode == "kernel":  # bit-for-bit deterministic
@@ -296,3 +298,53 @@ def test_architect_update_long_sequence_drift(gpu_device, monkeypatch):
             b.update_sequence(lp[k0:], v[k0:], r[k0:])
             for p, q in zip(b.network.parameters(), ag.network.parameters()):
                 assert torch.equal(p, q)
+
+
+def test_score_log_batch_matches_per_episode_loop():
+    """AdversarialTrainer._score_log_batch (the column-wise scoring log the training loop
+    uses when no callback is set) writes the same metrics history (values and element
+    types), recent solve rates, game-log entries (all fields but the shared timestamp) and
+    Architect rewards as the per-episode _log_episode loop (training.py:383-416)."""
+    from collections import deque
+    from heist_amd.rewards import RewardCalculator
+    from heist_amd.training import AdversarialTrainer, TrainingMetrics
+
+    def fresh():
+        tr = AdversarialTrainer.__new__(AdversarialTrainer)
+        tr.metrics, tr.game_log, tr.reward_calc = TrainingMetrics(), [], RewardCalculator()
+        tr.warmup, tr._callback, tr.solver_episodes = False, None, 4
+        n = 12
+        rng = np.random.default_rng(3)
+        tr.b_episode = rng.integers(0, 10 ** 6, n).astype(np.int64)
+        tr.b_meta = [("Full Security", 15, int(rng.integers(0, 9)), int(rng.integers(0, 3)), int(rng.integers(0, 2)),
+                      float(rng.choice([1.0, 0.75]))) for _ in range(n)]
+        return tr
+
+    rng = np.random.default_rng(4)
+    ids = np.array([7, 2, 9, 0, 11, 5])
+    stats = rng.integers(0, 5, (len(ids), 4)).astype(np.float64)
+    rews = rng.standard_normal(len(ids)).astype(np.float32)
+    ov = {"interactive": False}
+    a, b = fresh(), fresh()
+    ars_a = a._score_log_batch(stats, rews, ids, ov)
+    ars_b = []
+    A = b.solver_episodes
+    for i, e in enumerate(ids):  # the loop of _score_commit
+        s, dt, to, steps = stats[i]
+        ar = b.reward_calc.architect_reward_from_rate(True, s / A)
+        ars_b.append(ar)
+        phase, budget, nw, nc, ng, temp = b.b_meta[e]
+        m = {"solve_rate": s / A, "detection_rate": dt / A, "timeout_rate": to / A, "architect_reward": ar,
+             "solver_reward": rews[i] / A, "architect_loss": 0, "solver_loss": 0, "avg_steps": steps / A,
+             "budget": budget, "phase": phase}
+        b._log_episode(int(b.b_episode[e]), m, (nw, nc, ng), True, temp, ov, env_id=int(e))
+    assert ars_a == ars_b and [type(x) for x in ars_a] == [type(x) for x in ars_b]
+    for key in a.metrics.history:
+        assert a.metrics.history[key] == b.metrics.history[key], key
+        assert [type(x) for x in a.metrics.history[key]] == [type(x) for x in b.metrics.history[key]], key
+    assert list(a.metrics.recent_solve_rates) == list(b.metrics.recent_solve_rates)
+    for ea, eb in zip(a.game_log, b.game_log):
+        da, db = dict(ea.to_dict()), dict(eb.to_dict())
+        da.pop("timestamp"), db.pop("timestamp")
+        assert da == db
+    assert len(a.game_log) == len(b.game_log) == len(ids)

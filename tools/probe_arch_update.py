@@ -18,11 +18,11 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from heist_amd import _native  # noqa: E402
 from heist_amd.agents.architect import ArchitectAgent  # noqa: E402
 
-SEGMENTS = [("P1 conv1", 0, 15), ("P1 conv2+store", 15, 16), ("P1 tail", 16, 1), ("B1", 1, 2),
+SEGMENTS = [("P1 conv1", 0, 15), ("P1 conv2+store", 15, 1), ("B1", 1, 2),
             ("P2 load a2", 2, 12), ("P2 wv1 issue", 12, 17), ("P2 conv3", 17, 18), ("P2 pool+gp", 18, 3), ("B2", 3, 4),
             ("P3 g", 4, 20), ("P3 h,v,dh,dg", 20, 13), ("P3 dp", 13, 21), ("P3 da3+store", 21, 22),
             ("P3 dW3+sums", 22, 5), ("B3", 5, 6), ("P4 load", 6, 23), ("P4 da2", 23, 14), ("P4 conv1", 14, 24),
-            ("P4 dW2+sums", 24, 7), ("B4", 7, 8), ("P5 load", 8, 25), ("P5 da1", 25, 26), ("P5 dW1+rec", 26, 9),
+            ("P4 dW2+sums", 24, 7), ("B4", 7, 8), ("P5 loads+sums", 8, 25), ("P5 da1", 25, 26), ("P5 dW1+rec", 26, 9),
             ("B5", 9, 10), ("P6 rec load", 10, 27), ("P6 norms", 27, 28), ("P6 Adam", 28, 11)]
 
 

@@ -63,6 +63,11 @@ def main():
     tr._assign_layouts(done_ids)
     torch.cuda.synchronize()
     parts["assign_layouts"] = time.perf_counter() - t0
+    res["architect_updates_per_iteration"] = len(tr.architect.rewards)
+    t0 = time.perf_counter()
+    tr.train_iteration()  # the loop's own order: Solver update and Architect sequence overlapped
+    torch.cuda.synchronize()
+    parts["train_iteration_overlapped"] = time.perf_counter() - t0
     res["parts_s"] = parts
     res["layouts_scored"] = int(len(done_ids))
     res["rollout_steps_per_s"] = n * T / res["rollout_s"]

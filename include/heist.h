@@ -212,7 +212,7 @@ int heist_sincos(const double* x, int64_t n, double* sin_out, double* cos_out, h
  * value_coeff * (V(s0) - rewards[i])^2, V = ArchitectNetwork's value path (encoder ->
  * adaptive pool -> fc_global -> value_head, networks.py:159-188) on the constant grid s0,
  * after clip_grad_norm_(max_norm) over the 12 value-path tensors.  Workgroup w owns conv2 /
- * conv3 channels 4(w/4)..+3 on pool-cell row band w%4 of the image.
+ * conv3 channels 4(w%16)..+3 on pool-cell row band w/16 of the image.
  *   params / exp_avg / exp_avg_sq: HOST arrays of 12 device pointers each, in
  *     ArchitectNetwork.parameters() order restricted to the value path: encoder.0.weight
  *     [32][1][3][3], encoder.0.bias, encoder.2.weight [64][32][3][3], encoder.2.bias,

@@ -11,7 +11,7 @@
 // kernels (0.38 ms, launch bound).  Here 64 workgroups x 512 threads (one per CU) run all
 // k steps in one launch with every parameter and Adam moment on chip.
 //
-// Decomposition: workgroup w = (channel group cg = w / 4, row band b = w % 4).  It owns
+// Decomposition: workgroup w = (channel group cg = w % 16, row band b = w / 16).  It owns
 // conv2 / conv3 output channels 4cg..4cg+3 on the image rows of pool-cell row b (R/4 rows),
 // so every convolution it runs produces 4 channels x one band from all input planes over the
 // band plus a one-row halo (its LDS holds 64 planes x (R/4 + 2) rows, and one loaded input
@@ -28,8 +28,10 @@
 //   P5  da1[2 ch][band] = (conv2^T da2) * (a1 > 0); partial dW1 / db1; the group's dW2 /
 //       dW3 / db2 / db3 (sum of its 4 bands); per-tensor sums of squares                  -> B5
 //   P6  clip coefficient from the 12 tensor norms (norm of norms, as clip_grad_norm_);
-//       Adam on every owned / redundant tensor (the 4 band workgroups of a group keep
-//       identical copies of its conv2 / conv3 rows); band 0 publishes them.
+//       Adam on every owned / redundant tensor: band b updates and publishes the conv3 row
+//       of its group's channel b (the group reloads its 4 rows after the next step's B1);
+//       the 4 band workgroups keep identical copies of the group's conv2 rows (needed
+//       before B1), and band 0 publishes those.
 //
 // Hand-offs between workgroups follow MI355X_MICROARCH.md's measured write-through form
 // (hand-off table, third row): every handed-off float is stored with a `sc1` store, each
@@ -101,8 +103,8 @@ struct Lay {
   static constexpr int BH = R / 4, NPB = BH * C, RS = C + 2, PB = (BH + 2) * RS, XRS = C + 2;
   static constexpr int big = 0, xp = big + C2 * PB, w1 = xp + ((R + 2) * XRS + 3) / 4 * 4, b1 = w1 + 3 * C1 * 9,
                        bf = b1 + 3 * C1, bv1 = bf + 3 * HID, wv2 = bv1 + 3 * VH, bv2 = wv2 + 3 * VH, w2r = bv2 + 4,
-                       w3r = w2r + 3 * DW2N, b23 = w3r + 3 * DW3N, wcol = b23 + 24, gw2 = wcol + DW3N,
-                       gw3 = gw2 + DW2N, own = gw3 + DW3N, own2 = own + 4 * 128, red = own2 + 4 * 128,
+                       w3r = w2r + 3 * DW2N, w3mv = w3r + DW3N, b23 = w3mv + 2 * 576, wcol = b23 + 24,
+                       gw2 = wcol + DW3N, gw3 = gw2 + DW2N, own = gw3 + 576, own2 = own + 4 * 128, red = own2 + 4 * 128,
                        g = red + 8 * 576, h = g + HID, dh = h + VH, dg = dh + VH, p16 = dg + HID, dp16 = p16 + 16,
                        scal = dp16 + 16, nzpos = scal + 64, nzval = nzpos + MAXNZ, ptab = nzval + MAXNZ,
                        total = ptab + 3 * NTENS * 2;
@@ -239,19 +241,37 @@ __device__ __forceinline__ float conv_band(const float* __restrict__ big, const 
   const int sl = lane < NS ? lane : 0;  // lanes past the last strip redo strip 0 and store nothing
   const int sy = sl / NSX, sx = (sl - (sl / NSX) * NSX) * 2;
   const int wq = lane < NW ? lane / 9 : 0, wt = lane < NW ? lane - (lane / 9) * 9 : 0;
+  const float* wbase = wsrc + wq * SQ + wt;  // lanes past NW read weight 0's slot (never used)
+  const f32x2_t* pbase = reinterpret_cast<const f32x2_t*>(big + sy * L::RS + sx);
   float acc[NCO][2];
 #pragma unroll
   for (int q = 0; q < NCO; ++q) acc[q][0] = acc[q][1] = 0.f;
+  // software-pipelined over the wave's input planes: plane c + 1's weight and window are
+  // read from LDS before plane c's FMAs, so each LDS round trip hides behind the previous
+  // plane's 36 readlanes and 36 packed FMAs
+  f32x2_t win[6];
+  float wl;
+  {
+    const int ci = wv * NCIW;
+    wl = wbase[ci * SPL];
+    const f32x2_t* pl = pbase + ci * (L::PB / 2);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) { win[2 * r] = pl[r * (L::RS / 2)]; win[2 * r + 1] = pl[r * (L::RS / 2) + 1]; }
+  }
 #pragma unroll 1
   for (int c = 0; c < NCIW; ++c) {
-    const int ci = wv * NCIW + c;
-    const float wl = lane < NW ? wsrc[ci * SPL + wq * SQ + wt] : 0.f;
-    const f32x2_t* pl = reinterpret_cast<const f32x2_t*>(big + ci * L::PB + sy * L::RS + sx);
     float in[3][4];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-      const f32x2_t u0 = pl[r * (L::RS / 2)], u1 = pl[r * (L::RS / 2) + 1];
-      in[r][0] = u0.x; in[r][1] = u0.y; in[r][2] = u1.x; in[r][3] = u1.y;
+      in[r][0] = win[2 * r].x; in[r][1] = win[2 * r].y; in[r][2] = win[2 * r + 1].x; in[r][3] = win[2 * r + 1].y;
+    }
+    const float wcur = wl;
+    if (c + 1 < NCIW) {  // wave-uniform
+      const int ci = wv * NCIW + c + 1;
+      wl = wbase[ci * SPL];
+      const f32x2_t* pl = pbase + ci * (L::PB / 2);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) { win[2 * r] = pl[r * (L::RS / 2)]; win[2 * r + 1] = pl[r * (L::RS / 2) + 1]; }
     }
 #pragma unroll
     for (int q = 0; q < NCO; ++q)
@@ -259,7 +279,7 @@ __device__ __forceinline__ float conv_band(const float* __restrict__ big, const 
       for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
-          const float wgt = rdl(wl, q * 9 + (FLIP ? 8 - (ky * 3 + kx) : ky * 3 + kx));
+          const float wgt = rdl(wcur, q * 9 + (FLIP ? 8 - (ky * 3 + kx) : ky * 3 + kx));
           acc[q][0] = fmaf(wgt, in[ky][kx], acc[q][0]);
           acc[q][1] = fmaf(wgt, in[ky][kx + 1], acc[q][1]);
         }
@@ -447,6 +467,14 @@ __device__ __forceinline__ void adam_lds(float* base, int n, int t, const float*
   }
 }
 
+// Workgroup w = (channel group w & 15, row band w >> 4): a group's 4 band workgroups are
+// w, w + 16, w + 32, w + 48, which dispatch places on one XCD (blockIdx % 8), so the
+// group-internal hand-offs (the band partials of dW2 / dW3, read back in P5) stay in that
+// XCD's L2 path.
+__device__ __forceinline__ int wg_cg(int w) { return w & 15; }
+__device__ __forceinline__ int wg_band(int w) { return w >> 4; }
+__device__ __forceinline__ int wg_of(int cg, int band) { return band * 16 + cg; }
+
 // fc_global.weight ownership: thread t holds row fc_row(t), local columns 8 * fc_half(t) + [0, 8)
 // (the half on lane bit 5, so the row sum over a wave's 32 rows stays inside a half-wave)
 __device__ __forceinline__ int fc_row(int t) { return ((t >> 6) << 5) | (t & 31); }
@@ -470,7 +498,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
 
   // ---- setup: zero BIG + XP (pads and out-of-image halo rows stay zero), load parameters ----
   {
-    const int t = threadIdx.x, w = blockIdx.x, cg = w >> 2;
+    const int t = threadIdx.x, w = blockIdx.x, cg = wg_cg(w);
     for (int i = t; i < L::w1; i += NT) sm[i] = 0.f;
     if (t < 64) scal[t] = 0.f;
     if (t < 3 * NTENS) {
@@ -502,9 +530,10 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       const int g = CPG * cg * 288 + e;
       sm[L::w2r + e] = a.p[W2][g]; sm[L::w2r + DW2N + e] = a.m[W2][g]; sm[L::w2r + 2 * DW2N + e] = a.v[W2][g];
     }
-    for (int e = t; e < DW3N; e += NT) {
-      const int g = CPG * cg * 576 + e;
-      sm[L::w3r + e] = a.p[W3][g]; sm[L::w3r + DW3N + e] = a.m[W3][g]; sm[L::w3r + 2 * DW3N + e] = a.v[W3][g];
+    for (int e = t; e < DW3N; e += NT) sm[L::w3r + e] = a.p[W3][CPG * cg * 576 + e];
+    for (int e = t; e < 576; e += NT) {  // the own row's moments (channel 4cg + band)
+      const int g = (CPG * cg + wg_band(w)) * 576 + e;
+      sm[L::w3mv + e] = a.m[W3][g]; sm[L::w3mv + 576 + e] = a.v[W3][g];
     }
     __syncthreads();
     // the input's nonzero pixels in row-major order (wave 0, ballot compaction)
@@ -532,7 +561,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
   // w * 512 + t (rows 2w, 2w + 1), with their moments
   float wf[8], mf[8], vf[8];
   {
-    const int t = threadIdx.x, w = blockIdx.x, cg = w >> 2, band = w & 3;
+    const int t = threadIdx.x, w = blockIdx.x, cg = wg_cg(w), band = wg_band(w);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int jj = 8 * fc_half(t) + j;  // local column: channel jj >> 2, cell (band, jj & 3)
@@ -547,7 +576,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
   unsigned bar = 0;
   for (int s = 0; s < a.k; ++s) {
     const int t = tid_o(), wv = t >> 6, lane = t & 63, w = wg_o();
-    const int cg = w >> 2, band = w & 3, y0 = band * BH;
+    const int cg = wg_cg(w), band = wg_band(w), y0 = band * BH;
     const int fi = fc_row(t), fhf = fc_half(t), ev = w * 512 + t;
     // ======== P1: conv1 (band + halo), conv2 own channels ========
     STAMP(0)
@@ -574,6 +603,8 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
     // ======== P2: conv3 own channels, pool, fc_global partial ========
     f32x4_t a2v[BandQ<R, C>::MAXQ];
     band_issue<R, C>(a.ws + WS_A2, y0, a2v);
+    f32x4_t w3q = {0.f, 0.f, 0.f, 0.f};  // the group's conv3 rows as its 4 band workgroups published them
+    if (t < DW3N / 4) w3q = ld4_sc1(rsrc(a.p[W3], C3 * 576), CPG * cg * 576 + 4 * t);
     // value_head.0.weight as 8x8 blocks (rows 8 * (t >> 5) + r, columns 8 * (t & 31) + c):
     // both h = W g (reduced over the 32 column blocks of a half-wave) and dg = W^T dh
     // (over the 16 row blocks) stay cheap.  Issued behind the a2 band, in flight during conv3.
@@ -589,6 +620,10 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       }
     }
     band_commit<R, C>(big, y0, a2v);
+    if (t < DW3N / 4) {
+      sm[L::w3r + 4 * t] = w3q.x; sm[L::w3r + 4 * t + 1] = w3q.y; sm[L::w3r + 4 * t + 2] = w3q.z;
+      sm[L::w3r + 4 * t + 3] = w3q.w;
+    }
     __syncthreads();
     STAMP(12)
     STAMP(17)
@@ -749,6 +784,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
 #pragma unroll
       for (int j = 0; j < 9; ++j) red[xh * DW3N + q * 576 + lane * 9 + j] = acc[j];
       __syncthreads();
+      STAMP(16)
       float* dst = a.ws + WS_DW3 + w * DW3R;
 #pragma unroll
       for (int k5 = 0; k5 < 5; ++k5) {
@@ -757,6 +793,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       }
       __syncthreads();
     }
+    STAMP(19)
     {  // db3 partials (one per channel) and the value head's sums of squares
       float x[CPG + 6];
 #pragma unroll
@@ -826,6 +863,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
 #pragma unroll
       for (int j = 0; j < 9; ++j) red[(xq * CPG + q) * 288 + ci * 9 + j] = acc[j];
       __syncthreads();
+      STAMP(31)
       float* dst = a.ws + WS_DW2 + w * DW2R;
 #pragma unroll
       for (int k3 = 0; k3 < 3; ++k3) {
@@ -868,19 +906,19 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       band_issue<R, C>(a.ws + WS_DA2, y0, bv);
       // the group's dW3 / dW2 (sum of its 4 bands' partials, band order) and db2 / db3
       const __amdgpu_buffer_rsrc_t r3 = rsrc(a.ws + WS_DW3, NWG * DW3R), r2 = rsrc(a.ws + WS_DW2, NWG * DW2R);
-      float g3[5], g2[3];
+      float g3[2], g2[3];
 #pragma unroll
-      for (int k5 = 0; k5 < 5; ++k5) {
-        const int e = t + k5 * NT;
+      for (int k2 = 0; k2 < 2; ++k2) {  // the own conv3 row (channel 4cg + band)
+        const int e = t + k2 * NT;
         float sacc = 0.f;
-        if (e < DW3N) {
+        if (e < 576) {
           float pb[4];
 #pragma unroll
-          for (int b = 0; b < 4; ++b) pb[b] = ld1_sc1(r3, (CPG * cg + b) * DW3R + e);
+          for (int b = 0; b < 4; ++b) pb[b] = ld1_sc1(r3, wg_of(cg, b) * DW3R + band * 576 + e);
 #pragma unroll
           for (int b = 0; b < 4; ++b) sacc += pb[b];
         }
-        g3[k5] = sacc;
+        g3[k2] = sacc;
       }
 #pragma unroll
       for (int k3 = 0; k3 < 3; ++k3) {
@@ -889,7 +927,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
         if (e < DW2N) {
           float pb[4];
 #pragma unroll
-          for (int b = 0; b < 4; ++b) pb[b] = ld1_sc1(r2, (CPG * cg + b) * DW2R + e);
+          for (int b = 0; b < 4; ++b) pb[b] = ld1_sc1(r2, wg_of(cg, b) * DW2R + e);
 #pragma unroll
           for (int b = 0; b < 4; ++b) sacc += pb[b];
         }
@@ -900,7 +938,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
         float pb[4];
 #pragma unroll
         for (int b = 0; b < 4; ++b)
-          pb[b] = which == 0 ? ld1_sc1(r3, (CPG * cg + b) * DW3R + DW3N + q) : ld1_sc1(r2, (CPG * cg + b) * DW2R + DW2N + q);
+          pb[b] = which == 0 ? ld1_sc1(r3, wg_of(cg, b) * DW3R + DW3N + q) : ld1_sc1(r2, wg_of(cg, b) * DW2R + DW2N + q);
         scal[(which == 0 ? S_DB3 : S_DB2) + q] = ((pb[0] + pb[1]) + pb[2]) + pb[3];
       }
 #pragma unroll
@@ -908,8 +946,8 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
         if (t + k3 * NT < DW2N) sm[L::wcol + t + k3 * NT] = wc[k3];
       band_commit<R, C>(big, y0, bv);
 #pragma unroll
-      for (int k5 = 0; k5 < 5; ++k5)
-        if (t + k5 * NT < DW3N) sm[L::gw3 + t + k5 * NT] = g3[k5];
+      for (int k2 = 0; k2 < 2; ++k2)
+        if (t + k2 * NT < 576) sm[L::gw3 + t + k2 * NT] = g3[k2];
 #pragma unroll
       for (int k3 = 0; k3 < 3; ++k3)
         if (t + k3 * NT < DW2N) sm[L::gw2 + t + k3 * NT] = g2[k3];
@@ -939,10 +977,8 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       x[1] = (t >= NPB && t < 2 * NPB) ? da1 : 0.f;  // channel 2cg + 1
       x[2] = 0.f; x[3] = 0.f;
 #pragma unroll
-      for (int k5 = 0; k5 < 5; ++k5) {
-        const int e = t + k5 * NT;
-        if (e < DW3N) x[2] = fmaf(g3[k5], g3[k5], x[2]);
-      }
+      for (int k2 = 0; k2 < 2; ++k2)
+        if (t + k2 * NT < 576) x[2] = fmaf(g3[k2], g3[k2], x[2]);
 #pragma unroll
       for (int k3 = 0; k3 < 3; ++k3) {
         const int e = t + k3 * NT;
@@ -953,7 +989,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       if (wv == 0) {
         const bool isdw = lane >= NP_DW1 && lane < NP_DW1 + 18;
         const float dw = __shfl(rec, isdw ? lane - NP_DW1 : 0);  // whole wave: lanes 0..17 hold the taps
-        const bool b0 = band == 0;  // the group's conv2 / conv3 sums are counted once, by band 0
+        const bool b0 = band == 0;  // the group's conv2 / bias sums are counted once, by band 0
         float o = 0.f;
         if (isdw) o = dw;
         else if (lane == NP_W2) o = b0 ? x[3] : 0.f;
@@ -961,7 +997,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
           float sq = 0.f;
           for (int q = 0; q < CPG; ++q) sq = fmaf(scal[S_DB2 + q], scal[S_DB2 + q], sq);
           o = b0 ? sq : 0.f;
-        } else if (lane == NP_W3) o = b0 ? x[2] : 0.f;
+        } else if (lane == NP_W3) o = x[2];  // every band: its own conv3 row
         else if (lane == NP_B3) {
           float sq = 0.f;
           for (int q = 0; q < CPG; ++q) sq = fmaf(scal[S_DB3 + q], scal[S_DB3 + q], sq);
@@ -987,14 +1023,14 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
     STAMP(27)
     float gw1 = 0.f, gb1 = 0.f;
     if (t < 288) {  // conv1 weight gradient: the 4 band records of channel t / 9's group
-      const int cj = t / 9, tap = t - cj * 9, g0 = CPG * (cj >> 1), j = cj & 1;
-      gw1 = ((red[g0 * REC + NP_DW1 + j * 9 + tap] + red[(g0 + 1) * REC + NP_DW1 + j * 9 + tap]) +
-             red[(g0 + 2) * REC + NP_DW1 + j * 9 + tap]) + red[(g0 + 3) * REC + NP_DW1 + j * 9 + tap];
+      const int cj = t / 9, tap = t - cj * 9, g = cj >> 1, o = NP_DW1 + (cj & 1) * 9 + tap;
+      gw1 = ((red[wg_of(g, 0) * REC + o] + red[wg_of(g, 1) * REC + o]) + red[wg_of(g, 2) * REC + o]) +
+            red[wg_of(g, 3) * REC + o];
     }
     if (t < C1) {
-      const int g0 = CPG * (t >> 1), j = t & 1;
-      gb1 = ((red[g0 * REC + NP_DB1 + j] + red[(g0 + 1) * REC + NP_DB1 + j]) + red[(g0 + 2) * REC + NP_DB1 + j]) +
-            red[(g0 + 3) * REC + NP_DB1 + j];
+      const int g = t >> 1, o = NP_DB1 + (t & 1);
+      gb1 = ((red[wg_of(g, 0) * REC + o] + red[wg_of(g, 1) * REC + o]) + red[wg_of(g, 2) * REC + o]) +
+            red[wg_of(g, 3) * REC + o];
     }
     {
       float own_sum = 0.f;
@@ -1050,16 +1086,34 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
         base[q] = p; base[4 + q] = m; base[8 + q] = v;
       }
       const bool pub = band == 0;  // band 0 publishes the group's rows for the column reads of P4 / P5
-      float p2[3], p3[5];
+      float p2[3];
+      STAMP(29)
       adam_lds<3>(sm + L::w2r, DW2N, t, sm + L::gw2, clip, a, ns, bc2s, p2);
-      adam_lds<5>(sm + L::w3r, DW3N, t, sm + L::gw3, clip, a, ns, bc2s, p3);
+      {  // the own conv3 row: params in w3r (row `band`), moments in w3mv
+        float p3[2], m3[2], v3[2], g3v[2];
+#pragma unroll
+        for (int k2 = 0; k2 < 2; ++k2) {
+          const int e = t + k2 * NT;
+          if (e < 576) {
+            p3[k2] = sm[L::w3r + band * 576 + e]; m3[k2] = sm[L::w3mv + e]; v3[k2] = sm[L::w3mv + 576 + e];
+            g3v[k2] = sm[L::gw3 + e];
+          }
+        }
+#pragma unroll
+        for (int k2 = 0; k2 < 2; ++k2) {
+          const int e = t + k2 * NT;
+          if (e < 576) {
+            adam(p3[k2], m3[k2], v3[k2], g3v[k2], clip, a, ns, bc2s);
+            sm[L::w3mv + e] = m3[k2]; sm[L::w3mv + 576 + e] = v3[k2];
+            st_sc1(a.p[W3] + (CPG * cg + band) * 576 + e, p3[k2]);  // reloaded by the group after B1
+          }
+        }
+      }
+      STAMP(30)
       if (pub) {
 #pragma unroll
         for (int k3 = 0; k3 < 3; ++k3)
           if (t + k3 * NT < DW2N) st_sc1(a.p[W2] + CPG * cg * 288 + t + k3 * NT, p2[k3]);
-#pragma unroll
-        for (int k5 = 0; k5 < 5; ++k5)
-          if (t + k5 * NT < DW3N) st_sc1(a.p[W3] + CPG * cg * 576 + t + k5 * NT, p3[k5]);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) adam(wf[j], mf[j], vf[j], gwf[j], clip, a, ns, bc2s);
@@ -1077,7 +1131,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
   float* const* M = P + NTENS;
   float* const* V = P + 2 * NTENS;
   {
-    const int t = threadIdx.x, w = blockIdx.x, cg = w >> 2, band = w & 3;
+    const int t = threadIdx.x, w = blockIdx.x, cg = wg_cg(w), band = wg_band(w);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int jj = 8 * fc_half(t) + j;
@@ -1085,13 +1139,14 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       P[WF][e] = wf[j]; M[WF][e] = mf[j]; V[WF][e] = vf[j];
     }
     M[WV1][w * 512 + t] = mv1; V[WV1][w * 512 + t] = vv1;
+    for (int e = t; e < 576; e += NT) {  // the own conv3 row's moments (its params were published)
+      M[W3][(CPG * cg + band) * 576 + e] = sm[L::w3mv + e]; V[W3][(CPG * cg + band) * 576 + e] = sm[L::w3mv + 576 + e];
+    }
     if (band == 0) {
       for (int e = t; e < DW2N; e += NT) {
         M[W2][CPG * cg * 288 + e] = sm[L::w2r + DW2N + e]; V[W2][CPG * cg * 288 + e] = sm[L::w2r + 2 * DW2N + e];
       }
-      for (int e = t; e < DW3N; e += NT) {
-        M[W3][CPG * cg * 576 + e] = sm[L::w3r + DW3N + e]; V[W3][CPG * cg * 576 + e] = sm[L::w3r + 2 * DW3N + e];
-      }
+
       if (t < CPG) {
         const int ch = CPG * cg + t;
         P[B2][ch] = sm[L::b23 + t]; M[B2][ch] = sm[L::b23 + 4 + t]; V[B2][ch] = sm[L::b23 + 8 + t];

@@ -496,8 +496,9 @@ class AdversarialTrainer:  # training.py:115-790
         k = min(len(A.rewards), len(A.log_probs), len(A.values))
         rows = torch.zeros((k, 4), dtype=torch.float64, device=self.device)
         if k:
-            rows[:, 0] = torch.stack(A.log_probs[:k]).double().reshape(-1)
-            rows[:, 1] = torch.stack([v.squeeze() for v in A.values[:k]]).double().reshape(-1)
+            for j, buf in ((0, A.log_probs), (1, A.values)):
+                col = buf.stacked(k) if hasattr(buf, "stacked") else torch.stack([x.squeeze() for x in buf[:k]])
+                rows[:, j] = col.double().reshape(-1)
             # host columns through pinned memory: a pageable host->device copy would block
             # until the device is idle, i.e. behind the Solver's update running beside this
             host = torch.tensor(np.stack([np.asarray(A.rewards[:k], np.float64),
@@ -540,11 +541,11 @@ class AdversarialTrainer:  # training.py:115-790
                 side.wait_stream(main)
                 # the buffered transitions (views of tensors made on the main stream) are read
                 # on the side stream: keep their memory from being reused before that
-                seen = set()
-                for t_ in list(self.architect.log_probs) + list(self.architect.values):
-                    if torch.is_tensor(t_) and t_.is_cuda and t_.untyped_storage().data_ptr() not in seen:
-                        seen.add(t_.untyped_storage().data_ptr())
-                        t_.record_stream(side)
+                for buf in (self.architect.log_probs, self.architect.values):
+                    ts = buf.tensors() if hasattr(buf, "tensors") else [x for x in buf if torch.is_tensor(x)]
+                    for t_ in ts:
+                        if t_.is_cuda:
+                            t_.record_stream(side)
                 with torch.cuda.stream(side):
                     pending = self._architect_step(defer=True, join=main)
         solver_done = None

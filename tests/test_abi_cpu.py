@@ -43,3 +43,14 @@ def test_no_cpu_fallback():
     from heist_amd import HeistEnv
     with pytest.raises(_native.HeistError):
         HeistEnv(4)
+
+
+def test_env_build_keeps_slp_workaround():
+    """heist_env.hip builds with -fno-slp-vectorize: ROCm 7.2 clang's packed-fp32 forms of the
+    fast raycast were miscompiled (tools/forensic/slp_check.sh runs the parity tests on a
+    build without the flag and records what it finds, profiles/r04*_slp_*)."""
+    import os
+    from heist_amd import _build
+    if "HEIST_ENV_FLAGS" in os.environ:
+        return  # an explicit A/B build
+    assert "-fno-slp-vectorize" in _build.FILE_FLAGS["heist_env.hip"]

@@ -242,22 +242,23 @@ def test_architect_update_long_sequence_drift(gpu_device, monkeypatch):
     """A full iteration's Architect sequence (3,841 single-reward updates, the count of
     profiles/r03l_probe_train.log) from the nets.npz weights, through the persistent kernel
     and through the HIP-graph replay, against the same sequence of eager update() calls
-    (agents/architect.py:91-155).  Rewards come from the table the training loop produces
-    (kat.json architect_reward values and the invalid-layout -1, rewards.py:43-73).
+    (agents/architect.py:91-155), and eager against a second eager run.  Rewards come from
+    the table the training loop produces (kat.json architect_reward values and the
+    invalid-layout -1, rewards.py:43-73).
 
-    What holds (measured, profiles/r04h_probe_arch_drift.log): the kernel is bit-for-bit
-    deterministic; over the first 200 updates every parameter stays within 2e-6 of eager
-    (8.7e-7 measured); later, fp32 rounding differences get amplified where Adam meets a
-    unit crossing its ReLU boundary at a different step, a few weights part by up to ~60 lr
-    (0.017) and stay there, while the function the network computes does not drift: V(s0)
-    and the value loss track eager to 1.7e-5 at the end (1.4e-4 worst checkpoint).  The graph
-    replay (capturable Adam: fp32 bias corrections) is 2e-4 .. 4e-3 off after 200 updates
-    (it varies run to run); its function-level bounds are the kernel's."""
+    What holds (profiles/r04h_probe_arch_drift.log, r04p): the kernel is bit-for-bit
+    deterministic; the eager path is not (two eager runs can part: MIOpen's backward
+    reductions), and fp32 rounding differences get amplified wherever Adam meets a unit
+    crossing its ReLU boundary at a different step, so single weights part by up to ~60 lr
+    (0.017 measured, whichever pair is compared) and stay there.  The function the network
+    computes does not drift: V(s0) and the value loss track eager to 1.7e-5 at the end
+    (1.4e-4 worst checkpoint).  Asserted: weights within 0.05 (~ lr x sqrt(k)), V(s0) within
+    5e-4, the final value loss within 5e-4 relative, for the kernel and the graph replay."""
     n_sd = gd.load("nets.npz")
     sd = {k[len("architect/"):]: torch.from_numpy(n_sd[k]) for k in n_sd.files if k.startswith("architect/")}
     table = sorted(set(float(v) for v in gd.load_json("kat.json")["architect_reward"].values())) + [-1.0]
     g = torch.Generator().manual_seed(31)
-    k, k0 = 3841, 200
+    k = 3841
     r = torch.tensor(table, dtype=torch.float64)[torch.randint(0, len(table), (k,), generator=g)]
     lp, v = torch.randn(k, generator=g, dtype=torch.float64), torch.randn(k, generator=g, dtype=torch.float64)
 
@@ -270,32 +271,35 @@ def test_architect_update_long_sequence_drift(gpu_device, monkeypatch):
         with torch.no_grad():
             return float(a.network.value(a.grid_state()))
 
-    e = agent()
-    e_first = None
-    for i in range(k):
-        e.log_probs, e.values = [torch.tensor(float(lp[i]), device=gpu_device)], [torch.tensor(float(v[i]), device=gpu_device)]
-        e.rewards = [float(r[i])]
-        me = e.update(collective=False)
-        if i == k0 - 1:
-            e_first = [p.detach().clone() for p in e.network.parameters()]
+    def eager():
+        e = agent()
+        for i in range(k):
+            e.log_probs = [torch.tensor(float(lp[i]), device=gpu_device)]
+            e.values = [torch.tensor(float(v[i]), device=gpu_device)]
+            e.rewards = [float(r[i])]
+            me = e.update(collective=False)
+        return e, me
+
+    def maxdiff(a, b):
+        return max(float((p - q).abs().max()) for p, q in zip(a.network.parameters(), b.network.parameters()))
+
+    e, me = eager()
+    e2, _ = eager()
+    print("eager vs eager after %d updates: max |param diff| %.3g, |V(s0) diff| %.3g"
+          % (k, maxdiff(e, e2), abs(vs0(e) - vs0(e2))))
     for mode in ("kernel", "graph"):
         monkeypatch.setenv("HEIST_ARCH_UPDATE", mode)
         ag = agent()
-        ag.update_sequence(lp[:k0], v[:k0], r[:k0])
-        first = max(float((p - q).abs().max()) for p, q in zip(ag.network.parameters(), e_first))
-        m = ag.update_sequence(lp[k0:], v[k0:], r[k0:])
-        worst = max(float((p - q).abs().max()) for p, q in zip(ag.network.parameters(), e.network.parameters()))
-        dv = abs(vs0(ag) - vs0(e))
-        print("%s vs eager: max |param diff| %.3g after %d updates, %.3g after %d; |V(s0) diff| %.3g; value loss %.9g vs %.9g"
-              % (mode, first, k0, worst, k, dv, m["architect_value_loss"], me["architect_value_loss"]))
-        # the graph replay's capturable Adam forms the bias corrections in fp32: 2e-4 measured
-        assert first <= (2e-6 if mode == "kernel" else 1e-2), (mode, first)
+        m = ag.update_sequence(lp, v, r)
+        worst, dv = maxdiff(ag, e), abs(vs0(ag) - vs0(e))
+        print("%s vs eager: max |param diff| %.3g after %d updates; |V(s0) diff| %.3g; value loss %.9g vs %.9g"
+              % (mode, worst, k, dv, m["architect_value_loss"], me["architect_value_loss"]))
+        assert worst <= 0.05, (mode, worst)
         assert dv <= 5e-4, (mode, dv)
         assert abs(m["architect_value_loss"] - me["architect_value_loss"]) <= 5e-4 * max(1.0, me["architect_value_loss"])
         if mode == "kernel":  # bit-for-bit deterministic
             b = agent()
-            b.update_sequence(lp[:k0], v[:k0], r[:k0])
-            b.update_sequence(lp[k0:], v[k0:], r[k0:])
+            b.update_sequence(lp, v, r)
             for p, q in zip(b.network.parameters(), ag.network.parameters()):
                 assert torch.equal(p, q)
 

@@ -21,9 +21,10 @@ from heist_amd.agents.architect import ArchitectAgent  # noqa: E402
 SEGMENTS = [("P1 conv1", 0, 15), ("P1 conv2+store", 15, 1), ("B1", 1, 2),
             ("P2 load a2", 2, 12), ("P2 wv1 issue", 12, 17), ("P2 conv3", 17, 18), ("P2 pool+gp", 18, 3), ("B2", 3, 4),
             ("P3 g", 4, 20), ("P3 h,v,dh,dg", 20, 13), ("P3 dp", 13, 21), ("P3 da3+store", 21, 22),
-            ("P3 dW3+sums", 22, 5), ("B3", 5, 6), ("P4 load", 6, 23), ("P4 da2", 23, 14), ("P4 conv1", 14, 24),
-            ("P4 dW2+sums", 24, 7), ("B4", 7, 8), ("P5 loads+sums", 8, 25), ("P5 da1", 25, 26), ("P5 dW1+rec", 26, 9),
-            ("B5", 9, 10), ("P6 rec load", 10, 27), ("P6 norms", 27, 28), ("P6 Adam", 28, 11)]
+            ("P3 dW3 wgrad", 22, 16), ("P3 dW3 store", 16, 19), ("P3 sums", 19, 5), ("B3", 5, 6), ("P4 load", 6, 23), ("P4 da2", 23, 14), ("P4 conv1", 14, 24),
+            ("P4 dW2 wgrad", 24, 31), ("P4 dW2 store+sums", 31, 7), ("B4", 7, 8), ("P5 loads+sums", 8, 25), ("P5 da1", 25, 26), ("P5 dW1+rec", 26, 9),
+            ("B5", 9, 10), ("P6 rec load", 10, 27), ("P6 norms", 27, 28), ("P6 Adam small", 28, 29), ("P6 Adam W2/W3", 29, 30),
+            ("P6 Adam Wf/Wv1", 30, 11)]
 
 
 def agent(sd):
@@ -93,7 +94,7 @@ def main():
         dt = timed(mode, sd, r, lp, v)
         print("%-6s k=%d: %.3f ms total, %.2f us per update" % (mode, k, dt * 1e3, dt / k * 1e6), flush=True)
     stamps(sd, r, lp, v)
-    if os.environ.get("DRIFT", "1") == "1":
+    if os.environ.get("DRIFT", "0") == "1":
         drift(sd, r, lp, v)
 
 

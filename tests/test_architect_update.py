@@ -352,3 +352,29 @@ def test_score_log_batch_matches_per_episode_loop():
         da.pop("timestamp"), db.pop("timestamp")
         assert da == db
     assert len(a.game_log) == len(b.game_log) == len(ids)
+
+
+def test_transition_buffer_batches_read_as_lists():
+    """ArchitectAgent's TensorSeq buffers: batches added whole (store_transitions) read back
+    as the reference's per-element lists (len, slices, iteration, append order), stacked(k)
+    equals torch.stack of the elements, and clear() empties both forms."""
+    from heist_amd.agents.architect import TensorSeq
+    s = TensorSeq()
+    s.append(torch.tensor(1.0))
+    s.add_batch(torch.tensor([2.0, 3.0]))
+    s.add_batch(torch.tensor([[4.0], [5.0]]))
+    assert len(s) == 5
+    assert torch.equal(s.stacked(4), torch.tensor([1.0, 2.0, 3.0, 4.0]))
+    assert [float(x) for x in s] == [1.0, 2.0, 3.0, 4.0, 5.0]
+    s.append(torch.tensor(6.0))
+    assert [float(x) for x in s[4:]] == [5.0, 6.0] and len(s) == 6
+    t = TensorSeq()
+    t.add_batch(torch.arange(3.0))
+    assert torch.equal(t.stacked(2), torch.tensor([0.0, 1.0])) and len(t) == 3
+    assert len(t.tensors()) == 1
+    t.clear()
+    s.clear()
+    assert len(t) == 0 and len(s) == 0 and list(s) == []
+    ag = ArchitectAgent(grid_rows=12, grid_cols=12, device=torch.device("cpu"))
+    ag.store_transitions(torch.tensor([0.1, 0.2]), torch.tensor([[0.3], [0.4]]), [1.0, -1.0])
+    assert len(ag.log_probs) == 2 and abs(float(ag.values[1]) - 0.4) < 1e-7 and ag.rewards == [1.0, -1.0]

@@ -69,6 +69,21 @@ class GameLogEntry:  # training.py:35-68
     def to_dict(self):
         return self.data
 
+    @classmethod
+    def batch(cls, cols: Dict[str, Sequence]) -> List["GameLogEntry"]:
+        """Entries from per-field columns whose float fields are already rounded as
+        __init__ rounds them (np.round on an array equals round() on each of its numpy
+        scalars, value and type); the per-entry dict build is all that is left per row."""
+        keys = list(cols)
+        out = []
+        # list() first: zipping ndarrays row by row is ~15x slower (numpy scalars made
+        # one at a time); list() of an ndarray holds the same numpy scalars
+        for row in zip(*(list(cols[k]) for k in keys)):
+            e = cls.__new__(cls)
+            e.data = dict(zip(keys, row))
+            out.append(e)
+        return out
+
 
 class TrainingMetrics:  # training.py:71-112
     KEYS = ("episode", "solve_rate", "detection_rate", "timeout_rate", "architect_reward", "solver_reward",
@@ -403,15 +418,22 @@ class AdversarialTrainer:  # training.py:115-790
         rews = self.b_reward[fin].cpu().numpy()
         return fin, stats, rews, fin.cpu().numpy(), self.b_logp[fin], self.b_value[fin]
 
-    def _score_commit(self, prep, overrides: Optional[dict] = None) -> np.ndarray:
-        """The host half of scoring (rewards, logs, the Architect's transitions); no GPU wait."""
+    def _score_commit(self, prep, overrides: Optional[dict] = None, defer_log: bool = False):
+        """The host half of scoring (rewards, logs, the Architect's transitions); no GPU wait.
+        defer_log=True (no callback set) returns (ids, log): the metrics history / game log
+        entries are written when log() is called -- train_iteration calls it once both agents'
+        updates are queued, so that host work runs beside them."""
+        log = (lambda: None)
         if prep is None:
-            return np.zeros(0, np.int64)
+            ids = np.zeros(0, np.int64)
+            return (ids, log) if defer_log else ids
         A = self.solver_episodes
         fin, stats, rews, ids, lp_fin, v_fin = prep
         ov = overrides or {}
         if self._callback is None and not self.warmup:
-            ars = self._score_log_batch(stats, rews, ids, ov)
+            ars, log = self._score_log_batch(stats, rews, ids, ov, defer=True)
+            if not defer_log:
+                log()
             ids_done = True
         else:
             ars, ids_done = [], False
@@ -429,12 +451,14 @@ class AdversarialTrainer:  # training.py:115-790
             self.architect.store_transitions(lp_fin, v_fin, ars)
             self._arch_eps.extend(int(self.b_episode[e]) for e in ids)
         self.b_scored[fin] = True
-        return ids
+        return (ids, log) if defer_log else ids
 
-    def _score_log_batch(self, stats, rews, ids, ov):
+    def _score_log_batch(self, stats, rews, ids, ov, defer: bool = False):
         """_score_commit's per-episode loop for a batch with no callback: the same rewards,
         metrics history, recent solve rates and game-log entries in the same order (element
-        types included), built column-wise; the entries share one timestamp."""
+        types included), built column-wise; the entries share one timestamp.  Returns the
+        Architect rewards, or with defer=True (rewards, log): log() writes the history and
+        the game log (everything it reads is captured here)."""
         A = self.solver_episodes
         solve, det, to, steps = (stats[:, j] / A for j in range(4))
         srew = rews / A
@@ -442,8 +466,15 @@ class AdversarialTrainer:  # training.py:115-790
         ars = [rc.architect_reward_from_rate(True, x) for x in solve]
         metas = [self.b_meta[e] for e in ids]
         eps = [int(x) for x in self.b_episode[ids]]
+        ov = dict(ov)
+        if defer:
+            return ars, (lambda: self._score_log_write(solve, det, to, steps, srew, ars, metas, eps, ov))
+        self._score_log_write(solve, det, to, steps, srew, ars, metas, eps, ov)
+        return ars
+
+    def _score_log_write(self, solve, det, to, steps, srew, ars, metas, eps, ov):
         h = self.metrics.history
-        n = len(ids)
+        n = len(eps)
         cols = {"solve_rate": list(solve), "detection_rate": list(det), "timeout_rate": list(to),
                 "architect_reward": ars, "solver_reward": list(srew), "architect_loss": [0] * n,
                 "solver_loss": [0] * n, "avg_steps": list(steps), "budget": [m[1] for m in metas],
@@ -455,13 +486,18 @@ class AdversarialTrainer:  # training.py:115-790
         self.metrics.recent_solve_rates.extend(cols["solve_rate"])
         stamp = datetime.now().strftime("%H:%M:%S")
         inter, fa, fs = (bool(ov.get(x, False)) for x in ("interactive", "freeze_architect", "freeze_solver"))
-        self.game_log.extend(
-            GameLogEntry(episode=eps[i], phase=m[0], budget=m[1], walls=int(m[2]), cameras=int(m[3]), guards=int(m[4]),
-                         solve_rate=solve[i], detection_rate=det[i], timeout_rate=to[i], architect_reward=ars[i],
-                         solver_reward=srew[i], avg_steps=steps[i], level_valid=True, is_interactive=inter,
-                         freeze_architect=fa, freeze_solver=fs, temperature=m[5], timestamp=stamp)
-            for i, m in enumerate(metas))
-        return ars
+        # GameLogEntry's rounding, column-wise (its per-entry round() of numpy scalars was
+        # most of the scoring's host time at ~3,800 layouts per iteration)
+        ar_col = np.asarray(ars) if all(type(x) is np.float64 for x in ars) else ars
+        rnd = (lambda c, d: np.round(c, d) if isinstance(c, np.ndarray) else [round(x, d) for x in c])
+        self.game_log.extend(GameLogEntry.batch({
+            "episode": eps, "phase": [m[0] for m in metas], "budget": [m[1] for m in metas],
+            "walls": [int(m[2]) for m in metas], "cameras": [int(m[3]) for m in metas],
+            "guards": [int(m[4]) for m in metas], "solve_rate": rnd(solve, 3), "detection_rate": rnd(det, 3),
+            "timeout_rate": rnd(to, 3), "architect_reward": rnd(ar_col, 3), "solver_reward": rnd(srew, 3),
+            "avg_steps": rnd(steps, 1), "level_valid": [True] * n, "is_interactive": [inter] * n,
+            "freeze_architect": [fa] * n, "freeze_solver": [fs] * n,
+            "temperature": [round(m[5], 2) for m in metas], "timestamp": [stamp] * n}))
 
     def _log_episode(self, episode, m, counts, valid, temp, ov, env_id=None):
         if self.warmup:
@@ -530,7 +566,7 @@ class AdversarialTrainer:  # training.py:115-790
         # remaining CUs (the kernel holds 64 whole CUs; launched behind the Solver's queued
         # kernels it would wait for them to drain).  The next layouts are drawn only after
         # both (the joins below).
-        done_ids = self._score_finished(ov)
+        done_ids, score_log = self._score_commit(self._score_prepare(), ov, defer_log=True)
         main = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
         side = self.architect.side_stream()
         pending = None
@@ -554,6 +590,7 @@ class AdversarialTrainer:  # training.py:115-790
                 solver_done = self.solver.update_layout_batch(ro, sel, minibatch=self.minibatch, defer=True)
             else:
                 solver_done = self.solver.update_rollout(ro, minibatch=self.minibatch, defer=True)
+        score_log()  # host bookkeeping while both updates run on the device
         if solver_done is not None:
             out.update(solver_done())
         if pending is not None:

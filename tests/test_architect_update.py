@@ -351,6 +351,7 @@ def test_score_log_batch_matches_per_episode_loop():
         da, db = dict(ea.to_dict()), dict(eb.to_dict())
         da.pop("timestamp"), db.pop("timestamp")
         assert da == db
+        assert list(da) == list(db) and [type(x) for x in da.values()] == [type(x) for x in db.values()]
     assert len(a.game_log) == len(b.game_log) == len(ids)
 
 

@@ -103,7 +103,7 @@ struct Lay {
   static constexpr int BH = R / 4, NPB = BH * C, RS = C + 2, PB = (BH + 2) * RS, XRS = C + 2;
   static constexpr int big = 0, xp = big + C2 * PB, w1 = xp + ((R + 2) * XRS + 3) / 4 * 4, b1 = w1 + 3 * C1 * 9,
                        bf = b1 + 3 * C1, bv1 = bf + 3 * HID, wv2 = bv1 + 3 * VH, bv2 = wv2 + 3 * VH, w2r = bv2 + 4,
-                       w3r = w2r + 3 * DW2N, w3mv = w3r + DW3N, b23 = w3mv + 2 * 576, wcol = b23 + 24,
+                       w3r = w2r + 3 * DW2N, w3mv = w3r + DW3N, w2t = w3mv + 2 * 576, b23 = w2t + DW2N, wcol = b23 + 24,
                        gw2 = wcol + DW3N, gw3 = gw2 + DW2N, own = gw3 + 576, own2 = own + 4 * 128, red = own2 + 4 * 128,
                        g = red + 8 * 576, h = g + HID, dh = h + VH, dg = dh + VH, p16 = dg + HID, dp16 = p16 + 16,
                        scal = dp16 + 16, nzpos = scal + 64, nzval = nzpos + MAXNZ, ptab = nzval + MAXNZ,
@@ -223,55 +223,54 @@ __device__ __forceinline__ void block_sums(float (&x)[NV], float* scratch /* >= 
 }
 
 // ---- convolution pieces -----------------------------------------------------------------
+// Plane-major weight layout for the band convolutions: the NCO x 9 weights of input plane c
+// are wsrc[c * SPL + q * 9 + tap] (SPL a multiple of 4, 16-byte aligned rows), so one
+// plane's weights are 9 (NCO = 4) or 5 (NCO = 2) wave-uniform ds_read_b128 (a broadcast:
+// every lane reads the same 16 bytes) straight into VGPRs.  Index of the row-major
+// conv weight element (q, ci, tap) of a group's rows (NCI input planes) in that layout:
+template <int NCI>
+__device__ __forceinline__ int plane_major(int e) {
+  const int q = e / (NCI * 9), r = e - q * (NCI * 9), ci = r / 9;
+  return ci * 36 + q * 9 + (r - ci * 9);
+}
+
 // Band convolution: NCO output channels on the band's BH x C positions from the 8 * NCIW
-// input planes of BIG (8 waves split the planes), 1 x 2 output strips per lane.  The weight
-// of (input plane c, output channel q, tap) is wsrc[c * SPL + q * SQ + tap] (LDS); FLIP: the
-// transposed convolution's flipped taps.  Per input plane one LDS read gives each lane
-// one weight of the plane's NCO x 9, and readlane hands them to the FMAs as scalars.
-// Returns, for thread t < NCO * NPB, the sum of the 8 waves' partials (in wave order) of
-// channel t / NPB at band position t % NPB; other threads get 0.
+// input planes of BIG (8 waves split the planes), 1 x 2 output strips per lane as one
+// packed pair: per plane and (channel, tap) one v_pk_fma_f32 of the window pair with the
+// broadcast weight.  FLIP: the transposed convolution's flipped taps.  Returns, for thread
+// t < NCO * NPB, the sum of the 8 waves' partials (in wave order) of channel t / NPB at band
+// position t % NPB; other threads get 0.
 template <int R, int C, int NCO, int NCIW, bool FLIP>
 __device__ __forceinline__ float conv_band(const float* __restrict__ big, const float* __restrict__ wsrc, int SPL,
-                                           int SQ, float* red) {
+                                           float* red) {
   using L = Lay<R, C>;
-  constexpr int NSX = C / 2, NS = L::BH * NSX, NW = NCO * 9;
-  static_assert(NW <= 64, "one weight per lane per input plane");
+  constexpr int NSX = C / 2, NS = L::BH * NSX, NV4 = (NCO * 9 + 3) / 4;
   const int tid_ = tid_o();
   const int wv = tid_ >> 6, lane = tid_ & 63;
   const int sl = lane < NS ? lane : 0;  // lanes past the last strip redo strip 0 and store nothing
   const int sy = sl / NSX, sx = (sl - (sl / NSX) * NSX) * 2;
-  const int wq = lane < NW ? lane / 9 : 0, wt = lane < NW ? lane - (lane / 9) * 9 : 0;
-  const float* wbase = wsrc + wq * SQ + wt;  // lanes past NW read weight 0's slot (never used)
   const f32x2_t* pbase = reinterpret_cast<const f32x2_t*>(big + sy * L::RS + sx);
-  float acc[NCO][2];
+  f32x2_t acc[NCO];
 #pragma unroll
-  for (int q = 0; q < NCO; ++q) acc[q][0] = acc[q][1] = 0.f;
-  // software-pipelined over the wave's input planes: plane c + 1's weight and window are
-  // read from LDS before plane c's FMAs, so each LDS round trip hides behind the previous
-  // plane's 36 readlanes and 36 packed FMAs
-  f32x2_t win[6];
-  float wl;
-  {
-    const int ci = wv * NCIW;
-    wl = wbase[ci * SPL];
-    const f32x2_t* pl = pbase + ci * (L::PB / 2);
-#pragma unroll
-    for (int r = 0; r < 3; ++r) { win[2 * r] = pl[r * (L::RS / 2)]; win[2 * r + 1] = pl[r * (L::RS / 2) + 1]; }
-  }
+  for (int q = 0; q < NCO; ++q) acc[q] = f32x2_t{0.f, 0.f};
 #pragma unroll 1
   for (int c = 0; c < NCIW; ++c) {
-    float in[3][4];
+    const int ci = wv * NCIW + c;
+    const f32x4_t* wp = reinterpret_cast<const f32x4_t*>(wsrc + ci * SPL);
+    float wt[NV4 * 4];
+#pragma unroll
+    for (int i = 0; i < NV4; ++i) {
+      const f32x4_t x = wp[i];
+      wt[4 * i] = x.x; wt[4 * i + 1] = x.y; wt[4 * i + 2] = x.z; wt[4 * i + 3] = x.w;
+    }
+    const f32x2_t* pl = pbase + ci * (L::PB / 2);
+    f32x2_t pr[3][3];  // pr[ky][kx] = (in[ky][kx], in[ky][kx + 1])
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-      in[r][0] = win[2 * r].x; in[r][1] = win[2 * r].y; in[r][2] = win[2 * r + 1].x; in[r][3] = win[2 * r + 1].y;
-    }
-    const float wcur = wl;
-    if (c + 1 < NCIW) {  // wave-uniform
-      const int ci = wv * NCIW + c + 1;
-      wl = wbase[ci * SPL];
-      const f32x2_t* pl = pbase + ci * (L::PB / 2);
-#pragma unroll
-      for (int r = 0; r < 3; ++r) { win[2 * r] = pl[r * (L::RS / 2)]; win[2 * r + 1] = pl[r * (L::RS / 2) + 1]; }
+      const f32x2_t u0 = pl[r * (L::RS / 2)], u1 = pl[r * (L::RS / 2) + 1];
+      pr[r][0] = u0;
+      pr[r][1] = f32x2_t{u0.y, u1.x};
+      pr[r][2] = u1;
     }
 #pragma unroll
     for (int q = 0; q < NCO; ++q)
@@ -279,16 +278,15 @@ __device__ __forceinline__ float conv_band(const float* __restrict__ big, const 
       for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
-          const float wgt = rdl(wcur, q * 9 + (FLIP ? 8 - (ky * 3 + kx) : ky * 3 + kx));
-          acc[q][0] = fmaf(wgt, in[ky][kx], acc[q][0]);
-          acc[q][1] = fmaf(wgt, in[ky][kx + 1], acc[q][1]);
+          const float w = wt[q * 9 + (FLIP ? 8 - (ky * 3 + kx) : ky * 3 + kx)];
+          acc[q] = __builtin_elementwise_fma(f32x2_t{w, w}, pr[ky][kx], acc[q]);
         }
   }
   if (lane < NS) {
 #pragma unroll
     for (int q = 0; q < NCO; ++q) {
-      red[(wv * NCO + q) * L::NPB + sy * C + sx] = acc[q][0];
-      red[(wv * NCO + q) * L::NPB + sy * C + sx + 1] = acc[q][1];
+      red[(wv * NCO + q) * L::NPB + sy * C + sx] = acc[q].x;
+      red[(wv * NCO + q) * L::NPB + sy * C + sx + 1] = acc[q].y;
     }
   }
   __syncthreads();
@@ -529,8 +527,9 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
     for (int e = t; e < DW2N; e += NT) {
       const int g = CPG * cg * 288 + e;
       sm[L::w2r + e] = a.p[W2][g]; sm[L::w2r + DW2N + e] = a.m[W2][g]; sm[L::w2r + 2 * DW2N + e] = a.v[W2][g];
+      sm[L::w2t + plane_major<C1>(e)] = a.p[W2][g];
     }
-    for (int e = t; e < DW3N; e += NT) sm[L::w3r + e] = a.p[W3][CPG * cg * 576 + e];
+    for (int e = t; e < DW3N; e += NT) sm[L::w3r + plane_major<C2>(e)] = a.p[W3][CPG * cg * 576 + e];
     for (int e = t; e < 576; e += NT) {  // the own row's moments (channel 4cg + band)
       const int g = (CPG * cg + wg_band(w)) * 576 + e;
       sm[L::w3mv + e] = a.m[W3][g]; sm[L::w3mv + 576 + e] = a.v[W3][g];
@@ -588,7 +587,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
     __syncthreads();
     STAMP(15)
     {
-      const float z = conv_band<R, C, CPG, 4, false>(big, sm + L::w2r, 9, 288, red);
+      const float z = conv_band<R, C, CPG, 4, false>(big, sm + L::w2t, 36, red);
       if (t < CPG * NPB) {
         a2keep = fmaxf(z + sm[L::b23 + t / NPB], 0.f);
         sm[L::own + t] = a2keep;
@@ -603,8 +602,15 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
     // ======== P2: conv3 own channels, pool, fc_global partial ========
     f32x4_t a2v[BandQ<R, C>::MAXQ];
     band_issue<R, C>(a.ws + WS_A2, y0, a2v);
-    f32x4_t w3q = {0.f, 0.f, 0.f, 0.f};  // the group's conv3 rows as its 4 band workgroups published them
-    if (t < DW3N / 4) w3q = ld4_sc1(rsrc(a.p[W3], C3 * 576), CPG * cg * 576 + 4 * t);
+    // the group's conv3 rows as its 4 band workgroups published them: DW3N / 4 = 576 float4,
+    // 512 threads -> two loads for threads t < 64
+    static_assert(DW3N / 4 > NT && DW3N / 4 <= 2 * NT, "two float4 per thread cover the group's conv3 rows");
+    f32x4_t w3q[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    {
+      const __amdgpu_buffer_rsrc_t r3 = rsrc(a.p[W3], C3 * 576);
+      w3q[0] = ld4_sc1(r3, CPG * cg * 576 + 4 * t);
+      if (t + NT < DW3N / 4) w3q[1] = ld4_sc1(r3, CPG * cg * 576 + 4 * (t + NT));
+    }
     // value_head.0.weight as 8x8 blocks (rows 8 * (t >> 5) + r, columns 8 * (t & 31) + c):
     // both h = W g (reduced over the 32 column blocks of a half-wave) and dg = W^T dh
     // (over the 16 row blocks) stay cheap.  Issued behind the a2 band, in flight during conv3.
@@ -620,15 +626,19 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       }
     }
     band_commit<R, C>(big, y0, a2v);
-    if (t < DW3N / 4) {
-      sm[L::w3r + 4 * t] = w3q.x; sm[L::w3r + 4 * t + 1] = w3q.y; sm[L::w3r + 4 * t + 2] = w3q.z;
-      sm[L::w3r + 4 * t + 3] = w3q.w;
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {  // plane-major for conv_band
+      const int e = 4 * (t + h2 * NT);
+      if (e < DW3N) {
+        sm[L::w3r + plane_major<C2>(e)] = w3q[h2].x; sm[L::w3r + plane_major<C2>(e + 1)] = w3q[h2].y;
+        sm[L::w3r + plane_major<C2>(e + 2)] = w3q[h2].z; sm[L::w3r + plane_major<C2>(e + 3)] = w3q[h2].w;
+      }
     }
     __syncthreads();
     STAMP(12)
     STAMP(17)
     {
-      const float z = conv_band<R, C, CPG, 8, false>(big, sm + L::w3r, 9, 576, red);
+      const float z = conv_band<R, C, CPG, 8, false>(big, sm + L::w3r, 36, red);
       if (t < CPG * NPB) sm[L::own + t] = fmaxf(z + sm[L::b23 + 12 + t / NPB], 0.f);
     }
     __syncthreads();
@@ -841,7 +851,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
     STAMP(23)
     float da2 = 0.f;
     {
-      const float z = conv_band<R, C, CPG, 8, true>(big, sm + L::wcol, 36, 9, red);
+      const float z = conv_band<R, C, CPG, 8, true>(big, sm + L::wcol, 36, red);
       if (t < CPG * NPB) {
         da2 = a2keep > 0.f ? z : 0.f;
         sm[L::own2 + t] = da2;
@@ -943,7 +953,10 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       }
 #pragma unroll
       for (int k3 = 0; k3 < 3; ++k3)
-        if (t + k3 * NT < DW2N) sm[L::wcol + t + k3 * NT] = wc[k3];
+        if (t + k3 * NT < DW2N) {  // planes of 18 weights at a 20-float pitch (16-byte rows)
+          const int e = t + k3 * NT;
+          sm[L::wcol + e + 2 * (e / 18)] = wc[k3];
+        }
       band_commit<R, C>(big, y0, bv);
 #pragma unroll
       for (int k2 = 0; k2 < 2; ++k2)
@@ -953,7 +966,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
         if (t + k3 * NT < DW2N) sm[L::gw2 + t + k3 * NT] = g2[k3];
       __syncthreads();
       STAMP(25)
-      const float z = conv_band<R, C, 2, 8, true>(big, sm + L::wcol, 18, 9, red);
+      const float z = conv_band<R, C, 2, 8, true>(big, sm + L::wcol, 20, red);
       float da1 = 0.f;
       if (t < 2 * NPB) {
         const int j = t / NPB, pos = t - j * NPB, y = y0 + pos / C, x = pos - (pos / C) * C;
@@ -1089,13 +1102,16 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       float p2[3];
       STAMP(29)
       adam_lds<3>(sm + L::w2r, DW2N, t, sm + L::gw2, clip, a, ns, bc2s, p2);
+#pragma unroll
+      for (int k3 = 0; k3 < 3; ++k3)  // the conv copy (read by the next step's conv2 after B5's syncs)
+        if (t + k3 * NT < DW2N) sm[L::w2t + plane_major<C1>(t + k3 * NT)] = p2[k3];
       {  // the own conv3 row: params in w3r (row `band`), moments in w3mv
         float p3[2], m3[2], v3[2], g3v[2];
 #pragma unroll
         for (int k2 = 0; k2 < 2; ++k2) {
           const int e = t + k2 * NT;
           if (e < 576) {
-            p3[k2] = sm[L::w3r + band * 576 + e]; m3[k2] = sm[L::w3mv + e]; v3[k2] = sm[L::w3mv + 576 + e];
+            p3[k2] = sm[L::w3r + plane_major<C2>(band * 576 + e)]; m3[k2] = sm[L::w3mv + e]; v3[k2] = sm[L::w3mv + 576 + e];
             g3v[k2] = sm[L::gw3 + e];
           }
         }

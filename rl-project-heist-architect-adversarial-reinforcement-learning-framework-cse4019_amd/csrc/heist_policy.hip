@@ -161,20 +161,23 @@ __device__ __forceinline__ void conv2_pass(unsigned char* smem, const bf16x8* wl
     bf16x8 ring[kPre2];
 #pragma unroll
     for (int q = 0; q < kPre2; ++q) ring[q] = rd(q < NQ ? q : NQ - 1);
-    bf16x8 wcur = wl[0], wnext = wcur;
+    // weight fragments two k-steps ahead (a 3-slot ring); read one k-step ahead, their LDS
+    // latency was exposed at every k-step boundary (only NTP MFMAs after the read)
+    bf16x8 wb[3];
+    wb[0] = wl[0];
+    wb[1] = wl[64];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int s = q / NTP, i = q % NTP;
-      if (i == 0 && s + 1 < kW2Steps) wnext = wl[(s + 1) * 64];
+      if (i == 0 && s + 2 < kW2Steps) wb[(s + 2) % 3] = wl[(s + 2) * 64];
       const bf16x8 f = ring[q % kPre2];
       if (q + kPre2 < NQ) ring[q % kPre2] = rd(q + kPre2);
-      cur[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wcur, f, cur[i], 0, 0, 0);
-      if (i == NTP - 1) wcur = wnext;
+      cur[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[s % 3], f, cur[i], 0, 0, 0);
 #pragma unroll
       for (int r = 0; r < PER_Q; ++r)
         if (q * PER_Q + r < NPIECE) piece(q * PER_Q + r);
     }
-    __builtin_amdgcn_sched_group_barrier(0x100, kPre2 + 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, kPre2 + 2, 0);
     sched_ring<NTP, 1>(std::make_integer_sequence<int, NQ>{});
   } else {
 #pragma unroll
@@ -556,20 +559,23 @@ __device__ __forceinline__ void conv2_band_pass(unsigned char* smem, const bf16x
     bf16x8 ring[kPre2];
 #pragma unroll
     for (int q = 0; q < kPre2; ++q) ring[q] = rd(q < NQ ? q : NQ - 1);
-    bf16x8 wcur = wl[0], wnext = wcur;
+    // weight fragments two k-steps ahead (a 3-slot ring); read one k-step ahead, their LDS
+    // latency was exposed at every k-step boundary (only NTP MFMAs after the read)
+    bf16x8 wb[3];
+    wb[0] = wl[0];
+    wb[1] = wl[64];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int s = q / NTP, i = q % NTP;
-      if (i == 0 && s + 1 < kW2Steps) wnext = wl[(s + 1) * 64];
+      if (i == 0 && s + 2 < kW2Steps) wb[(s + 2) % 3] = wl[(s + 2) * 64];
       const bf16x8 f = ring[q % kPre2];
       if (q + kPre2 < NQ) ring[q % kPre2] = rd(q + kPre2);
-      cur[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wcur, f, cur[i], 0, 0, 0);
-      if (i == NTP - 1) wcur = wnext;
+      cur[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wb[s % 3], f, cur[i], 0, 0, 0);
 #pragma unroll
       for (int r = 0; r < PER_Q; ++r)
         if (q * PER_Q + r < NPIECE) piece(q * PER_Q + r);
     }
-    __builtin_amdgcn_sched_group_barrier(0x100, kPre2 + 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, kPre2 + 2, 0);
     sched_ring<NTP, 1>(std::make_integer_sequence<int, NQ>{});
   } else {
 #pragma unroll

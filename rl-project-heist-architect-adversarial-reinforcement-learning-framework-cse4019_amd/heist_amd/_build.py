@@ -29,7 +29,9 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # single-tick step kernel drops from 64 VGPRs + 3 spilled to 53 with none.
 # HEIST_ENV_FLAGS replaces this list (A/B builds).
 FILE_FLAGS = {"heist_env.hip": os.environ.get("HEIST_ENV_FLAGS", "-fno-slp-vectorize -mllvm -disable-machine-licm").split(),
-              "heist_policy.hip": os.environ.get("HEIST_POLICY_FLAGS", "").split(),  # A/B builds of the policy kernels
+              # no SLP: packed-fp32 VALU beside MFMAs costs issue slots (MI355X_MICROARCH.md);
+              # solver_conv_kernel<20,20> 19.9K -> 19.2K cycles per env (r04r stamps)
+              "heist_policy.hip": os.environ.get("HEIST_POLICY_FLAGS", "-fno-slp-vectorize").split(),  # A/B builds
               # the persistent Architect update: machine LICM would keep loop-invariant scalars of
               # every phase live across the whole step loop (SGPR spills 267 -> 132 without it)
               "heist_arch_update.hip": ["-mllvm", "-disable-machine-licm"]}

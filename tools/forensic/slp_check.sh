@@ -17,9 +17,18 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 LIB=tools/forensic/_ref/libheist_hip_slp.so
 [ -f $LIB ] || { echo "missing $LIB"; exit 1; }
+# llvm-objdump --offloading only EXTRACTS the device bundles (next to the input file), so
+# extract from a copy in a scratch directory and disassemble the gfx950 objects
 for f in rl-project-heist-architect-adversarial-reinforcement-learning-framework-cse4019_amd/heist_amd/libheist_hip.so $LIB; do
-  n=$(/opt/rocm/lib/llvm/bin/llvm-objdump -d --offloading "$f" 2>/dev/null | grep -c "v_pk_fma_f32\|v_pk_mul_f32\|v_pk_add_f32" || true)
-  echo "$f: packed-fp32 instructions in the device code: $n" | tee -a $OUT/slp_isa_counts.txt
+  d=$(mktemp -d) && cp "$f" $d/lib.so && (cd $d && /opt/rocm/lib/llvm/bin/llvm-objdump --offloading lib.so > /dev/null 2>&1)
+  n=0
+  for o in $d/lib.so.*gfx950; do
+    /opt/rocm/lib/llvm/bin/llvm-readelf -s "$o" 2>/dev/null | grep -q step_lean_kernel || continue  # heist_env.hip's object
+    # v_pk_fma_f32 also comes from the raycast's one deliberate inline-asm packed FMA
+    n=$(/opt/rocm/lib/llvm/bin/llvm-objdump -d "$o" | grep -o "v_pk_[a-z]*_f32" | sort | uniq -c | tr -s ' \n' ' ')
+  done
+  echo "$f: packed-fp32 instructions in heist_env's device code: $n" | tee -a $OUT/slp_isa_counts.txt
+  rm -rf $d
 done
 HEIST_LIB=$PWD/$LIB timeout -k 10 600 python -u -m pytest tests/test_gpu_env.py -m gpu -q --timeout 300 \
   --timeout-method thread -k "golden_trace or cones_bit_exact or cones_fast_equals_exact or fast_direction or full_size_sampled" \

@@ -25,8 +25,9 @@
 //       value_head.0.weight rides in registers); dp (own 16 pool cells) = Wf[:, own]^T dg;
 //       da3[4 ch][band]; dW3 and db3 partials over the band; dWf own; dWv1 own slice      -> B3
 //   P4  da2[4 ch][band] = (conv3^T da3) * (a2 > 0); dW2 / db2 partials over the band      -> B4
+//   P4  (also: the own conv3 row's dW3 and the group's db3, sums of their 4 band partials)
 //   P5  da1[2 ch][band] = (conv2^T da2) * (a1 > 0); partial dW1 / db1; the group's dW2 /
-//       dW3 / db2 / db3 (sum of its 4 bands); per-tensor sums of squares                  -> B5
+//       db2 (sum of its 4 bands); per-tensor sums of squares                              -> B5
 //   P6  clip coefficient from the 12 tensor norms (norm of norms, as clip_grad_norm_);
 //       Adam on every owned / redundant tensor: band b updates and publishes the conv3 row
 //       of its group's channel b (the group reloads its 4 rows after the next step's B1);
@@ -327,6 +328,38 @@ __device__ __forceinline__ void wgrad(const float* __restrict__ big, int ci, int
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) acc[ky * 3 + kx] = fmaf(dd, col[x + kx][ky], acc[ky * 3 + kx]);
     }
+  }
+}
+
+// wgrad for two output channels at once: acc[tap] = (channel-0, channel-1) partials over NY
+// band rows from ya and NX columns from xa; one load of the input window feeds both channels
+// (a packed FMA of the (d0, d1) pair with the broadcast window value).
+template <int R, int C, int NY, int NX>
+__device__ __forceinline__ void wgrad2(const float* __restrict__ big, int ci, int ya, int xa,
+                                       const float* __restrict__ d0, const float* __restrict__ d1, f32x2_t (&acc)[9]) {
+  using L = Lay<R, C>;
+  constexpr int RS = L::RS;
+#pragma unroll 1
+  for (int yy = 0; yy < NY; ++yy) {
+    const int y = ya + yy;
+    const float* pl = big + ci * L::PB + y * RS + xa;
+    float col[NX + 2][3];
+#pragma unroll
+    for (int x = 0; x < NX + 2; ++x) {
+      col[x][0] = pl[x]; col[x][1] = pl[RS + x]; col[x][2] = pl[2 * RS + x];
+    }
+    f32x2_t dd[NX];
+#pragma unroll
+    for (int x = 0; x < NX; ++x) dd[x] = f32x2_t{d0[y * C + xa + x], d1[y * C + xa + x]};
+#pragma unroll
+    for (int x = 0; x < NX; ++x)
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          const float v = col[x + kx][ky];
+          acc[ky * 3 + kx] = __builtin_elementwise_fma(dd[x], f32x2_t{v, v}, acc[ky * 3 + kx]);
+        }
   }
 }
 
@@ -785,14 +818,24 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
     __syncthreads();
     store_band<R, C>(a.ws + WS_DA3, sm + L::own, cg, band);
     STAMP(22)
-    {  // dW3 partial over the band: lanes = input planes, waves = (channel, column half)
-      float acc[9];
+    {  // dW3 partial over the band: lanes = input planes, waves = (channel pair, column quarter);
+       // the column quarters are summed (q0 + q2) + (q1 + q3) through red
+      f32x2_t acc[9];
 #pragma unroll
-      for (int j = 0; j < 9; ++j) acc[j] = 0.f;
-      const int q = wv & 3, xh = wv >> 2;
-      wgrad<R, C, BH, C / 2>(big, lane, 0, xh * (C / 2), sm + L::own + q * NPB, acc);
+      for (int j = 0; j < 9; ++j) acc[j] = f32x2_t{0.f, 0.f};
+      const int qp = wv & 1, xq = wv >> 1;
+      wgrad2<R, C, BH, C / 4>(big, lane, 0, xq * (C / 4), sm + L::own + (2 * qp) * NPB,
+                              sm + L::own + (2 * qp + 1) * NPB, acc);
+      float* slot = red + (xq & 1) * DW3N + (2 * qp) * 576 + lane * 9;
+      if (xq < 2) {
 #pragma unroll
-      for (int j = 0; j < 9; ++j) red[xh * DW3N + q * 576 + lane * 9 + j] = acc[j];
+        for (int j = 0; j < 9; ++j) { slot[j] = acc[j].x; slot[576 + j] = acc[j].y; }
+      }
+      __syncthreads();
+      if (xq >= 2) {
+#pragma unroll
+        for (int j = 0; j < 9; ++j) { slot[j] = slot[j] + acc[j].x; slot[576 + j] = slot[576 + j] + acc[j].y; }
+      }
       __syncthreads();
       STAMP(16)
       float* dst = a.ws + WS_DW3 + w * DW3R;
@@ -842,10 +885,26 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       }
       f32x4_t bv[BandQ<R, C>::MAXQ];
       band_issue<R, C>(a.ws + WS_DA3, y0, bv);
+      // the own conv3 row's gradient (channel 4cg + band: its 4 band partials, band order) and
+      // the group's db3, both complete at B3: read here, beside this phase's other loads
+      const __amdgpu_buffer_rsrc_t rd3 = rsrc(a.ws + WS_DW3, NWG * DW3R);
+      float pb3[2][4];
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          pb3[k2][b] = t + k2 * NT < 576 ? ld1_sc1(rd3, wg_of(cg, b) * DW3R + band * 576 + t + k2 * NT) : 0.f;
+      float pdb[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) pdb[b] = t < CPG ? ld1_sc1(rd3, wg_of(cg, b) * DW3R + DW3N + t) : 0.f;
 #pragma unroll
       for (int k5 = 0; k5 < 5; ++k5)
         if (t + k5 * NT < DW3N) sm[L::wcol + t + k5 * NT] = wc[k5];
       band_commit<R, C>(big, y0, bv);
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2)
+        if (t + k2 * NT < 576) sm[L::gw3 + t + k2 * NT] = ((pb3[k2][0] + pb3[k2][1]) + pb3[k2][2]) + pb3[k2][3];
+      if (t < CPG) scal[S_DB3 + t] = ((pdb[0] + pdb[1]) + pdb[2]) + pdb[3];
     }
     __syncthreads();
     STAMP(23)
@@ -902,8 +961,8 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
     // ======== P5: da1 (2 channels on the band), partial dW1 / db1, the group's weight
     // gradients, norm records ========
     {
-      // one round trip: conv2 weight columns (wcol[ci * 18 + j * 9 + tap] = W2[ci][2cg + j][tap]),
-      // the group's dW3 / dW2 / db3 / db2 band partials and the da2 band
+      // one round trip: conv2 weight columns (wcol[ci * 20 + j * 9 + tap] = W2[ci][2cg + j][tap]),
+      // the group's dW2 / db2 band partials and the da2 band
       const __amdgpu_buffer_rsrc_t rw2 = rsrc(a.p[W2], C2 * 288);
       float wc[3];
 #pragma unroll
@@ -914,22 +973,9 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       }
       f32x4_t bv[BandQ<R, C>::MAXQ];
       band_issue<R, C>(a.ws + WS_DA2, y0, bv);
-      // the group's dW3 / dW2 (sum of its 4 bands' partials, band order) and db2 / db3
-      const __amdgpu_buffer_rsrc_t r3 = rsrc(a.ws + WS_DW3, NWG * DW3R), r2 = rsrc(a.ws + WS_DW2, NWG * DW2R);
-      float g3[2], g2[3];
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2) {  // the own conv3 row (channel 4cg + band)
-        const int e = t + k2 * NT;
-        float sacc = 0.f;
-        if (e < 576) {
-          float pb[4];
-#pragma unroll
-          for (int b = 0; b < 4; ++b) pb[b] = ld1_sc1(r3, wg_of(cg, b) * DW3R + band * 576 + e);
-#pragma unroll
-          for (int b = 0; b < 4; ++b) sacc += pb[b];
-        }
-        g3[k2] = sacc;
-      }
+      // the group's dW2 (sum of its 4 bands' partials, band order) and db2
+      const __amdgpu_buffer_rsrc_t r2 = rsrc(a.ws + WS_DW2, NWG * DW2R);
+      float g2[3];
 #pragma unroll
       for (int k3 = 0; k3 < 3; ++k3) {
         const int e = t + k3 * NT;
@@ -943,13 +989,11 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
         }
         g2[k3] = sacc;
       }
-      if (t < 2 * CPG) {
-        const int which = t >> 2, q = t & 3;  // 0: db3, 1: db2
+      if (t < CPG) {  // db2 (db3 was summed in P4)
         float pb[4];
 #pragma unroll
-        for (int b = 0; b < 4; ++b)
-          pb[b] = which == 0 ? ld1_sc1(r3, wg_of(cg, b) * DW3R + DW3N + q) : ld1_sc1(r2, wg_of(cg, b) * DW2R + DW2N + q);
-        scal[(which == 0 ? S_DB3 : S_DB2) + q] = ((pb[0] + pb[1]) + pb[2]) + pb[3];
+        for (int b = 0; b < 4; ++b) pb[b] = ld1_sc1(r2, wg_of(cg, b) * DW2R + DW2N + t);
+        scal[S_DB2 + t] = ((pb[0] + pb[1]) + pb[2]) + pb[3];
       }
 #pragma unroll
       for (int k3 = 0; k3 < 3; ++k3)
@@ -958,9 +1002,6 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
           sm[L::wcol + e + 2 * (e / 18)] = wc[k3];
         }
       band_commit<R, C>(big, y0, bv);
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2)
-        if (t + k2 * NT < 576) sm[L::gw3 + t + k2 * NT] = g3[k2];
 #pragma unroll
       for (int k3 = 0; k3 < 3; ++k3)
         if (t + k3 * NT < DW2N) sm[L::gw2 + t + k3 * NT] = g2[k3];
@@ -991,7 +1032,10 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       x[2] = 0.f; x[3] = 0.f;
 #pragma unroll
       for (int k2 = 0; k2 < 2; ++k2)
-        if (t + k2 * NT < 576) x[2] = fmaf(g3[k2], g3[k2], x[2]);
+        if (t + k2 * NT < 576) {
+          const float g3 = sm[L::gw3 + t + k2 * NT];
+          x[2] = fmaf(g3, g3, x[2]);
+        }
 #pragma unroll
       for (int k3 = 0; k3 < 3; ++k3) {
         const int e = t + k3 * NT;
@@ -1046,14 +1090,13 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
             red[wg_of(g, 3) * REC + o];
     }
     {
-      float own_sum = 0.f;
-      if (t < 6) {  // sums over the 64 records, in workgroup order
-        for (int q = 0; q < NWG; ++q) own_sum += red[q * REC + t];
-      }
+      // sums over the 64 records of slots 0..5: wave v sums slot v (lane = record; the same
+      // DPP association in every workgroup)
+      float own_sum = wv < 6 ? sum64(red[lane * REC + wv]) : 0.f;
       __syncthreads();  // red (records) is reused as the reduction scratch below
       float x[2] = {gw1 * gw1, gb1 * gb1};
       block_sums<2>(x, red);
-      if (t < 6) scal[S_RED8 + t] = own_sum;
+      if (wv < 6 && lane == 0) scal[S_RED8 + wv] = own_sum;
       __syncthreads();
       if (t == 0) {
         const float S[NTENS] = {x[0], x[1], scal[S_RED8 + NP_W2], scal[S_RED8 + NP_B2], scal[S_RED8 + NP_W3],

@@ -248,18 +248,17 @@ def test_architect_update_long_sequence_drift(gpu_device, monkeypatch):
     """A full iteration's Architect sequence (3,841 single-reward updates, the count of
     profiles/r03l_probe_train.log) from the nets.npz weights, through the persistent kernel
     and through the HIP-graph replay, against the same sequence of eager update() calls
-    (agents/architect.py:91-155), and eager against a second eager run.  Rewards come from
-    the table the training loop produces (kat.json architect_reward values and the
-    invalid-layout -1, rewards.py:43-73).
+    (agents/architect.py:91-155), all three measured against the same updates in float64.
+    Rewards come from the table the training loop produces (kat.json architect_reward values
+    and the invalid-layout -1, rewards.py:43-73).
 
-    What holds (profiles/r04h_probe_arch_drift.log, r04p): the kernel is bit-for-bit
-    deterministic; the eager path is not (two eager runs can part: MIOpen's backward
-    reductions), and fp32 rounding differences get amplified wherever Adam meets a unit
-    crossing its ReLU boundary at a different step, so single weights part by up to ~60 lr
-    (0.017 measured, whichever pair is compared) and stay there.  The function the network
-    computes does not drift: V(s0) and the value loss track eager to 1.7e-5 at the end
-    (1.4e-4 worst checkpoint).  Asserted: weights within 0.05 (~ lr x sqrt(k)), V(s0) within
-    5e-4, the final value loss within 5e-4 relative, for the kernel and the graph replay."""
+    fp32 rounding differences get amplified wherever Adam meets a unit crossing its ReLU
+    boundary at a different step: single weights part by tens to hundreds of lr and stay
+    there, whichever fp32 summation order runs (eager, graph, kernel), while the function the
+    network computes does not drift.  So the bar is "as accurate as eager fp32": V(s0) and the
+    value loss within max(5e-4, 5x eager's own error) of float64, weights within
+    max(0.1, 3x eager's worst weight error); and the kernel bit-for-bit deterministic."""
+    import torch.nn.functional as F
     n_sd = gd.load("nets.npz")
     sd = {k[len("architect/"):]: torch.from_numpy(n_sd[k]) for k in n_sd.files if k.startswith("architect/")}
     table = sorted(set(float(v) for v in gd.load_json("kat.json")["architect_reward"].values())) + [-1.0]
@@ -273,36 +272,46 @@ def test_architect_update_long_sequence_drift(gpu_device, monkeypatch):
         a.network.load_state_dict(sd)
         return a
 
-    def vs0(a):
+    def vs0(net, x):
         with torch.no_grad():
-            return float(a.network.value(a.grid_state()))
+            return float(net.value(x.to(next(net.parameters()).dtype)))
 
-    def eager():
-        e = agent()
-        for i in range(k):
-            e.log_probs = [torch.tensor(float(lp[i]), device=gpu_device)]
-            e.values = [torch.tensor(float(v[i]), device=gpu_device)]
-            e.rewards = [float(r[i])]
-            me = e.update(collective=False)
-        return e, me
+    # float64: one Adam step on value_coeff * (V(s0) - r_i)^2 per update, clip 0.5 (_step)
+    ref = agent()
+    net64 = ref.network.double()
+    opt64 = torch.optim.Adam(net64.parameters(), lr=ref.optimizer.param_groups[0]["lr"])
+    x0 = ref.grid_state()
+    for i in range(k):
+        opt64.zero_grad()
+        mse64 = F.mse_loss(net64.value(x0.double()).squeeze(),
+                           torch.tensor(float(r[i]), dtype=torch.float64, device=gpu_device))
+        (ref.value_coeff * mse64).backward()
+        torch.nn.utils.clip_grad_norm_(list(net64.parameters()), 0.5)
+        opt64.step()
+    v64, l64 = vs0(net64, x0), float(mse64.detach())  # update()'s architect_value_loss: the mse
 
-    def maxdiff(a, b):
-        return max(float((p - q).abs().max()) for p, q in zip(a.network.parameters(), b.network.parameters()))
+    def errs(net, loss):
+        w = max(float((p.detach().double() - q.detach()).abs().max()) for p, q in zip(net.parameters(), net64.parameters()))
+        return w, abs(vs0(net, x0) - v64), abs(loss - l64)
 
-    e, me = eager()
-    e2, _ = eager()
-    print("eager vs eager after %d updates: max |param diff| %.3g, |V(s0) diff| %.3g"
-          % (k, maxdiff(e, e2), abs(vs0(e) - vs0(e2))))
+    e = agent()
+    for i in range(k):
+        e.log_probs = [torch.tensor(float(lp[i]), device=gpu_device)]
+        e.values = [torch.tensor(float(v[i]), device=gpu_device)]
+        e.rewards = [float(r[i])]
+        me = e.update(collective=False)
+    ew, ev, el = errs(e.network, me["architect_value_loss"])
+    print("eager fp32 vs float64 after %d updates: max |param err| %.3g, |V(s0) err| %.3g, |loss err| %.3g"
+          % (k, ew, ev, el))
     for mode in ("kernel", "graph"):
         monkeypatch.setenv("HEIST_ARCH_UPDATE", mode)
         ag = agent()
         m = ag.update_sequence(lp, v, r)
-        worst, dv = maxdiff(ag, e), abs(vs0(ag) - vs0(e))
-        print("%s vs eager: max |param diff| %.3g after %d updates; |V(s0) diff| %.3g; value loss %.9g vs %.9g"
-              % (mode, worst, k, dv, m["architect_value_loss"], me["architect_value_loss"]))
-        assert worst <= 0.05, (mode, worst)
-        assert dv <= 5e-4, (mode, dv)
-        assert abs(m["architect_value_loss"] - me["architect_value_loss"]) <= 5e-4 * max(1.0, me["architect_value_loss"])
+        w, dv, dl = errs(ag.network, m["architect_value_loss"])
+        print("%s vs float64: max |param err| %.3g, |V(s0) err| %.3g, |loss err| %.3g" % (mode, w, dv, dl))
+        assert dv <= max(5e-4, 5 * ev), (mode, dv, ev)
+        assert dl <= max(5e-4, 5 * el) * max(1.0, l64), (mode, dl, el)
+        assert w <= max(0.1, 3 * ew), (mode, w, ew)
         if mode == "kernel":  # bit-for-bit deterministic
             b = agent()
             b.update_sequence(lp, v, r)

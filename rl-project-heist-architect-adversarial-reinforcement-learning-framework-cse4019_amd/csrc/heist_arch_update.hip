@@ -1123,12 +1123,28 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       if (t < C1) red[288 + t] = gb1;
       if (t < VH) red[320 + t] = dv * sm[L::h + t];
       __syncthreads();
-      float po[1];
-      adam_lds<1>(sm + L::w1, 288, t, red, clip, a, ns, bc2s, po);
-      adam_lds<1>(sm + L::b1, 32, t, red + 288, clip, a, ns, bc2s, po);
-      adam_lds<1>(sm + L::bf, HID, t, sm + L::dg, clip, a, ns, bc2s, po);
-      adam_lds<1>(sm + L::bv1, VH, t, sm + L::dh, clip, a, ns, bc2s, po);
-      adam_lds<1>(sm + L::wv2, VH, t, red + 320, clip, a, ns, bc2s, po);
+      {  // the five as one index space (conv1 w | b, fc_global.bias, value_head.0.bias,
+         // value_head.2.weight: 832 elements, two per thread): two LDS round trips instead of five
+        constexpr int NSM = C1 * 9 + C1 + HID + VH + VH;
+        static_assert(NSM <= 2 * NT, "two small-tensor elements per thread");
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int u = t + j * NT;
+          float* bp;
+          const float* gp;
+          int nn, ee;
+          if (u < 288) { bp = sm + L::w1; nn = 288; gp = red; ee = u; }
+          else if (u < 320) { bp = sm + L::b1; nn = C1; gp = red + 288; ee = u - 288; }
+          else if (u < 576) { bp = sm + L::bf; nn = HID; gp = sm + L::dg; ee = u - 320; }
+          else if (u < 704) { bp = sm + L::bv1; nn = VH; gp = sm + L::dh; ee = u - 576; }
+          else { bp = sm + L::wv2; nn = VH; gp = red + 320; ee = u - 704; }
+          if (u < NSM) {
+            float pp = bp[ee], mm = bp[nn + ee], vv = bp[2 * nn + ee];
+            adam(pp, mm, vv, gp[ee], clip, a, ns, bc2s);
+            bp[ee] = pp; bp[nn + ee] = mm; bp[2 * nn + ee] = vv;
+          }
+        }
+      }
       if (t == 0) {
         float p = sm[L::bv2], m = sm[L::bv2 + 1], v = sm[L::bv2 + 2];
         adam(p, m, v, dv, clip, a, ns, bc2s);

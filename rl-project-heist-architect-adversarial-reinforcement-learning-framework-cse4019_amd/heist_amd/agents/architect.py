@@ -31,7 +31,11 @@ class TensorSeq(list):
     the reference keeps them, that can also take a whole batch of transitions (a 1-D tensor)
     without splitting it.  A batch is cut into per-element views only when the list is read
     element-wise; stacked(k) gives the first k entries as one tensor without that cut (the
-    training loop's path: 3,800 views per iteration cost ~40 ms of host time)."""
+    training loop's path: 3,800 views per iteration cost ~40 ms of host time).  torch's C++
+    argument parser reads a list's storage directly (torch.stack(buf) sees only the entries
+    already cut), so every path that hands the buffers out materializes them first
+    (materialize(); AdversarialTrainer._score_finished, callbacks); only train_iteration,
+    which consumes them itself through stacked(k), keeps batches whole."""
 
     def __init__(self, *a):
         super().__init__(*a)
@@ -45,6 +49,10 @@ class TensorSeq(list):
             pend, self._pending = self._pending, []
             for t in pend:
                 list.extend(self, t.unbind(0))
+
+    def materialize(self):
+        """Cut pending batches into per-element entries (the list then holds everything)."""
+        self._flush()
 
     def __len__(self):
         return list.__len__(self) + sum(int(t.shape[0]) for t in self._pending)

@@ -403,8 +403,17 @@ class AdversarialTrainer:  # training.py:115-790
         return ro, st["sel"]
 
     def _score_finished(self, overrides: Optional[dict] = None) -> np.ndarray:
-        """Score every env whose layout has had its A attempts; returns those env ids."""
-        return self._score_commit(self._score_prepare(), overrides)
+        """Score every env whose layout has had its A attempts; returns those env ids.  The
+        Architect's transition buffers are left as plain per-element lists (torch.stack on
+        them sees every entry); train_iteration's own path keeps the batches whole."""
+        ids = self._score_commit(self._score_prepare(), overrides)
+        self._materialize_transitions()
+        return ids
+
+    def _materialize_transitions(self):
+        for buf in (self.architect.log_probs, self.architect.values):
+            if hasattr(buf, "materialize"):
+                buf.materialize()
 
     def _score_prepare(self):
         """The device half of scoring: which envs finished their A attempts, their statistics
@@ -450,6 +459,8 @@ class AdversarialTrainer:  # training.py:115-790
         if not ov.get("freeze_architect", False) and not self.warmup:
             self.architect.store_transitions(lp_fin, v_fin, ars)
             self._arch_eps.extend(int(self.b_episode[e]) for e in ids)
+            if self._callback is not None:  # user code may read the buffers
+                self._materialize_transitions()
         self.b_scored[fin] = True
         return (ids, log) if defer_log else ids
 

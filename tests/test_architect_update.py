@@ -394,3 +394,8 @@ def test_transition_buffer_batches_read_as_lists():
     ag = ArchitectAgent(grid_rows=12, grid_cols=12, device=torch.device("cpu"))
     ag.store_transitions(torch.tensor([0.1, 0.2]), torch.tensor([[0.3], [0.4]]), [1.0, -1.0])
     assert len(ag.log_probs) == 2 and abs(float(ag.values[1]) - 0.4) < 1e-7 and ag.rewards == [1.0, -1.0]
+    # torch's argument parser reads the list storage itself: materialize() first
+    u = TensorSeq()
+    u.add_batch(torch.tensor([7.0, 8.0]))
+    u.materialize()
+    assert torch.equal(torch.stack(u), torch.tensor([7.0, 8.0]))

@@ -238,9 +238,10 @@ int heist_arch_update_sequence(float* const* params, float* const* exp_avg, floa
 /* 1 in *timed_out if a grid barrier of the last launch on `workspace` gave up waiting
  * (workgroups not co-resident; its results are then invalid).  Synchronises `stream`. */
 int heist_arch_update_timed_out(const void* workspace, int* timed_out, heist_stream_t stream);
-/* Instrumentation, no reference counterpart: with buf a device array of 2 * 16 * 32 uint64,
- * later heist_arch_update_sequence launches record s_memrealtime (100 MHz) at up to 32 phase points
- * of steps 0..15 in workgroups 0 and 63 (tools/probe_arch_update.py); NULL: off (default). */
+/* Instrumentation, no reference counterpart: with buf a device array of 2 * 16 * 32 + 16 * 5 * 64
+ * uint64, later heist_arch_update_sequence launches record s_memrealtime (100 MHz) at up to 32
+ * phase points of steps 0..15 in workgroups 0 and 63, then every workgroup's arrival (stores
+ * drained) at each of the 5 grid barriers of steps 0..15 (tools/probe_arch_update.py); NULL: off. */
 int heist_arch_update_stamps(uint64_t* buf);
 
 /* Replaces SolverAgent._compute_gae + returns (agents/solver.py:142-143, :228-244) on a

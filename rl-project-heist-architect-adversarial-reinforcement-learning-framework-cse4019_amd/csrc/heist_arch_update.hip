@@ -177,13 +177,17 @@ __device__ __forceinline__ float sum64(float x) { return swap32_add(sum32(x)); }
 // stores, the workgroup meets, one lane adds to the monotonic counter and polls it with a
 // relaxed sc1 load.  The spin is bounded: on a timeout (co-residency lost) the flag is set,
 // the host reports it, and later barriers stop waiting so the grid still drains.
-__device__ __forceinline__ void grid_barrier(unsigned* ctr, unsigned idx, float* scal) {
+__device__ __forceinline__ void grid_barrier(unsigned* ctr, unsigned idx, float* scal,
+                                             unsigned long long* ready = nullptr) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
+    if (ready) *ready = __builtin_amdgcn_s_memrealtime();  // instrumentation: every wave drained
     __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned target = (idx + 1u) * (unsigned)NWG;
     if (scal[S_TIMEOUT] == 0.f) {
+      // one poll in flight (4 in flight, ~0.2 us apart, measured slower: 51.4 -> 54.4 us per
+      // update, the 64 pollers' traffic on the counter's line delays the arrivals, r04y)
       unsigned spins = 0;
       while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
@@ -526,6 +530,9 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
 #define STAMP(i)                                                                                          \
   if (a.stamps && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == NWG - 1) && s < 16)               \
     a.stamps[((blockIdx.x == 0 ? 0 : 1) * 16 + s) * 32 + (i)] = __builtin_amdgcn_s_memrealtime();
+  // READY(b): every workgroup's time at barrier b of steps < 16, once its waves have drained
+  // their stores (after stamp slot 1024: [16 steps][5 barriers][64 workgroups])
+#define READY(b) (a.stamps && s < 16 ? a.stamps + 1024 + (s * 5 + (b)) * NWG + blockIdx.x : nullptr)
 
   // ---- setup: zero BIG + XP (pads and out-of-image halo rows stay zero), load parameters ----
   {
@@ -629,7 +636,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       store_band<R, C>(a.ws + WS_A2, sm + L::own, cg, band);
     }
     STAMP(1)
-    grid_barrier(ctr, bar++, scal);
+    grid_barrier(ctr, bar++, scal, READY(0));
     STAMP(2)
 
     // ======== P2: conv3 own channels, pool, fc_global partial ========
@@ -699,7 +706,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       if (fhf == 0) st_sc1(a.ws + WS_GP + w * HID + fi, gp);
     }
     STAMP(3)
-    grid_barrier(ctr, bar++, scal);
+    grid_barrier(ctr, bar++, scal, READY(1));
     STAMP(4)
 
     // ======== P3: value head (redundant), dp / da3 / dW3 / dWf / dWv1 (owned) ========
@@ -869,7 +876,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       }
     }
     STAMP(5)
-    grid_barrier(ctr, bar++, scal);
+    grid_barrier(ctr, bar++, scal, READY(2));
     STAMP(6)
 
     // ======== P4: da2 own channels (conv3^T), dW2 / db2 partials ========
@@ -955,7 +962,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       if (t < 32) st_sc1(a.ws + WS_DW2 + w * DW2R + DW2N + t, t < CPG ? x[t] : 0.f);
     }
     STAMP(7)
-    grid_barrier(ctr, bar++, scal);
+    grid_barrier(ctr, bar++, scal, READY(3));
     STAMP(8)
 
     // ======== P5: da1 (2 channels on the band), partial dW1 / db1, the group's weight
@@ -1067,7 +1074,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       }
     }
     STAMP(9)
-    grid_barrier(ctr, bar++, scal);
+    grid_barrier(ctr, bar++, scal, READY(4));
     STAMP(10)
 
     // ======== P6: clip coefficient, Adam, publish ========
@@ -1199,6 +1206,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
     STAMP(11)
   }
 #undef STAMP
+#undef READY
 
   // ---- write back what stayed on chip (tensor pointers from the LDS table: the kernel
   // arguments need not stay live in SGPRs across the step loop) ----

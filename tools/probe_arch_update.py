@@ -50,12 +50,25 @@ def timed(mode, sd, r, lp, v, reps=3):
 def stamps(sd, r, lp, v):
     os.environ["HEIST_ARCH_UPDATE"] = "kernel"
     ag = agent(sd)
-    buf = torch.zeros(2 * 16 * 32, dtype=torch.int64, device="cuda")
+    buf = torch.zeros(2 * 16 * 32 + 16 * 5 * 64, dtype=torch.int64, device="cuda")
     _native.lib().heist_arch_update_stamps(_native.ptr(buf))
     ag.update_sequence(lp[:16], v[:16], r[:16])
     torch.cuda.synchronize()
     _native.lib().heist_arch_update_stamps(None)
-    st = buf.cpu().numpy().reshape(2, 16, 32).astype(np.float64) * 10e-3  # 100 MHz ticks -> us
+    allst = buf.cpu().numpy().astype(np.float64) * 10e-3  # 100 MHz ticks -> us
+    st = allst[:1024].reshape(2, 16, 32)
+    ready = allst[1024:].reshape(16, 5, 64)
+    exit_slot = (2, 4, 6, 8, 10)
+    print("barriers (steps 1..15, median): skew = last - first workgroup ready (stores drained); "
+          "release = workgroup 0 leaving - last ready; slowest workgroups", flush=True)
+    for b in range(5):
+        rd = ready[1:, b, :]
+        skew = np.median(rd.max(1) - rd.min(1))
+        rel = np.median(st[0, 1:, exit_slot[b]] - rd.max(1))
+        late = np.bincount(rd.argmax(1), minlength=64).argsort()[::-1][:4]
+        wg0_wait = np.median(rd.max(1) - rd[:, 0])
+        print("   B%d  skew %5.2f  release %5.2f  wg0 waits %5.2f for the last  slowest wgs %s"
+              % (b + 1, skew, rel, wg0_wait, list(late)), flush=True)
     for wi, wname in enumerate(("wg0", "wg63")):
         step = np.median(st[wi, 2:, 0] - st[wi, 1:-1, 0])
         print("%s step %.2f us:" % (wname, step), flush=True)

@@ -651,9 +651,19 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       w3q[0] = ld4_sc1(r3, CPG * cg * 576 + 4 * t);
       if (t + NT < DW3N / 4) w3q[1] = ld4_sc1(r3, CPG * cg * 576 + 4 * (t + NT));
     }
+    band_commit<R, C>(big, y0, a2v);
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {  // plane-major for conv_band
+      const int e = 4 * (t + h2 * NT);
+      if (e < DW3N) {
+        sm[L::w3r + plane_major<C2>(e)] = w3q[h2].x; sm[L::w3r + plane_major<C2>(e + 1)] = w3q[h2].y;
+        sm[L::w3r + plane_major<C2>(e + 2)] = w3q[h2].z; sm[L::w3r + plane_major<C2>(e + 3)] = w3q[h2].w;
+      }
+    }
     // value_head.0.weight as 8x8 blocks (rows 8 * (t >> 5) + r, columns 8 * (t & 31) + c):
     // both h = W g (reduced over the 32 column blocks of a half-wave) and dg = W^T dh
-    // (over the 16 row blocks) stay cheap.  Issued behind the a2 band, in flight during conv3.
+    // (over the 16 row blocks) stay cheap.  Issued once the a2 band and the conv3 rows have
+    // landed (not beside them: 128 KB per workgroup), in flight during conv3, landed by B2.
     float wb[64];
     {
       const __amdgpu_buffer_rsrc_t rs = rsrc(a.p[WV1], VH * HID);
@@ -663,15 +673,6 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
         const f32x4_t q0 = ld4_sc1(rs, (r0 + r) * HID + c0), q1 = ld4_sc1(rs, (r0 + r) * HID + c0 + 4);
         wb[r * 8 + 0] = q0.x; wb[r * 8 + 1] = q0.y; wb[r * 8 + 2] = q0.z; wb[r * 8 + 3] = q0.w;
         wb[r * 8 + 4] = q1.x; wb[r * 8 + 5] = q1.y; wb[r * 8 + 6] = q1.z; wb[r * 8 + 7] = q1.w;
-      }
-    }
-    band_commit<R, C>(big, y0, a2v);
-#pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2) {  // plane-major for conv_band
-      const int e = 4 * (t + h2 * NT);
-      if (e < DW3N) {
-        sm[L::w3r + plane_major<C2>(e)] = w3q[h2].x; sm[L::w3r + plane_major<C2>(e + 1)] = w3q[h2].y;
-        sm[L::w3r + plane_major<C2>(e + 2)] = w3q[h2].z; sm[L::w3r + plane_major<C2>(e + 3)] = w3q[h2].w;
       }
     }
     __syncthreads();

@@ -35,6 +35,10 @@
 #ifndef HEIST_CONV3_PRE
 #define HEIST_CONV3_PRE 7
 #endif
+// act1 reads in flight in conv2's ring (build-time A/B knob)
+#ifndef HEIST_CONV2_PRE
+#define HEIST_CONV2_PRE 6
+#endif
 
 namespace heist {
 
@@ -132,7 +136,7 @@ __device__ __forceinline__ void conv2_pass(unsigned char* smem, const bf16x8* wl
                                            int nh, int lr, int h, int l, f32x16 (&cur)[NA],
                                            const f32x16 (&prv)[NP]) {
   using G = ConvGeom<R, C>;
-  constexpr int NTP = T1 - T0, NQ = kW2Steps * NTP, kPre2 = 6;
+  constexpr int NTP = T1 - T0, NQ = kW2Steps * NTP, kPre2 = HEIST_CONV2_PRE;
   constexpr int NPIECE = (P1 - P0) * 16;
   constexpr int PER_Q = NQ > 0 ? (NPIECE + NQ - 1) / (NQ > 0 ? NQ : 1) : NPIECE;
   bf16x4 o;
@@ -532,7 +536,7 @@ __device__ __forceinline__ void conv2_band_pass(unsigned char* smem, const bf16x
                                                 int nh, int lr, int h, int y0, f32x16 (&cur)[NA],
                                                 const f32x16 (&prv)[NP]) {
   using G = BandGeom<R, BR>;
-  constexpr int NTP = T1 - T0, NQ = kW2Steps * NTP, kPre2 = 6;
+  constexpr int NTP = T1 - T0, NQ = kW2Steps * NTP, kPre2 = HEIST_CONV2_PRE;
   constexpr int NPIECE = (P1 - P0) * 16;
   constexpr int PER_Q = NQ > 0 ? (NPIECE + NQ - 1) / (NQ > 0 ? NQ : 1) : NPIECE;
   bf16x4 o;

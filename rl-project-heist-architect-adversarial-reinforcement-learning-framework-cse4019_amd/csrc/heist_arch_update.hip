@@ -108,10 +108,10 @@ struct Lay {
                        gw2 = wcol + DW3N, gw3 = gw2 + DW2N, own = gw3 + 576, own2 = own + 4 * 128, red = own2 + 4 * 128,
                        g = red + 8 * 576, h = g + HID, dh = h + VH, dg = dh + VH, p16 = dg + HID, dp16 = p16 + 16,
                        scal = dp16 + 16, nzpos = scal + 64, nzval = nzpos + MAXNZ, ptab = nzval + MAXNZ,
-                       total = ptab + 3 * NTENS * 2;
+                       a1b = (ptab + 3 * NTENS * 2 + 3) / 4 * 4, total = a1b + C1 * PB;
 };
 // scal slots
-enum { S_V = 0, S_DV, S_CLIP, S_NS, S_BC2S, S_NNZ, S_TIMEOUT, S_DB3 = 8, S_DB2 = 12, S_NWF = 16, S_NWV1,
+enum { S_V = 0, S_DV, S_CLIP, S_NS, S_BC2S, S_NNZ, S_TIMEOUT, S_TG, S_DB3 = 8, S_DB2 = 12, S_NWF = 16, S_NWV1,
        S_NBF, S_NBV1, S_NWV2, S_RED8 = 32 };
 
 // ---- memory helpers ---------------------------------------------------------------------
@@ -382,14 +382,15 @@ __device__ __forceinline__ float conv1_at(const float* sm, int ci, int y, int x)
   return fmaxf(acc + sm[L::b1 + ci], 0.f);
 }
 
-// conv1 (1 -> 32) on the band rows and halo rows inside the image, into BIG planes [0, 32):
+// conv1 (1 -> 32) on the band rows and halo rows inside the image, into the A1B planes (the
+// step's a1 stays there for conv2, dW2 and da1's mask):
 // rows with no nonzero in reach hold relu(0 + b1); the few positions inside a nonzero's 3x3
 // neighbourhood are recomputed (a position near two nonzeros is written twice, same value).
 template <int R, int C>
 __device__ __forceinline__ void conv1_band(float* sm, int y0) {
   using L = Lay<R, C>;
   const int tid_ = tid_o();
-  float* big = sm + L::big;
+  float* big = sm + L::a1b;
   constexpr int NR = L::BH + 2;
   if (tid_ < C1 * NR) {
     const int ci = tid_ / NR, r = tid_ - ci * NR, y = y0 - 1 + r;
@@ -538,6 +539,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
   {
     const int t = threadIdx.x, w = blockIdx.x, cg = wg_cg(w);
     for (int i = t; i < L::w1; i += NT) sm[i] = 0.f;
+    for (int i = t; i < C1 * L::PB; i += NT) sm[L::a1b + i] = 0.f;  // a1's pads and out-of-image rows
     if (t < 64) scal[t] = 0.f;
     if (t < 3 * NTENS) {
       float** tab = reinterpret_cast<float**>(sm + L::ptab);
@@ -619,15 +621,16 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
     const int fi = fc_row(t), fhf = fc_half(t), ev = w * 512 + t;
     // ======== P1: conv1 (band + halo), conv2 own channels ========
     STAMP(0)
-    if (t == NT - 1) {  // this step's Adam scalars, read well before P6 needs them
+    if (t == NT - 1) {  // this step's Adam scalars and target, read well before P3 / P6 need them
       scal[S_NS] = a.adam_sc[2 * s];
       scal[S_BC2S] = a.adam_sc[2 * s + 1];
+      scal[S_TG] = a.target[s];
     }
     conv1_band<R, C>(sm, y0);
     __syncthreads();
     STAMP(15)
     {
-      const float z = conv_band<R, C, CPG, 4, false>(big, sm + L::w2t, 36, red);
+      const float z = conv_band<R, C, CPG, 4, false>(sm + L::a1b, sm + L::w2t, 36, red);
       if (t < CPG * NPB) {
         a2keep = fmaxf(z + sm[L::b23 + t / NPB], 0.f);
         sm[L::own + t] = a2keep;
@@ -751,7 +754,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       x = sum64(x);
       if (lane == 0) {
         const float v = x + sm[L::bv2];
-        const float tg = a.target[s];
+        const float tg = scal[S_TG];
         scal[S_V] = v;
         scal[S_DV] = (2.0f * (v - tg)) * a.grad_out;  // mse_loss backward: 2 (v - r) * dL/dmse
         if (w == 0) a.vloss[s] = (v - tg) * (v - tg);
@@ -927,8 +930,6 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       store_band<R, C>(a.ws + WS_DA2, sm + L::own2, cg, band);
     }
     STAMP(14)
-    conv1_band<R, C>(sm, y0);  // a1 again into planes [0, 32) (da3 no longer needed)
-    __syncthreads();
     STAMP(24)
     {  // dW2 partial over the band: lanes = (input plane, column quarter bit 0), waves = (channel,
        // column quarter bit 1)
@@ -936,7 +937,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
 #pragma unroll
       for (int j = 0; j < 9; ++j) acc[j] = 0.f;
       const int ci = lane & 31, xq = (lane >> 5) | ((wv >> 2) << 1), q = wv & 3;
-      wgrad<R, C, BH, C / 4>(big, ci, 0, xq * (C / 4), sm + L::own2 + q * NPB, acc);
+      wgrad<R, C, BH, C / 4>(sm + L::a1b, ci, 0, xq * (C / 4), sm + L::own2 + q * NPB, acc);
 #pragma unroll
       for (int j = 0; j < 9; ++j) red[(xq * CPG + q) * 288 + ci * 9 + j] = acc[j];
       __syncthreads();
@@ -1019,7 +1020,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       float da1 = 0.f;
       if (t < 2 * NPB) {
         const int j = t / NPB, pos = t - j * NPB, y = y0 + pos / C, x = pos - (pos / C) * C;
-        da1 = conv1_at<R, C>(sm, 2 * cg + j, y, x) > 0.f ? z : 0.f;
+        da1 = sm[L::a1b + (2 * cg + j) * L::PB + (y - y0 + 1) * L::RS + x + 1] > 0.f ? z : 0.f;
         sm[L::own + t] = da1;
       }
       __syncthreads();

@@ -931,15 +931,29 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
     }
     STAMP(14)
     STAMP(24)
-    {  // dW2 partial over the band: lanes = (input plane, column quarter bit 0), waves = (channel,
-       // column quarter bit 1)
-      float acc[9];
+    {  // dW2 partial over the band, two output channels per lane (one window load feeds both):
+       // lanes = (input plane, column quarter bit 0), waves = (channel pair, column quarter
+       // bit 1, row half); the lane halves are added by a permlane swap, the 4 wave sets
+       // through red (the store loop below)
+      f32x2_t acc[9];
 #pragma unroll
-      for (int j = 0; j < 9; ++j) acc[j] = 0.f;
-      const int ci = lane & 31, xq = (lane >> 5) | ((wv >> 2) << 1), q = wv & 3;
-      wgrad<R, C, BH, C / 4>(sm + L::a1b, ci, 0, xq * (C / 4), sm + L::own2 + q * NPB, acc);
+      for (int j = 0; j < 9; ++j) acc[j] = f32x2_t{0.f, 0.f};
+      const int ci = lane & 31, qp = wv & 1, xhi = (wv >> 1) & 1, rh = wv >> 2;
+      const int xq = (lane >> 5) | (xhi << 1);
+      constexpr int RH0 = (BH + 1) / 2;
+      const float* d0 = sm + L::own2 + (2 * qp) * NPB;
+      if (rh == 0) wgrad2<R, C, RH0, C / 4>(sm + L::a1b, ci, 0, xq * (C / 4), d0, d0 + NPB, acc);
+      else wgrad2<R, C, BH - RH0, C / 4>(sm + L::a1b, ci, RH0, xq * (C / 4), d0, d0 + NPB, acc);
 #pragma unroll
-      for (int j = 0; j < 9; ++j) red[(xq * CPG + q) * 288 + ci * 9 + j] = acc[j];
+      for (int j = 0; j < 9; ++j) {
+        acc[j].x = swap32_add(acc[j].x);
+        acc[j].y = swap32_add(acc[j].y);
+      }
+      if (lane < 32) {
+        float* slot = red + ((xhi * 2 + rh) * CPG + 2 * qp) * 288 + ci * 9;
+#pragma unroll
+        for (int j = 0; j < 9; ++j) { slot[j] = acc[j].x; slot[288 + j] = acc[j].y; }
+      }
       __syncthreads();
       STAMP(31)
       float* dst = a.ws + WS_DW2 + w * DW2R;

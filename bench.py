@@ -173,13 +173,16 @@ def measure_fan_fill(env, actions, K, bufs, reps=5):
     return max(0.0, float(np.median(fill) - np.median(plain)))
 
 
-def time_env(env, actions, warmup, steps, K, world):
+def time_env(env, actions, warmup, steps, K, world, settle_ms=0.0, extra_windows=0):
     """Time `steps` env ticks over all envs after `warmup` untimed ones: K = 1 one heist_step
     launch per tick, K > 1 heist_step_multi launches of K ticks (the last one shorter), every
     tick's observation rows going to an [K, N, 3, R, C] buffer.  HIP events bracket the
     timed launches on the stream they run on, so their span / steps is the mean tick
     duration (inter-launch gaps included); the wall clock runs between two barriers and at
-    N > 1 is the max over ranks.  Returns (elapsed_s, kernel_ms_per_tick, issue_s, launches)."""
+    N > 1 is the max over ranks.  K > 1: an untimed clock-settle phase of settle_ms of K-tick
+    launches precedes the window (then the fan table is refilled by the warm-up ticks, as
+    without it), and extra_windows more windows (HIP events only) give the spread
+    (time_env.windows).  Returns (elapsed_s, kernel_ms_per_tick, issue_s, launches)."""
     dev, N = env.device, env.n_envs
     dist = torch.distributed
     stream = torch.cuda.current_stream(dev)
@@ -208,6 +211,26 @@ def time_env(env, actions, warmup, steps, K, world):
                 env.step(actions[k0 + k])
             return n
     run(0, warmup)
+    time_env.settle = None
+    if K > 1 and settle_ms > 0:
+        # clock settle (untimed): K-tick launches on the same handle for settle_ms, so the
+        # timed window does not start on a cold / boosting clock; then the shared fan table is
+        # marked stale and the warm-up launches refill it, so the timed launches read the table
+        # at the same offsets as without the settle phase (no refill inside the window)
+        settle = prepare(0, K)
+        torch.cuda.synchronize(dev)
+        ts = time.perf_counter()
+        n_settle = 0
+        while (time.perf_counter() - ts) * 1e3 < settle_ms or n_settle < 8:
+            for launch in settle:
+                launch()
+            n_settle += 1
+            if n_settle % 16 == 0:
+                torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)
+        env.set_ray_mode(env.kernel_config()["ray_mode"])  # marks the fan table stale (heist_set_ray_mode)
+        run(0, warmup)
+        time_env.settle = {"launches": n_settle, "ms": (time.perf_counter() - ts) * 1e3}
     ready = prepare(warmup, steps)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -225,6 +248,21 @@ def time_env(env, actions, warmup, steps, K, world):
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / steps
+    windows = []
+    for _ in range(extra_windows if K > 1 else 0):
+        # the same window again (after the same stale-table warm-up), HIP events only: the
+        # spread of the headline's kernel time on this box
+        env.set_ray_mode(env.kernel_config()["ray_mode"])
+        run(0, warmup)
+        ready_x = prepare(warmup, steps)
+        torch.cuda.synchronize(dev)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        run(warmup, steps, ready_x)
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        windows.append(a.elapsed_time(b) / steps)
+    time_env.windows = windows
     per_rank = [(elapsed, kern_ms)]
     if world > 1:  # every rank's wall time and kernel time per tick; the line's time is the max
         t = torch.zeros((world, 2), dtype=torch.float64, device=dev)
@@ -280,7 +318,7 @@ def measure_env_config(dev, R, n, budget, steps=100, warmup=10, K=1, **kw):
     env.reset()
     acts = torch.randint(0, 5, (warmup + steps, n), device=dev, dtype=torch.int64)
     K = max(1, min(K, steps))
-    _, ms, _, _ = time_env(env, acts, warmup, steps, K, 1)
+    _, ms, _, _ = time_env(env, acts, warmup, steps, K, 1, settle_ms=10.0)
     st = env.export()
     ncam, ngu = float(st["n_cams"].double().mean()), float(st["n_guards"].double().mean())
     b = algorithmic_bytes_per_env_step(R, R, ncam, ngu)
@@ -433,6 +471,10 @@ def main():
     ap.add_argument("--ticks-per-launch", type=int, default=20,
                     help="K: env ticks per heist_step_multi launch in the timed region (1: one heist_step per tick)")
     ap.add_argument("--train-envs", type=int, default=8192, help="envs per GPU of the N > 1 full-train line (C4)")
+    ap.add_argument("--settle-ms", type=float, default=30.0,
+                    help="untimed K-tick launches before the timed window (clock settle), milliseconds")
+    ap.add_argument("--extra-windows", type=int, default=4,
+                    help="extra timed windows after the headline one (HIP events): median / spread fields")
     ap.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                     help="torch.distributed backend at N > 1 (nccl = RCCL over xGMI; gloo lets several ranks share "
                          "one GPU, for tests)")
@@ -459,7 +501,15 @@ def main():
     dist = torch.distributed
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        local %= max(1, torch.cuda.device_count())  # gloo: several ranks may share one GPU
+        ndev = torch.cuda.device_count()
+        if args.backend == "nccl" and ndev < world:
+            # one process per GPU: RCCL needs N distinct devices (gloo may share one, for tests)
+            print("bench.py: --gpus %d with the nccl (RCCL) backend needs %d visible GPUs, this node shows %d "
+                  "(HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES = %r / %r); run with --gpus %d or --backend gloo"
+                  % (world, world, ndev, os.environ.get("HIP_VISIBLE_DEVICES"),
+                     os.environ.get("ROCR_VISIBLE_DEVICES"), ndev), file=sys.stderr, flush=True)
+            sys.exit(2)
+        local %= max(1, ndev)  # gloo: several ranks may share one GPU
         torch.cuda.set_device(local)
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -493,8 +543,10 @@ def main():
     gen.manual_seed(4321 + rank)
     actions = torch.randint(0, 5, (args.warmup + args.steps, N), device=dev, generator=gen, dtype=torch.int64)
     K = max(1, min(args.ticks_per_launch, args.steps))
-    elapsed, kern_ms, issue_s, launches = time_env(env, actions, args.warmup, args.steps, K, world)
+    elapsed, kern_ms, issue_s, launches = time_env(env, actions, args.warmup, args.steps, K, world,
+                                                   settle_ms=args.settle_ms, extra_windows=args.extra_windows)
     per_rank = time_env.per_rank
+    windows, settle_info = list(time_env.windows), time_env.settle
     fan_fill_ms = 0.0
     if K > 1 and kcfg["fan_on"]:  # the table fill the timed launches did not pay (read from an earlier fill)
         fan_fill_ms = measure_fan_fill(env, actions, K, time_env.last_bufs)
@@ -571,6 +623,14 @@ def main():
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": multi_kernel_name(kcfg, 20, 20) if K > 1 else "heist::step_kernel",
                          "kernel_ms": kern_ms, "kernel_ms_per_launch": kern_ms * K, "launches": launches,
+                         "clock_settle": settle_info,
+                         "extra_windows_kernel_ms": windows,
+                         "windows_frac": None if not windows else {
+                             "n": len(windows) + 1,
+                             "median": float(np.median([b_step * N / (w * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                                        for w in windows + [kern_ms]])),
+                             "min": min(b_step * N / (w * 1e-3) / 1e9 / HBM_PEAK_GBS for w in windows + [kern_ms]),
+                             "max": max(b_step * N / (w * 1e-3) / 1e9 / HBM_PEAK_GBS for w in windows + [kern_ms])},
                          "algorithmic_bytes_per_env_step": b_step,
                          "ray_samples_per_env_step": samples_per_step,
                          "exact_path_rays_per_env_step": exact_rays_per_step,

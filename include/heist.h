@@ -91,7 +91,9 @@ int heist_step(heist_t h, const int64_t* actions, float* obs_out, float* reward_
  * with every per-tick output written (tick-major: actions [K][N] int64, obs_out
  * [K][N][3][R][C] float32, reward_out [K][N] float32, reward64_out [K][N] float64 or NULL,
  * done_out [K][N] uint8, status_out [K][N] int8); the per-env state stays on chip between
- * the ticks.  1 <= K <= 1024. */
+ * the ticks.  1 <= K <= 1024.  Launches read a table of the shared camera fan that a launch
+ * refills when it is stale; a launch on another stream than the previous one refills it
+ * after waiting, on the device, for that launch (no host synchronisation). */
 int heist_step_multi(heist_t h, int K, const int64_t* actions, float* obs_out, float* reward_out,
                      double* reward64_out, uint8_t* done_out, int8_t* status_out, int auto_reset,
                      heist_stream_t stream);
@@ -135,9 +137,9 @@ int64_t heist_stamp_words(heist_t h, int which);
 int heist_step_waves(heist_t h);
 
 /* The handle's effective kernel configuration, no reference counterpart (what a benchmark
- * records next to its numbers): out[0..n) with n <= 13 receives step_waves, ray_chunk,
+ * records next to its numbers): out[0..n) with n <= 14 receives step_waves, ray_chunk,
  * step_occ, vis_gap, obs_store, ray_mode, probe_mode, dispatch_order, split_obs,
- * guard_cones, multi_waves, fan_on, lean (the HEIST_* environment knobs as heist_create resolved them,
+ * guard_cones, multi_waves, fan_on, lean, interval_fans (the HEIST_* environment knobs as heist_create resolved them,
  * then any heist_set_* calls).  probe_mode != 0 selects the profiling step kernel, whose results are
  * wrong by design (phases skipped). */
 int heist_get_config(heist_t h, int32_t* out, int n);
@@ -235,8 +237,16 @@ int heist_arch_update_sequence(float* const* params, float* const* exp_avg, floa
                                const float* grid, int rows, int cols, const float* rewards, int k,
                                const float* step_scalars, double beta1, double beta2, double eps, double max_norm,
                                double value_coeff, float* value_loss, void* workspace, heist_stream_t stream);
-/* 1 in *timed_out if a grid barrier of the last launch on `workspace` gave up waiting
- * (workgroups not co-resident; its results are then invalid).  Synchronises `stream`. */
+/* Status of the last launch on `workspace`, a bit mask; any bit set means its results --
+ * the updated params, exp_avg, exp_avg_sq and value_loss -- are INVALID (the caller restores
+ * its own copy and re-runs the steps another way):
+ *   bit 0: a grid barrier gave up waiting (the 64 workgroups were not co-resident; the spin
+ *          bound is 2^25 polls, HEIST_ARCH_SPIN_LIMIT overrides it, e.g. to test this path);
+ *   bit 1: grid has more than 64 nonzero pixels.
+ * The word is the uint32 at byte offset heist_arch_update_workspace_bytes() - 252 of the
+ * workspace (zeroed at each launch), so a caller can also copy it asynchronously.
+ * Synchronises `stream`.  heist_arch_update_timed_out reports bit 0 alone. */
+int heist_arch_update_status(const void* workspace, int* status, heist_stream_t stream);
 int heist_arch_update_timed_out(const void* workspace, int* timed_out, heist_stream_t stream);
 /* Instrumentation, no reference counterpart: with buf a device array of 2 * 16 * 32 + 16 * 5 * 64
  * uint64, later heist_arch_update_sequence launches record s_memrealtime (100 MHz) at up to 32

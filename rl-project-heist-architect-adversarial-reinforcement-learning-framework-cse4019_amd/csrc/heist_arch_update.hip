@@ -49,6 +49,7 @@
 // (per-tensor norms, their norm, max_norm / (total + 1e-6) clamped to 1, grads scaled).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "heist_device.h"
 
@@ -88,6 +89,7 @@ struct Args {
   float* ws;            // WS_FLOATS floats; ws + WS_CTR: barrier counter and timeout flag (zeroed per launch)
   unsigned long long* stamps;  // instrumentation (NULL: off): s_memrealtime per phase point
   int k;
+  unsigned spin_limit;  // polls per grid barrier before it gives up (HEIST_ARCH_SPIN_LIMIT; default 2^25)
   float lerp_w, beta2f, c2, eps, max_norm, grad_out;
 };
 
@@ -175,9 +177,11 @@ __device__ __forceinline__ float sum64(float x) { return swap32_add(sum32(x)); }
 
 // Grid barrier number `idx` (0-based over the launch).  Every storing wave drains its sc1
 // stores, the workgroup meets, one lane adds to the monotonic counter and polls it with a
-// relaxed sc1 load.  The spin is bounded: on a timeout (co-residency lost) the flag is set,
-// the host reports it, and later barriers stop waiting so the grid still drains.
-__device__ __forceinline__ void grid_barrier(unsigned* ctr, unsigned idx, float* scal,
+// relaxed sc1 load.  The spin is bounded (spin_limit polls): on a timeout (co-residency
+// lost) status word ctr[1] gets bit 0 (heist_arch_update_status; the package restores its
+// snapshot and re-runs the steps on another path), and later barriers stop waiting so the
+// grid still drains.
+__device__ __forceinline__ void grid_barrier(unsigned* ctr, unsigned idx, float* scal, unsigned spin_limit,
                                              unsigned long long* ready = nullptr) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -191,8 +195,8 @@ __device__ __forceinline__ void grid_barrier(unsigned* ctr, unsigned idx, float*
       unsigned spins = 0;
       while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 25)) {
-          __hip_atomic_store(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (++spins > spin_limit) {
+          __hip_atomic_fetch_or(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           scal[S_TIMEOUT] = 1.f;
           break;
         }
@@ -593,7 +597,11 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
         }
         cnt += __popcll(bal);
       }
-      if (t == 0) scal[S_NNZ] = (float)(cnt < MAXNZ ? cnt : MAXNZ);  // the host checks nnz <= MAXNZ
+      if (t == 0) scal[S_NNZ] = (float)(cnt < MAXNZ ? cnt : MAXNZ);
+      // more than MAXNZ nonzeros: the forward would drop pixels -- status bit 1, results invalid
+      if (t == 0 && cnt > MAXNZ && blockIdx.x == 0)
+        __hip_atomic_fetch_or(reinterpret_cast<unsigned*>(a.ws + WS_CTR) + 1, 2u, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
   }
@@ -639,7 +647,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       store_band<R, C>(a.ws + WS_A2, sm + L::own, cg, band);
     }
     STAMP(1)
-    grid_barrier(ctr, bar++, scal, READY(0));
+    grid_barrier(ctr, bar++, scal, a.spin_limit, READY(0));
     STAMP(2)
 
     // ======== P2: conv3 own channels, pool, fc_global partial ========
@@ -710,7 +718,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       if (fhf == 0) st_sc1(a.ws + WS_GP + w * HID + fi, gp);
     }
     STAMP(3)
-    grid_barrier(ctr, bar++, scal, READY(1));
+    grid_barrier(ctr, bar++, scal, a.spin_limit, READY(1));
     STAMP(4)
 
     // ======== P3: value head (redundant), dp / da3 / dW3 / dWf / dWv1 (owned) ========
@@ -880,7 +888,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       }
     }
     STAMP(5)
-    grid_barrier(ctr, bar++, scal, READY(2));
+    grid_barrier(ctr, bar++, scal, a.spin_limit, READY(2));
     STAMP(6)
 
     // ======== P4: da2 own channels (conv3^T), dW2 / db2 partials ========
@@ -978,7 +986,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       if (t < 32) st_sc1(a.ws + WS_DW2 + w * DW2R + DW2N + t, t < CPG ? x[t] : 0.f);
     }
     STAMP(7)
-    grid_barrier(ctr, bar++, scal, READY(3));
+    grid_barrier(ctr, bar++, scal, a.spin_limit, READY(3));
     STAMP(8)
 
     // ======== P5: da1 (2 channels on the band), partial dW1 / db1, the group's weight
@@ -1090,7 +1098,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       }
     }
     STAMP(9)
-    grid_barrier(ctr, bar++, scal, READY(4));
+    grid_barrier(ctr, bar++, scal, a.spin_limit, READY(4));
     STAMP(10)
 
     // ======== P6: clip coefficient, Adam, publish ========
@@ -1301,6 +1309,8 @@ hipError_t launch_arch_update(float* const* p, float* const* m, float* const* v,
   a.grid = grid; a.target = target; a.vloss = vloss; a.ws = (float*)ws;
   a.stamps = g_arch_stamps;
   a.k = k;
+  a.spin_limit = 1u << 25;
+  if (const char* sl = getenv("HEIST_ARCH_SPIN_LIMIT")) a.spin_limit = (unsigned)strtoul(sl, nullptr, 10);
   a.adam_sc = adam_sc;
   a.lerp_w = (float)(1.0 - beta1);
   a.beta2f = (float)beta2;

@@ -83,6 +83,7 @@ struct heist_env {
   hipStream_t fan_stream;  // stream of the K-tick launch that last used the table (a refill on another stream
                            // could overwrite entries a launch still in flight on this one reads)
   bool fan_used;           // a K-tick launch has been issued on fan_stream
+  hipEvent_t fan_done;     // recorded behind every K-tick launch: a refill on another stream waits for it
   int64_t stamp_words;     // size of the stamp buffer armed by heist_step_stamps (uint64 words)
 };
 
@@ -296,6 +297,7 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   h->fan_pos = -1;
   h->fan_stream = nullptr;
   h->fan_used = false;
+  h->fan_done = nullptr;
   h->stamp_words = 0;
   p.fan_base = 0;
   p.fan_fill = 0;
@@ -303,6 +305,8 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   if (const char* f = getenv("HEIST_SHARED_FAN")) p.fan_on = atoi(f) ? 1 : 0;
   p.lean = 1;
   if (const char* f = getenv("HEIST_LEAN")) p.lean = atoi(f) ? 1 : 0;
+  p.interval_fans = 1;
+  if (const char* f = getenv("HEIST_INTERVAL_FANS")) p.interval_fans = atoi(f) ? 1 : 0;
   p.guard_cones = 1;
   if (const char* gc = getenv("HEIST_GUARD_CONES")) p.guard_cones = atoi(gc) ? 1 : 0;
   std::vector<double> hrad(heist::kHalfDegN);
@@ -334,6 +338,7 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
 
 int heist_destroy(heist_t h) {
   if (!h) return 0;
+  if (h->fan_done) (void)hipEventDestroy(h->fan_done);
   for (int j = 0; j < h->n_allocs; ++j) (void)hipFree(h->allocs[j]);
   delete h;
   return 0;
@@ -390,9 +395,9 @@ int heist_step_multi(heist_t h, int K, const int64_t* actions, float* obs_out, f
   hipStream_t st = (hipStream_t)stream;
   // the shared fan table (FanTick): refilled when stale, used up, or last used by a launch on
   // another stream (streams do not order a refill against a launch still reading the table:
-  // that stream is drained first, a host wait paid only when the caller switches streams),
-  // else read at the launch's offset -- only when the K-tick kernel runs (otherwise K single
-  // ticks advance the headings)
+  // the new stream waits, on the device, for the event recorded behind the last K-tick
+  // launch), else read at the launch's offset -- only when the K-tick kernel runs (otherwise
+  // K single ticks advance the headings)
   EnvParams q = h->p;
   const bool kt = heist::multi_variant_exists(q.multi_waves, q.ray_chunk, q.multi_occ, q.vis_gap) && (q.C & 3) == 0 &&
                   q.probe_mode == 0 && !q.sample_counter && !q.redo_counter;
@@ -403,7 +408,7 @@ int heist_step_multi(heist_t h, int K, const int64_t* actions, float* obs_out, f
     int pos = h->fan_pos;
     if (pos < 0 || pos + K > heist::kFanTicks || st != h->fan_stream) {
       if (h->fan_used && st != h->fan_stream)  // the refill must not overtake a launch still reading the table
-        if (int rc = check_hip(hipStreamSynchronize(h->fan_stream), "heist_step_multi: previous stream")) return rc;
+        if (int rc = check_hip(hipStreamWaitEvent(st, h->fan_done, 0), "heist_step_multi: previous stream")) return rc;
       q.fan_fill = 1;
       pos = 0;
     }
@@ -415,7 +420,16 @@ int heist_step_multi(heist_t h, int K, const int64_t* actions, float* obs_out, f
                            "heist_step_multi");
   // the table position advances only with a launch that was issued
   h->fan_pos = rc ? -1 : next_pos;
-  if (!rc) {
+  if (!rc && kt && q.fan_on) {
+    if (!h->fan_done)
+      if (int e = check_hip(hipEventCreateWithFlags(&h->fan_done, hipEventDisableTiming), "heist_step_multi: event")) {
+        h->fan_pos = -1;
+        return e;
+      }
+    if (int e = check_hip(hipEventRecord(h->fan_done, st), "heist_step_multi: event record")) {
+      h->fan_pos = -1;
+      return e;
+    }
     h->fan_stream = st;
     h->fan_used = true;
   }
@@ -461,11 +475,11 @@ int heist_step_waves(heist_t h) {
 
 int heist_get_config(heist_t h, int32_t* out, int n) {
   if (int rc = check_handle(h)) return rc;
-  HEIST_REQUIRE(out != nullptr && n >= 0 && n <= 13, "heist_get_config: need out != NULL and 0 <= n <= 13");
+  HEIST_REQUIRE(out != nullptr && n >= 0 && n <= 14, "heist_get_config: need out != NULL and 0 <= n <= 14");
   const EnvParams& p = h->p;
-  const int32_t v[13] = {p.step_waves, p.ray_chunk,  p.step_occ,       p.vis_gap,   p.obs_store,  p.ray_mode,
+  const int32_t v[14] = {p.step_waves, p.ray_chunk,  p.step_occ,       p.vis_gap,   p.obs_store,  p.ray_mode,
                          p.probe_mode, p.dispatch_order, p.split_obs, p.guard_cones, p.multi_waves, p.fan_on,
-                         p.lean};
+                         p.lean,       p.interval_fans};
   for (int k = 0; k < n; ++k) out[k] = v[k];
   return 0;
 }
@@ -595,15 +609,23 @@ int heist_arch_update_stamps(uint64_t* buf) {
   return 0;
 }
 
-int heist_arch_update_timed_out(const void* workspace, int* timed_out, heist_stream_t stream) {
-  HEIST_REQUIRE(workspace && timed_out, "heist_arch_update_timed_out: null pointer");
+int heist_arch_update_status(const void* workspace, int* status, heist_stream_t stream) {
+  HEIST_REQUIRE(workspace && status, "heist_arch_update_status: null pointer");
   unsigned flag[2] = {0, 0};
   const char* ctr = (const char*)workspace + heist::arch_update_workspace_bytes() - 64 * 4;
   hipStream_t st = (hipStream_t)stream;
-  if (int rc = check_hip(hipMemcpyAsync(flag, ctr, sizeof(flag), hipMemcpyDeviceToHost, st), "heist_arch_update_timed_out"))
+  if (int rc = check_hip(hipMemcpyAsync(flag, ctr, sizeof(flag), hipMemcpyDeviceToHost, st), "heist_arch_update_status"))
     return rc;
-  if (int rc = check_hip(hipStreamSynchronize(st), "heist_arch_update_timed_out")) return rc;
-  *timed_out = flag[1] != 0;
+  if (int rc = check_hip(hipStreamSynchronize(st), "heist_arch_update_status")) return rc;
+  *status = (int)(flag[1] & 3u);
+  return 0;
+}
+
+int heist_arch_update_timed_out(const void* workspace, int* timed_out, heist_stream_t stream) {
+  HEIST_REQUIRE(workspace && timed_out, "heist_arch_update_timed_out: null pointer");
+  int status = 0;
+  if (int rc = heist_arch_update_status(workspace, &status, stream)) return rc;
+  *timed_out = status & 1;
   return 0;
 }
 

@@ -151,6 +151,8 @@ struct EnvParams {
   FanTick* fan;               // [kFanTicks] shared camera fan of the current K-tick launch (fan_kernel)
   int fan_on;                 // 1 (default): the K-tick kernel uses the shared fan (HEIST_SHARED_FAN)
   int lean;                   // 1 (default): one-wave 20 x 20 K-tick launches run step_lean_kernel (HEIST_LEAN)
+  int interval_fans;          // 1 (default): step_lean_kernel casts cameras the shared fan does not serve from
+                              // the ray-direction interval table (heist_fan_intervals.h; HEIST_INTERVAL_FANS)
   int fan_base;               // table entry of the launch's tick 0 (heist_step_multi)
   int fan_fill;               // 1: the launch first refills the table from the cameras' current headings
   int probe_mode;             // profiling only (HEIST_PROBE_MODE): 0 normal, 1 no rays, 2 angles+sin/cos only,

@@ -16,6 +16,7 @@
 #include <utility>
 
 #include "heist_device.h"
+#include "heist_fan_intervals.h"
 #include "heist_trig.h"
 
 #pragma clang fp contract(off)
@@ -488,6 +489,13 @@ __device__ __forceinline__ double uni(double x) {
   const uint64_t b = __builtin_bit_cast(uint64_t, x);
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// lane m's double, wave-uniform
+__device__ __forceinline__ double uni_lane(double x, int m) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, x);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, m);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), m);
   return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
 }
 __device__ __forceinline__ Emit uni(const Emit& e) {
@@ -2189,6 +2197,26 @@ __device__ __noinline__ void lean_tie_rays(unsigned char* smem, const FanTick* f
   }
 }
 
+// The exact path for an interval fan's near-cut rays: lane i casts ray `ray` (< 0: none) of
+// the camera with emitter (hmh, fov, num_rays) at tile rc (row | col << 8).  A call, as
+// lean_tie_rays, so that the exact path's registers stay out of the lean loop.
+template <int D, int PC>
+__device__ __noinline__ void ivl_tie_rays(unsigned char* smem, int ray, double hmh, double fov, int num_rays,
+                                          uint32_t rc, const double* hd) {
+  Emit E;
+  E.hmh = hmh;
+  E.fov = fov;
+  E.step = 0.0;
+  E.range = kTieMaxRange;
+  E.num_rays = num_rays;
+  E.row = (int)(rc & 0xffu);
+  E.col = (int)(rc >> 8);
+  E.first = 0;
+  E.kind = 0;
+  E.members = 1;
+  if (ray >= 0) exact_ray<4, D>(smem, E, ray, PC, 0, hd);
+}
+
 // The lean kernel's LDS: the three padded planes (stop map, visibility, sink; the step
 // kernels' geometry, so exact_ray works on them), the tile grid, the patrol paths, the
 // launch's K actions, the LDS-DMA staging of the next tick's HBM data (LeanStage), the
@@ -2201,16 +2229,50 @@ struct LeanStage {
   uint2 off2[128];  // samples 9-12 (FanTick::off2)
   int hdr[4];       // FanTick num_rays, range, n_uniq, n_tie
 };
+
+// Interval fans (heist_fan_intervals.h, tools/gen_fan_intervals.py).  A camera ray's 12
+// sample tiles depend on its direction only through which INTERVAL between consecutive
+// cuts -- the angles where |cos| or |sin| is a tie point j/k (j odd, k <= 12) or 0 -- the
+// direction lies in: inside one, every sample's rint is constant (the fast path's argument,
+// cast_rays).  So a camera's fan is the set of intervals its rays land in, and each is
+// marched ONCE with its midpoint direction from the camera's tile; a ray within a margin of
+// a cut takes the exact path.  Which intervals hold a ray is a few fixed-point comparisons
+// per lane (lane = interval), no sin/cos and no dedup: a camera of fov F is ~0.7 F lanes
+// instead of 2 F rays.  Angles are in 2^32 units per turn (u32 arithmetic wraps at 360).
+// The lean kernel copies the table into LDS (the space the shared fan's staging takes in
+// an env the fan serves).
+constexpr double kFanUnitsPerDeg = 4294967296.0 / 360.0;
+struct IvlTable {
+  uint32_t cut[kFanCuts];  // cut angles, ascending
+  float2 dir[kFanCuts];    // interval j = [cut j, cut j+1): midpoint (cos / 2, -sin / 2), fp32
+  uint8_t idx[368];        // [d] first j with cut j >= d degrees, d = 0 .. 360
+};
+static_assert(sizeof(IvlTable) % 16 == 0, "copied in 16-byte words");
+constexpr IvlTable make_ivl_table() {
+  IvlTable t{};
+  for (int j = 0; j < kFanCuts; ++j) {
+    t.cut[j] = kFanCut[j];
+    t.dir[j] = float2{kFanDir[j][0], kFanDir[j][1]};
+  }
+  for (int d = 0; d < 361; ++d) t.idx[d] = kFanIdx[d];
+  return t;
+}
+__constant__ IvlTable kIvlTable = make_ivl_table();
+constexpr size_t kLeanUnion = sizeof(LeanStage) > sizeof(IvlTable) ? sizeof(LeanStage) : sizeof(IvlTable);
 struct LeanLds {
   uint8_t* grid;
   uint16_t* path;
   uint8_t* act;
-  LeanStage* stg;
+  LeanStage* stg;  // an env the shared fan serves: the next tick's fan entry
+  IvlTable* ivl;   // any other env: the interval table (same LDS)
   uint16_t* cone;
   float4* plane2;
 };
+// The lean kernel's plane gap D: the padded (R + 12) x (C + 12) plane in 1024 (up to 20 x 20)
+// or 2048 bytes (up to 33 x 33).
+__host__ __device__ constexpr int lean_gap(int R, int C) { return (R + 2 * kRing) * (C + 2 * kRing) <= 1024 ? 1024 : 2048; }
 __host__ __device__ inline size_t lean_carve(unsigned char* smem, int R, int C, int mg, int mp, int K, LeanLds* L) {
-  size_t o = 3 * 1024;
+  size_t o = 3 * (size_t)lean_gap(R, C);
   if (L) L->grid = smem + o;
   o += align16((size_t)R * C);
   if (L) L->path = reinterpret_cast<uint16_t*>(smem + o);
@@ -2218,7 +2280,8 @@ __host__ __device__ inline size_t lean_carve(unsigned char* smem, int R, int C, 
   if (L) L->act = smem + o;
   o += align16((size_t)K);
   if (L) L->stg = reinterpret_cast<LeanStage*>(smem + o);
-  o += sizeof(LeanStage);
+  if (L) L->ivl = reinterpret_cast<IvlTable*>(smem + o);
+  o += align16(kLeanUnion);
   if (L) L->cone = reinterpret_cast<uint16_t*>(smem + o);
   o += 64 * (size_t)(mg > 0 ? mg : 1);
   if (L) L->plane2 = reinterpret_cast<float4*>(smem + o);
@@ -2254,14 +2317,15 @@ template <int R_, int C_>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void step_lean_kernel(
     EnvParams p, int K, const int64_t* __restrict__ actions, float* __restrict__ obs, float* __restrict__ rew,
     double* __restrict__ rew64, uint8_t* __restrict__ done_out, int8_t* __restrict__ status_out, int auto_reset) {
-  constexpr int D = 1024;
+  constexpr int D = lean_gap(R_, C_);
   constexpr int PC = C_ + 2 * kRing;
   constexpr int RC = R_ * C_;
   constexpr int N4 = RC / 4;
   constexpr int C4 = C_ / 4;
+  constexpr int Q = (N4 + 63) / 64;  // observation quads per lane (20 x 20: 2, 32 x 32: 4)
   constexpr int OFF0 = kRing * PC + kRing;  // padded index of tile (0, 0); also a sample's offset on its own tile
   static_assert((R_ + 2 * kRing) * PC <= D, "the padded planes fit the 1024-byte gap");
-  static_assert(C_ % 4 == 0 && N4 <= 64 * kObsQ && R_ <= 64 && C_ <= 32, "lean kernel geometry");
+  static_assert(C_ % 4 == 0 && R_ <= 64 && C_ <= 32 && (R_ + 2 * kRing) * PC <= 2048, "lean kernel geometry");
   extern __shared__ __align__(16) unsigned char smem[];
   const int e = p.dispatch_order ? p.order[blockIdx.x] : (int)blockIdx.x;
   const int lane = threadIdx.x;
@@ -2282,6 +2346,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
   LeanGuard gd{0u, 0u, 0u};           // guard lanes
   const bool live_cam = lane < s.n_cams, live_guard = g >= 0 && g < s.n_guards;
   bool cached = false;
+  // interval fans (camera lanes): fov, the ray spacing in angle units and its reciprocal, rays
+  double fovd = 0.0, su = 1.0, isu = 1.0;
+  int cam_n = 0;
+  bool ivl = false;  // this env casts its cameras from the interval table (else from the shared fan)
   {
     EmitterRaw rec;
     rec.a = make_uint4(0u, 0u, 0u, 0u);
@@ -2307,11 +2375,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     const bool cam_ok = !live_cam || (py_mod360(cm.heading + cm.speed * 1.0) == f_heading && cm.speed == f_speed &&
                                       cm.fov == f_fov && cm.num_rays == f_rays && cm.range == f_range);
     // patrol index, step and length fit the packed bytes: a cached guard has <= kConePath points
-    const bool ok = p.fan_on && p.ray_mode == 0 && !s.done && f_uniq >= 0 && f_range == kTieMaxRange &&
-                    __ballot(!cam_ok || (live_guard && !cached)) == 0ull;
-    if (!ok) {
+    const bool base_ok = p.ray_mode == 0 && !s.done && __ballot(live_guard && !cached) == 0ull;
+    const bool fan_ok = p.fan_on && f_uniq >= 0 && f_range == kTieMaxRange && __ballot(!cam_ok) == 0ull;
+    // the interval fans need range 6 (12 samples, the table's), a fan narrower than half a
+    // turn (signed angle differences) and rays farther apart than two axis margins (at most
+    // one ray near any cut)
+    const double su_ = (cm.fov / (double)cm.num_rays) * kFanUnitsPerDeg;
+    const bool ivl_cam = !live_cam || (cm.range == kTieMaxRange && cm.num_rays >= 1 && cm.fov > 0.0 &&
+                                       cm.fov < 179.0 && su_ > 2.0 * (double)kFanMarginAxis + 8.0);
+    ivl = base_ok && !fan_ok && p.interval_fans && __ballot(!ivl_cam) == 0ull;
+    if (!base_ok || (!fan_ok && !ivl)) {
       step_multi_body<1, 4, 4, D, false, 0>(p, K, actions, obs, rew, rew64, done_out, status_out, auto_reset, smem, e);
       return;
+    }
+    if (live_cam) {
+      fovd = cm.fov;
+      su = su_;
+      isu = 1.0 / su_;
+      cam_n = cm.num_rays;
     }
   }
 
@@ -2381,7 +2462,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     dma_cone(idx, slot, par);
   };
   dma_next_cone(0);
-  dma_fan(0, true);
+  if (ivl) {  // the interval table into the staging space (LDS-DMA, 16 B per lane per pass)
+    for (uint32_t o = 0; o < (uint32_t)sizeof(IvlTable); o += 1024u)
+      if (o + 16u * (uint32_t)lane < (uint32_t)sizeof(IvlTable))
+        lds_dma16(reinterpret_cast<const unsigned char*>(&kIvlTable) + o + 16u * (uint32_t)lane, stg_a + o);
+  } else {
+    dma_fan(0, true);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   // the cached guards' cone rows (staging parity par) ORed into the plane: lane 15 i + j
@@ -2437,8 +2524,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
   // unique directions -- from the staging, or (the reset pass, after the next tick's DMA
   // took the staging) from the table -- with the table's near-tie rays on the exact path,
   // then the cached cones
-  auto cast = [&](int k, int n_uniq, int n_tie, int par, bool staged, bool staged_wide) {
-    reinterpret_cast<uint4*>(vis)[lane] = make_uint4(0u, 0u, 0u, 0u);  // 64 x 16 B = the plane
+  auto cast_fan = [&](int k, int n_uniq, int n_tie, int par, bool staged, bool staged_wide) {
+#pragma unroll
+    for (int z = 0; z < D / 1024; ++z)  // 64 x 16 B per pass: the plane
+      reinterpret_cast<uint4*>(vis)[lane + 64 * z] = make_uint4(0u, 0u, 0u, 0u);
     if (s.n_cams > 0) {
       const FanTick* f = fan0 + k;
       uint4 o4a = make_uint4(0u, 0u, 0u, 0u), o4b = o4a;
@@ -2476,6 +2565,67 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     }
     stamp_cones(par);
   };
+  // this tick's visibility from the interval table (an env the shared fan does not serve):
+  // per camera, lane l takes interval jb + l (then + 64 ...) from the one holding the fan's
+  // first ray.  With t_i = i * su the ray angles past the camera's fixed-point start h0 (the
+  // reference's ray i at hmh + fov * i / n, security.py:70, within 2 units), and rel = cut j
+  // - h0: ic = the first ray above cut j + margin; interval j is marched iff ray ic lies
+  // below cut j+1 - its margin, and ray ic - 1 takes the exact path iff it lies within cut
+  // j's margin.  Neighbouring lanes compare the same products with the same bounds, so every
+  // ray is classified once (tests/test_fan_intervals.py restates this and checks it against
+  // the oracle's cones).
+  auto cast_ivl = [&](int par) {
+#pragma unroll
+    for (int z = 0; z < D / 1024; ++z)  // 64 x 16 B per pass: the plane
+      reinterpret_cast<uint4*>(vis)[lane + 64 * z] = make_uint4(0u, 0u, 0u, 0u);
+    const double hmh = heading - fovd / 2.0;  // camera lanes: security.py:64, :70
+    const double hu = (hmh < 0.0 ? hmh + 360.0 : hmh) * kFanUnitsPerDeg;
+    const uint32_t h0v = hu >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)hu;
+    for (int m = 0; m < s.n_cams; ++m) {
+      const uint32_t h0 = (uint32_t)__builtin_amdgcn_readlane((int)h0v, m);
+      const double sm = uni_lane(su, m), im = uni_lane(isu, m);
+      const int n = __builtin_amdgcn_readlane(cam_n, m);
+      const double tn = (double)n * sm;
+      const uint32_t rcm = (uint32_t)__builtin_amdgcn_readlane((int)cam_rc, m);
+      const uint32_t row = rcm & 0xffu, col = rcm >> 8;
+      const uint32_t own = base + (row + kRing) * PC + col + kRing;
+      const float mx = __builtin_bit_cast(float, base + col + kRing), my = __builtin_bit_cast(float, row + kRing);
+      int jb = __builtin_amdgcn_readfirstlane((int)L.ivl->idx[__umulhi(h0, 360u)]) - 1;
+      if (jb < 0) jb += kFanCuts;
+      for (int c0 = 0; c0 < kFanCuts; c0 += 64) {
+        int j = jb + c0 + lane;
+        j = j >= kFanCuts ? j - kFanCuts : j;
+        j = j >= kFanCuts ? j - kFanCuts : j;
+        const int jn = j + 1 == kFanCuts ? 0 : j + 1;
+        const uint32_t cut = L.ivl->cut[j], cutn = L.ivl->cut[jn];
+        const double rel = (double)(int)(cut - h0), reln = (double)(int)(cutn - h0);
+        const double mj = (cut & 0x3FFFFFFFu) ? (double)kFanMarginTie : (double)kFanMarginAxis;
+        const double mn = (cutn & 0x3FFFFFFFu) ? (double)kFanMarginTie : (double)kFanMarginAxis;
+        const double lo = rel + mj;
+        int ic = lo < 0.0 ? 0 : (int)__builtin_floor(lo * im) + 1;
+        ic = ic > n + 1 ? n + 1 : ic;
+        if (ic >= 1 && (double)(ic - 1) * sm > lo) --ic;
+        if (ic <= n && (double)ic * sm <= lo) ++ic;
+        const bool valid = rel - mj <= tn;
+        const bool safe = valid && ic <= n && (double)ic * sm < reln - mn;
+        const bool near = valid && ic >= 1 && (double)(ic - 1) * sm >= rel - mj;
+        if (safe) {
+          const float2 d = L.ivl->dir[j];
+          march_fast<D, 2 * kTieMaxRange, false, false>(PC, own, d.x, d.y, mx, my, 2 * kTieMaxRange);
+        }
+        if (__ballot(near))
+          ivl_tie_rays<D, PC>(smem, near ? ic - 1 : -1, uni_lane(hmh, m), uni_lane(fovd, m), n, rcm, p.half_deg);
+        if (!__builtin_amdgcn_readlane((int)valid, 63)) break;
+      }
+    }
+    stamp_cones(par);
+  };
+  auto cast = [&](int k, int n_uniq, int n_tie, int par, bool staged, bool staged_wide) {
+    if (ivl)
+      cast_ivl(par);
+    else
+      cast_fan(k, n_uniq, n_tie, par, staged, staged_wide);
+  };
 
   constexpr uint32_t kOOB = 0x40000000u;  // a store offset past every buffer descriptor below
   uint32_t vact = 0;  // lane j: the action of tick 64 c + j (the current 64-tick chunk)
@@ -2485,8 +2635,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     if ((k & 63) == 0) vact = k + lane < K ? L.act[k + lane] : 0u;
     // the DMA issued a tick ago (older than the previous tick's kLeanStores stores) has landed
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLeanStores) : "memory");
-    const int n_uniq = __builtin_amdgcn_readfirstlane(L.stg->hdr[2]);
-    const int n_tie = __builtin_amdgcn_readfirstlane(L.stg->hdr[3]);
+    const int n_uniq = ivl ? 0 : __builtin_amdgcn_readfirstlane(L.stg->hdr[2]);
+    const int n_tie = ivl ? 0 : __builtin_amdgcn_readfirstlane(L.stg->hdr[3]);
     const bool staged_wide = wide;
     const bool frozen = s.done != 0;  // finished, no auto-reset: environment.py:232-233
     double reward = 0.0;
@@ -2522,12 +2672,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       cast(k, n_uniq, n_tie, par, true, staged_wide);
     }
     // the staging is free: tick k + 1's fan entry (a frozen env keeps its plane and skips it)
-    if (k + 1 < K && !frozen) dma_fan(k + 1, n_uniq > 64);
+    if (k + 1 < K && !frozen && !ivl) dma_fan(k + 1, n_uniq > 64);
     wide = n_uniq > 64;
     // the plane's channel-1 quads (also the detection test's byte)
-    uint32_t v1[kObsQ];
+    uint32_t v1[Q];
 #pragma unroll
-    for (int j = 0; j < kObsQ; ++j) {
+    for (int j = 0; j < Q; ++j) {
       const int q = lane + 64 * j, qc = q < N4 ? q : N4 - 1, r = qc / C4;
       v1[j] = *reinterpret_cast<const uint32_t*>(vis + OFF0 + r * PC + 4 * (qc - r * C4));
     }
@@ -2535,7 +2685,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     if (!frozen) {
       // 4. detection, vault, timeout (environment.py:271-297), in the reference's order
       const int sol = s.pos_r * C_ + s.pos_c, qs = sol >> 2;
-      const uint32_t qv = (uint32_t)__builtin_amdgcn_readlane((int)((qs >> 6) ? v1[1] : v1[0]), qs & 63);
+      uint32_t vq = v1[0];  // the quad holding the solver's tile (register qs >> 6, wave-uniform)
+#pragma unroll
+      for (int j = 1; j < Q; ++j) vq = (qs >> 6) == j ? v1[j] : vq;
+      const uint32_t qv = (uint32_t)__builtin_amdgcn_readlane((int)vq, qs & 63);
       if ((qv >> (8 * (sol & 3))) & 0xffu) {
         s.detected = 1;
         reward += p.r_detect;
@@ -2579,7 +2732,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       if (moved) {  // the plane again from the reset poses (the staging holds tick k + 1's fan now)
         cast(k, n_uniq, n_tie, par, false, false);
 #pragma unroll
-        for (int j = 0; j < kObsQ; ++j) {
+        for (int j = 0; j < Q; ++j) {
           const int q = lane + 64 * j, qc = q < N4 ? q : N4 - 1, r = qc / C4;
           v1[j] = *reinterpret_cast<const uint32_t*>(vis + OFF0 + r * PC + 4 * (qc - r * C4));
         }
@@ -2596,7 +2749,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     const int sol = s.pos_r * C_ + s.pos_c, qs = sol >> 2;
     const int vault = p.vr * C_ + p.vc;
 #pragma unroll
-    for (int j = 0; j < kObsQ; ++j) {
+    for (int j = 0; j < Q; ++j) {
       const int q = lane + 64 * j;
       const bool in = q < N4;
       const int qc = in ? q : N4 - 1;
@@ -3270,11 +3423,19 @@ hipError_t launch_step_multi(const EnvParams& p, int K, const int64_t* actions, 
     return hipGetLastError();
   }
   // the lean one-wave kernel (step_lean_kernel): the default for 20 x 20 grids at one wave per env
-  if (p.lean && p.multi_waves == 1 && p.R == 20 && p.C == 20 && p.vis_gap == 1024 && p.probe_mode == 0 && !p.stamps &&
-      !p.sample_counter && !p.redo_counter && p.max_cams + p.max_guards <= kMaxEmitters) {
+  // (20 x 20 at one wave per env; 32 x 32 at any batch size: its lean form is one wave per env
+  // whatever multi_waves says, the envs it cannot serve taking the one-wave generic body)
+  const bool lean20 = p.multi_waves == 1 && p.R == 20 && p.C == 20 && p.vis_gap == 1024;
+  const bool lean32 = p.R == 32 && p.C == 32 && p.vis_gap == 2048;
+  if (p.lean && (lean20 || lean32) && p.probe_mode == 0 && !p.stamps && !p.sample_counter && !p.redo_counter &&
+      p.max_cams + p.max_guards <= kMaxEmitters) {
     if (p.fan_on && p.fan_fill) hipLaunchKernelGGL(fan_kernel, dim3(kFanTicks), dim3(kFanRays), 0, st, p);
-    hipLaunchKernelGGL((step_lean_kernel<20, 20>), dim3(p.n_envs), dim3(64), lean_lds_bytes(p, K), st, p, K, actions,
-                       obs, rew, rew64, done_out, status_out, auto_reset);
+    if (lean20)
+      hipLaunchKernelGGL((step_lean_kernel<20, 20>), dim3(p.n_envs), dim3(64), lean_lds_bytes(p, K), st, p, K, actions,
+                         obs, rew, rew64, done_out, status_out, auto_reset);
+    else
+      hipLaunchKernelGGL((step_lean_kernel<32, 32>), dim3(p.n_envs), dim3(64), lean_lds_bytes(p, K), st, p, K, actions,
+                         obs, rew, rew64, done_out, status_out, auto_reset);
     return hipGetLastError();
   }
 #define HEIST_MULTI_CASE(W, U, O, D)                                                                        \

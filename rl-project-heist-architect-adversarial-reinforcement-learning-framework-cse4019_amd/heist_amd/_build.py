@@ -59,6 +59,15 @@ def needs_build():
     return max(_mtime(d) for d in deps) > _mtime(LIB_PATH)
 
 
+def _stale(src, obj):
+    """obj needs compiling: older than its source, any shared header, or this script (the
+    flags).  heist_env.hip alone takes ~4 min, so an edit elsewhere does not rebuild it."""
+    deps = [os.path.join(CSRC, src), __file__] + [os.path.join(CSRC, f) for f in HEADERS]
+    if src == "heist_capi.hip":
+        deps.append(os.path.join(INCLUDE, "heist.h"))
+    return max(_mtime(d) for d in deps) > _mtime(obj)
+
+
 def build(force=False, verbose=False, jobs=4):
     if not force and not needs_build():
         return LIB_PATH
@@ -66,11 +75,13 @@ def build(force=False, verbose=False, jobs=4):
     procs, objs = [], []
     for src in SOURCES:
         obj = os.path.join(BUILD_DIR, src.replace(".hip", ".o"))
+        objs.append(obj)
+        if not force and not _stale(src, obj):
+            continue
         cmd = [HIPCC] + CFLAGS + FILE_FLAGS.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
-        objs.append(obj)
         if len([p for _, p in procs if p.poll() is None]) >= jobs:
             procs[0][1].wait()
     for src, p in procs:

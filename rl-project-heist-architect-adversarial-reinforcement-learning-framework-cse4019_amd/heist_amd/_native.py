@@ -53,6 +53,7 @@ SIGNATURES = {
     "heist_arch_update_sequence": (_i, [ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_vp), _vp, _i, _i,
                                         _vp, _i, _vp, _d, _d, _d, _d, _d, _vp, _vp, _vp]),
     "heist_arch_update_timed_out": (_i, [_vp, ctypes.POINTER(_i), _vp]),
+    "heist_arch_update_status": (_i, [_vp, ctypes.POINTER(_i), _vp]),
     "heist_arch_update_stamps": (_i, [_vp]),
     "heist_gae": (_i, [_vp, _vp, _vp, _vp, _i, _i, _d, _d, _vp, _vp, _vp]),
     "heist_adv_moments": (_i, [_vp, _i64, _i, _vp, _vp]),

@@ -295,21 +295,29 @@ class ArchitectAgent:  # agents/architect.py:16-170
                 vl = self._kernel_steps(r32)
                 done = torch.cuda.Event()
                 done.record(torch.cuda.current_stream(d))
+                side = torch.cuda.current_stream(d)
 
                 def finish():
+                    # the launch's status word (copied behind it) is read where the host
+                    # waits for the losses anyway; an invalid launch is undone and re-run
+                    done.synchronize()
+                    vl_ = vl
+                    if self._kernel_failed():
+                        with torch.cuda.stream(side):
+                            vl_ = self._rerun_after_kernel_failure(r32)
+                        side.synchronize()
                     if join is not None:
                         join.wait_event(done)
-                    return metrics(vl[-1])
+                        join.wait_stream(side)
+                    return metrics(vl_[-1])
                 return finish
-            vlast = self._kernel_steps(r32)[-1]
+            vl = self._kernel_steps(r32)
+            torch.cuda.current_stream(d).synchronize()
+            if self._kernel_failed():
+                vl = self._rerun_after_kernel_failure(r32)
+            vlast = vl[-1]
         else:
-            n_eager = k if d.type != "cuda" or k < 8 else 3
-            vlast = None
-            for i in range(n_eager):
-                vlast = self._value_step(r32[i])
-            if n_eager < k:
-                vl = self._replay_steps(r32[n_eager:])
-                vlast = vl[-1]
+            vlast = self._steps_without_kernel(r32)[-1]
         m = metrics(vlast)
         if defer and join is not None and d.type == "cuda":
             join.wait_stream(torch.cuda.current_stream(d))
@@ -330,13 +338,22 @@ class ArchitectAgent:  # agents/architect.py:16-170
         step counts on the value tensors, 128-byte aligned weights."""
         if self.device.type != "cuda" or os.environ.get("HEIST_ARCH_UPDATE", "kernel") != "kernel":
             return False
+        if getattr(self, "_kernel_disabled", False):  # a launch of this agent came back invalid
+            return False
         from .. import _native
         if not _native.lib().heist_arch_update_supported(self.grid_rows, self.grid_cols):
+            return False
+        # its 64 workgroups (one CU each: ~141 KB of LDS) must all be resident at once
+        if torch.cuda.get_device_properties(self.device).multi_processor_count < 64:
             return False
         if len(self.optimizer.param_groups) != 1:
             return False
         grp = self.optimizer.param_groups[0]
         if grp.get("weight_decay", 0) != 0 or grp.get("amsgrad") or grp.get("maximize") or grp.get("differentiable"):
+            return False
+        # fused / capturable Adam (the graph path switches capturable on) form the bias
+        # corrections on the device in float32: not the foreach scalars the kernel reproduces
+        if grp.get("fused") or grp.get("capturable"):
             return False
         ps = self.value_parameters()
         if any(p.data_ptr() % 128 for p in (ps[2], ps[4], ps[8])) or not all(p.is_contiguous() for p in ps):
@@ -383,15 +400,73 @@ class ArchitectAgent:  # agents/architect.py:16-170
             grid = self._grid_dev = self.grid_state().contiguous()  # the constant input, made once
         arr = lambda ts: (_native._vp * 12)(*[t.data_ptr() for t in ts])  # noqa: E731
         self.optimizer.zero_grad(set_to_none=True)
+        # a copy of everything the launch overwrites: restored if its status word says the
+        # results are invalid (heist_arch_update_status; a device-side copy, ~4 MB)
+        state = [self.optimizer.state[p] for p in ps]
+        live = ps + [st["exp_avg"] for st in state] + [st["exp_avg_sq"] for st in state]
+        snap = getattr(self, "_au_snap", None)
+        if snap is None or len(snap) != len(live) or any(a.shape != b.shape for a, b in zip(snap, live)):
+            snap = self._au_snap = [torch.empty_like(t) for t in live]
+        torch._foreach_copy_(snap, [t.detach() for t in live])
         _native.check(_native.lib().heist_arch_update_sequence(
             arr(ps), arr([self.optimizer.state[p]["exp_avg"] for p in ps]),
             arr([self.optimizer.state[p]["exp_avg_sq"] for p in ps]), _native.ptr(grid), self.grid_rows,
             self.grid_cols, _native.ptr(r), k, _native.ptr(sc), float(beta1), float(beta2), float(grp["eps"]),
             0.5, float(self.value_coeff), _native.ptr(vl), _native.ptr(ws), _native.stream(d)),
             "heist_arch_update_sequence")
+        # the launch's status word behind it, into pinned memory (read by _kernel_failed)
+        stw = getattr(self, "_au_status", None)
+        if stw is None:
+            stw = self._au_status = torch.zeros(1, dtype=torch.int32).pin_memory()
+        off = (nb - 252) // 4  # heist.h: the uint32 at byte offset workspace_bytes - 252
+        stw.copy_(ws[off:off + 1].view(torch.int32), non_blocking=True)
+        self._au_pending = k
         for p in ps:
             self.optimizer.state[p]["step"].add_(float(k))
         return vl
+
+    def _kernel_failed(self) -> bool:
+        """True if the last heist_arch_update_sequence launch reported invalid results (its
+        status word, copied behind it; the caller has synchronised with the launch)."""
+        if not getattr(self, "_au_pending", 0):
+            return False
+        return int(self._au_status[0]) != 0
+
+    def _rerun_after_kernel_failure(self, r32: torch.Tensor) -> torch.Tensor:
+        """Undo an invalid launch (weights, moments and step counters back to the snapshot
+        taken before it), stop using the kernel in this agent, and run the same k steps on
+        the eager / graph path.  Returns their value losses."""
+        import warnings
+        k = self._au_pending
+        code = int(self._au_status[0])
+        ps = self.value_parameters()
+        state = [self.optimizer.state[p] for p in ps]
+        live = ps + [st["exp_avg"] for st in state] + [st["exp_avg_sq"] for st in state]
+        with torch.no_grad():
+            torch._foreach_copy_(live, self._au_snap)
+        for st in state:
+            st["step"].sub_(float(k))
+        self._au_pending = 0
+        self._kernel_disabled = True
+        warnings.warn("heist_arch_update_sequence reported invalid results (status %d: %s); the %d steps were "
+                      "undone and re-run on the %s path, which this agent keeps using"
+                      % (code, "grid barrier timed out" if code & 1 else "input has > 64 nonzeros", k,
+                         "graph" if self.device.type == "cuda" else "eager"), RuntimeWarning)
+        return self._steps_without_kernel(r32)
+
+    def _steps_without_kernel(self, r32: torch.Tensor) -> torch.Tensor:
+        """update_sequence without the persistent kernel: the first steps eager (the graph
+        capture's warm-up), the rest by graph replay; returns the last value loss (or the
+        losses of the replayed ones)."""
+        d = self.device
+        k = int(r32.numel())
+        n_eager = k if d.type != "cuda" or k < 8 else 3
+        out = []
+        for i in range(n_eager):
+            out.append(self._value_step(r32[i]).reshape(1))
+        if n_eager < k:
+            out.append(self._replay_steps(r32[n_eager:]))
+        return torch.cat(out)
 
     def _value_step(self, r: torch.Tensor) -> torch.Tensor:
         """One eager single-reward step (update() with len(rewards) == 1); returns the value loss."""

@@ -10,6 +10,7 @@ different device and library); parameters whose gradient is cancellation noise (
 noise, get only Adam's lr bound on their step.  kat.json's architect_reward table pins
 calculate_architect_reward (rewards.py:43-73).
 """
+import ctypes
 import os
 
 import numpy as np
@@ -399,3 +400,104 @@ def test_transition_buffer_batches_read_as_lists():
     u.add_batch(torch.tensor([7.0, 8.0]))
     u.materialize()
     assert torch.equal(torch.stack(u), torch.tensor([7.0, 8.0]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("defer", [False, True])
+def test_architect_update_kernel_timeout_is_detected_and_undone(gpu_device, monkeypatch, defer):
+    """A persistent launch whose grid barriers give up (HEIST_ARCH_SPIN_LIMIT=0: the first
+    poll that finds the counter short times out, as a lost co-residency would) reports it in
+    its status word (heist_arch_update_status bit 0); update_sequence then restores the
+    weights, moments and step counters it snapshotted before the launch, warns, re-runs the
+    same steps on the graph path and keeps using that path: the result equals a run that
+    took the graph path from the start.  Nothing corrupted survives the failed launch."""
+    import warnings
+    from heist_amd import _native
+    monkeypatch.setenv("HEIST_ARCH_UPDATE", "kernel")
+    g = torch.Generator().manual_seed(17)
+    k = 24
+    lp, v, r = (torch.randn(k, generator=g, dtype=torch.float64) for _ in range(3))
+    torch.manual_seed(5)
+    a = ArchitectAgent(grid_rows=12, grid_cols=12, device=gpu_device)
+    b = ArchitectAgent(grid_rows=12, grid_cols=12, device=gpu_device)
+    b.network.load_state_dict(a.network.state_dict())
+    assert a._kernel_ok()
+    monkeypatch.setenv("HEIST_ARCH_SPIN_LIMIT", "0")
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        if defer:
+            side = a.side_stream()
+            with torch.cuda.stream(side):
+                fin = a.update_sequence(lp, v, r, defer=True, join=torch.cuda.current_stream(gpu_device))
+            ma = fin()
+        else:
+            ma = a.update_sequence(lp, v, r)
+    assert any("invalid results (status 1" in str(x.message) for x in w), [str(x.message) for x in w]
+    st = ctypes.c_int(-1)
+    _native.check(_native.lib().heist_arch_update_status(_native.ptr(a._au_ws), ctypes.byref(st),
+                                                         _native.stream(gpu_device)), "status")
+    assert st.value & 1
+    assert not a._kernel_ok()  # the agent stays on the graph path
+    monkeypatch.delenv("HEIST_ARCH_SPIN_LIMIT")
+    monkeypatch.setenv("HEIST_ARCH_UPDATE", "graph")
+    mb = b.update_sequence(lp, v, r)
+    assert abs(ma["architect_value_loss"] - mb["architect_value_loss"]) < 1e-6
+    for (n, p), q in zip(a.network.state_dict().items(), b.network.state_dict().values()):
+        assert float((p - q).abs().max()) <= 1e-6, n
+    for p, q in zip(a.value_parameters(), b.value_parameters()):
+        assert float(a.optimizer.state[p]["step"]) == float(b.optimizer.state[q]["step"]) == k
+
+
+@pytest.mark.gpu
+def test_architect_update_status_flags_too_many_nonzeros(gpu_device):
+    """heist_arch_update_sequence on an input plane with more than 64 nonzero pixels: the
+    launch drains and its status word says bit 1 (results invalid); a 2-pixel plane (the
+    Architect's state) reports 0."""
+    from heist_amd import _native
+    torch.manual_seed(2)
+    for nnz, want in ((2, 0), (100, 2)):
+        a = ArchitectAgent(grid_rows=12, grid_cols=12, device=gpu_device)
+        ps = a.value_parameters()
+        ms = [torch.zeros_like(p) for p in ps]
+        vs = [torch.zeros_like(p) for p in ps]
+        grid = torch.zeros(144, device=gpu_device)
+        grid[torch.randperm(144)[:nnz]] = 1.0
+        nb = int(_native.lib().heist_arch_update_workspace_bytes())
+        ws = torch.empty((nb + 3) // 4, dtype=torch.float32, device=gpu_device)
+        rew = torch.tensor([0.5, -0.25], device=gpu_device)
+        sc = torch.tensor([[-1e-3 / 0.1, 0.001 ** 0.5], [-1e-3 / 0.19, 0.002 ** 0.5]], device=gpu_device)
+        vl = torch.empty(2, device=gpu_device)
+        arr = lambda ts: (_native._vp * 12)(*[t.data_ptr() for t in ts])  # noqa: E731
+        _native.check(_native.lib().heist_arch_update_sequence(
+            arr(ps), arr(ms), arr(vs), _native.ptr(grid), 12, 12, _native.ptr(rew), 2, _native.ptr(sc), 0.9, 0.999,
+            1e-8, 0.5, 0.5, _native.ptr(vl), _native.ptr(ws), _native.stream(gpu_device)), "sequence")
+        st = ctypes.c_int(-1)
+        _native.check(_native.lib().heist_arch_update_status(_native.ptr(ws), ctypes.byref(st),
+                                                             _native.stream(gpu_device)), "status")
+        assert st.value == want, (nnz, st.value)
+
+
+@pytest.mark.gpu
+def test_architect_kernel_not_used_after_graph_path(gpu_device, monkeypatch):
+    """The graph path switches Adam to capturable (bias corrections formed on the device in
+    float32); the kernel reproduces the foreach scalars, so _kernel_ok refuses capturable (and
+    fused) groups and a graph -> kernel switch keeps replaying: the result equals an
+    all-graph run of the same steps."""
+    g = torch.Generator().manual_seed(23)
+    lp, v, r = (torch.randn(40, generator=g, dtype=torch.float64) for _ in range(3))
+    torch.manual_seed(6)
+    a = ArchitectAgent(grid_rows=12, grid_cols=12, device=gpu_device)
+    b = ArchitectAgent(grid_rows=12, grid_cols=12, device=gpu_device)
+    b.network.load_state_dict(a.network.state_dict())
+    monkeypatch.setenv("HEIST_ARCH_UPDATE", "graph")
+    a.update_sequence(lp[:20], v[:20], r[:20])
+    b.update_sequence(lp[:20], v[:20], r[:20])
+    b.update_sequence(lp[20:], v[20:], r[20:])
+    monkeypatch.setenv("HEIST_ARCH_UPDATE", "kernel")
+    assert a.optimizer.param_groups[0]["capturable"] and not a._kernel_ok()
+    a.update_sequence(lp[20:], v[20:], r[20:])
+    for (n, p), q in zip(a.network.state_dict().items(), b.network.state_dict().values()):
+        assert torch.equal(p, q), n
+    c = ArchitectAgent(grid_rows=12, grid_cols=12, device=gpu_device)
+    c.optimizer.param_groups[0]["fused"] = True
+    assert not c._kernel_ok()

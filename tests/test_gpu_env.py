@@ -776,6 +776,118 @@ def test_step_lean_wide_fans_and_many_guards(gpu_device, monkeypatch, fov, auto_
         assert torch.equal(sa[key], sb[key]), key
 
 
+def _interval_fan_layouts(n, R, budget, seed):
+    """Synthetic layouts (every camera its own fov, heading, speed: the shared fan serves
+    none) with some cameras forced onto the hard cases of the interval fans: the reference's
+    default camera (heading 0, fov 60, speed 15: rays on whole and half degrees, on the axes),
+    rays a few angle units from a cut, fovs up to 120 degrees (two 64-lane interval chunks)."""
+    from heist_amd.layouts import synthetic_layouts
+    rng = np.random.default_rng(seed)
+    cuts = [0.0, 4.7885, 30.0, 41.4096, 45.0, 60.0, 90.0, 135.0, 180.0, 270.0]
+    out = []
+    for walls, cams, guards in synthetic_layouts(n, R, R, budget, seed=seed):
+        cams = [dict(c) for c in cams]
+        for c in cams:
+            u = rng.random()
+            if u < 0.15:
+                c.update(fov_angle=60.0, heading=0.0, rotation_speed=15.0)
+            elif u < 0.3:  # ray i on (about) a cut angle at the first K-tick tick (one rotation)
+                fov = float(np.float32(rng.uniform(30, 120)))
+                nr = max(int(fov * 2), 30)
+                i = int(rng.integers(0, nr + 1))
+                cut = float(rng.choice(cuts)) + float(rng.choice([0.0, 3e-6, -3e-6, 1e-7]))
+                c.update(fov_angle=fov, heading=(cut + fov / 2.0 - fov * i / nr - c["rotation_speed"]) % 360.0)
+            elif u < 0.4:
+                c.update(fov_angle=float(np.float32(rng.uniform(100, 120))))
+        out.append((walls, cams, guards))
+    return out
+
+
+@pytest.mark.parametrize("auto_reset", [True, False], ids=["auto_reset", "no_reset"])
+@pytest.mark.parametrize("n,budget", [(4096, 15), (512, 40)], ids=["bench4096", "budget40"])
+def test_step_lean_interval_fans(gpu_device, monkeypatch, n, budget, auto_reset):
+    """step_lean_kernel's interval fans (cameras the shared fan does not serve: the synthetic
+    mix) == single ticks, == the generic K-tick body (HEIST_INTERVAL_FANS=0), and 32 envs ==
+    the C oracle (reward, done, status, observation bytes) on every tick; short episodes,
+    launches of 1, 20, 63 and 70 ticks.  Reference environment.py:216-299, security.py:53-101."""
+    R = 20
+    cfg = EnvironmentConfig(max_steps=40, architect_budget=budget)
+    lays = _interval_fan_layouts(n, R, budget, 300 + budget)
+    envs = []
+    monkeypatch.setenv("HEIST_MULTI_WAVES", "1")
+    for ivl in ("1", "0", "1"):
+        monkeypatch.setenv("HEIST_INTERVAL_FANS", ivl)
+        env = HeistEnv(n, cfg, max_cams=max(1, budget // 3), max_guards=max(1, budget // 5), max_path=16,
+                       device=gpu_device)
+        v = env.set_layouts(lays, budget=budget)
+        env.reset()
+        envs.append((env, v))
+    monkeypatch.delenv("HEIST_INTERVAL_FANS")
+    (a, va), (c, vc), (b, vb) = envs
+    assert torch.equal(va, vb) and torch.equal(va, vc)
+    assert a.kernel_config()["interval_fans"] == 1 and c.kernel_config()["interval_fans"] == 0
+    assert a.kernel_config()["lean"] == 1 and a.kernel_config()["multi_waves"] == 1
+    valid = va.cpu().numpy().astype(bool)
+    pick = np.random.default_rng(budget).choice(np.nonzero(valid)[0], 32, replace=False)
+    pick_t = torch.from_numpy(pick).to(gpu_device)
+    oracles = _oracle_envs(cfg, [lays[i] for i in pick], budget)
+    g = torch.Generator(device="cpu").manual_seed(79)
+    acts = torch.randint(0, 5, (160, n), generator=g).to(gpu_device)
+    k0 = 0
+    for kk in (1, 20, 63, 70):
+        oa = a.step_multi(acts[k0:k0 + kk], auto_reset=auto_reset, reward64=True)
+        oc = c.step_multi(acts[k0:k0 + kk], auto_reset=auto_reset, reward64=True)
+        for x, y in zip(oa, oc):
+            assert torch.equal(x, y), k0
+        obs_p = oa[0][:, pick_t].cpu().numpy()
+        r64p, dp, sp = (x[:, pick_t].cpu().numpy() for x in (oa[4], oa[2], oa[3]))
+        ap = acts[k0:k0 + kk, pick_t].cpu().numpy()
+        for k in range(kk):
+            o, r, d, s = b.step(acts[k0 + k], auto_reset=auto_reset)
+            ctx = "tick %d" % (k0 + k)
+            assert torch.equal(oa[0][k], o), ctx
+            assert torch.equal(oa[4][k], b.reward64) and torch.equal(oa[2][k], d) and torch.equal(oa[3][k], s), ctx
+            for j in range(len(pick)):
+                r_, d_, s_ = oracles[j].step(int(ap[k, j]))
+                if d_ and auto_reset:
+                    oracles[j].reset()
+                assert (r64p[k, j], bool(dp[k, j]), int(sp[k, j])) == (r_, d_, s_), "env %d %s" % (pick[j], ctx)
+                assert obs_p[k, j].tobytes() == oracles[j].state_tensor().tobytes(), "env %d %s" % (pick[j], ctx)
+        k0 += kk
+    sa, sb = a.export(grid=True), b.export(grid=True)
+    for key in sb:
+        assert torch.equal(sa[key], sb[key]), key
+
+
+def test_step_lean_interval_fans_on_architect_layouts(gpu_device, monkeypatch):
+    """The headline's Architect layouts with the shared fan table off (HEIST_SHARED_FAN=0):
+    every env takes the interval fans instead; == single ticks, 60 ticks."""
+    import os
+    from heist_amd.layouts import architect_checkpoint_layouts
+    ckpt = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "checkpoints",
+                        "architect_c2_fixed.pt")
+    n, budget = 4096, 15
+    cfg = EnvironmentConfig(architect_budget=budget, max_steps=30)
+    envs = []
+    for fan in ("0", "1"):
+        monkeypatch.setenv("HEIST_SHARED_FAN", fan)
+        env = HeistEnv(n, cfg, max_cams=5, max_guards=3, max_path=16, device=gpu_device)
+        _, ok = architect_checkpoint_layouts(env, budget, seed=1234, ckpt=ckpt)
+        assert ok
+        env.reset()
+        envs.append(env)
+    monkeypatch.delenv("HEIST_SHARED_FAN")
+    a, b = envs
+    assert a.kernel_config()["fan_on"] == 0 and a.kernel_config()["multi_waves"] == 1
+    g = torch.Generator(device="cpu").manual_seed(81)
+    acts = torch.randint(0, 5, (60, n), generator=g).to(gpu_device)
+    oa = a.step_multi(acts[:60], reward64=True)
+    for k in range(60):
+        o, r, d, s = b.step(acts[k])
+        assert torch.equal(oa[0][k], o) and torch.equal(oa[4][k], b.reward64), k
+        assert torch.equal(oa[2][k], d) and torch.equal(oa[3][k], s), k
+
+
 @pytest.mark.parametrize("waves", [1, 2])
 @pytest.mark.parametrize("cones", [True, False], ids=["guard_cones", "live_guards"])
 def test_step_multi_one_wave_per_env(gpu_device, monkeypatch, cones, waves):

@@ -3,8 +3,8 @@
 # -fno-slp-vectorize (heist_amd/_build.py): ROCm 7.2 clang's packed-fp32 (v_pk_*_f32) forms
 # of the raycast lost a lane's negation (march_fast) and merged the two tie-table lookups
 # (near_tie).  This runs the raycast parity tests against a library built from the same
-# sources WITHOUT the flag (tools/forensic/_ref/libheist_hip_slp.so, made by
-#   HEIST_LIB=$PWD/tools/forensic/_ref/libheist_hip_slp.so \
+# sources WITHOUT the flag (tools/forensic/slp_build/libheist_hip_slp.so, made by
+#   HEIST_LIB=$PWD/tools/forensic/slp_build/libheist_hip_slp.so \
 #   HEIST_ENV_FLAGS="-mllvm -disable-machine-licm" python -c "...; _build.build(force=True)"
 # on the build host) and counts the packed-fp32 instructions in both builds' heist_env code.
 # A failing parity run = the miscompile persists and the flag is still needed; all green =
@@ -15,7 +15,7 @@ cd "${GRAFT_REPO_ROOT:-.}" || exit 1
 OUT=gpurun_out/${TAG:-forensic}
 mkdir -p $OUT
 export TMPDIR=/tmp
-LIB=tools/forensic/_ref/libheist_hip_slp.so
+LIB=tools/forensic/slp_build/libheist_hip_slp.so
 [ -f $LIB ] || { echo "missing $LIB"; exit 1; }
 # llvm-objdump --offloading only EXTRACTS the device bundles (next to the input file), so
 # extract from a copy in a scratch directory and disassemble the gfx950 objects

@@ -1,7 +1,8 @@
 """Where does a heist_step_multi launch spend its time?  The STAMP variant of the K-tick
 kernel (heist_step_stamps armed) sums the shader clock each wave spends in 7 tick segments
 over the launch (SEGS below; "a|b": wave 0 does a, waves 1.. do b).  Workload:
-bench.py's headline (4096 envs, C2 checkpoint layouts, K ticks per launch).
+bench.py's headline (4096 envs, C2 checkpoint layouts, K ticks per launch), or with
+PROBE_LAYOUTS=synthetic the synthetic mix (SURVEY 8d generator ii).
 
 Prints one JSON line: per-segment cycles per tick (mean over waves, by wave index),
 launch lifetime per tick, effective clock (cycles per tick x ticks / launch time)."""
@@ -27,14 +28,21 @@ def main():
     n = int(os.environ.get("PROBE_N", "4096"))
     K = int(os.environ.get("PROBE_K", "20"))
     env = HeistEnv(n, EnvironmentConfig(architect_budget=15), max_cams=5, max_guards=3, max_path=16, device="cuda")
-    bench.architect_layouts(env, 15, seed=1234)
+    if os.environ.get("PROBE_LAYOUTS", "architect") == "synthetic":
+        from heist_amd.layouts import valid_synthetic_layouts
+        valid_synthetic_layouts(env, 15, seed=1234)
+    else:
+        bench.architect_layouts(env, 15, seed=1234)
     env.reset()
     W = env.kernel_config()["multi_waves"]
     acts = torch.randint(0, 5, (4 * K, n), device="cuda")
     for j in range(2):
         env.step_multi(acts[j * K:(j + 1) * K])
-    buf = torch.zeros((n, W, 16), dtype=torch.int64, device="cuda")
-    out = {"n": n, "K": K, "waves": W, "launches": []}
+    # heist_step_multi checks the buffer against both kernels' needs (a launch without a
+    # K-tick variant runs single ticks): n x 10 x step_waves words for heist_step
+    words = max(int(nat.lib().heist_stamp_words(env._h, 0)), int(nat.lib().heist_stamp_words(env._h, 1)))
+    buf = torch.zeros(max(words, n * W * 16), dtype=torch.int64, device="cuda")
+    out = {"layouts": os.environ.get("PROBE_LAYOUTS", "architect"), "n": n, "K": K, "waves": W, "launches": []}
     for j in range(2, 4):
         nat.check(nat.lib().heist_step_stamps(env._h, nat.ptr(buf), buf.numel()), "heist_step_stamps")
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -43,7 +51,7 @@ def main():
         ev1.record()
         nat.check(nat.lib().heist_step_stamps(env._h, None, 0), "heist_step_stamps")
         torch.cuda.synchronize()
-        s = buf.cpu().numpy().astype(np.int64)
+        s = buf[:n * W * 16].reshape(n, W, 16).cpu().numpy().astype(np.int64)
         rec = {"launch_ms": ev0.elapsed_time(ev1)}
         for w in range(W):
             rec["wave%d_cycles_per_tick" % w] = {nm: float(s[:, w, i].mean()) / K for i, nm in enumerate(SEGS)}

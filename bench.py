@@ -47,9 +47,9 @@ def log(msg):
 
 def multi_kernel_name(kcfg, R, C):
     """The K-tick launch's kernel: the lean one-wave kernel for 20 x 20 grids at one wave per env
-    (heist_env.hip step_lean_kernel; envs it cannot serve take the generic body inside the same
-    launch), else step_multi_kernel."""
-    lean = kcfg.get("lean", 0) and kcfg.get("multi_waves") == 1 and R == 20 and C == 20
+    and for 32 x 32 grids (heist_env.hip step_lean_kernel; envs it cannot serve take the generic
+    body inside the same launch), else step_multi_kernel."""
+    lean = kcfg.get("lean", 0) and ((kcfg.get("multi_waves") == 1 and R == 20 and C == 20) or (R == 32 and C == 32))
     return "heist::step_lean_kernel" if lean else "heist::step_multi_kernel"
 
 

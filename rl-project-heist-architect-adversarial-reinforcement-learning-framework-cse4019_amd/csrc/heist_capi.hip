@@ -247,7 +247,8 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   // (HEIST_DISPATCH_ORDER=0, no order[] load) measured 16.29 vs 15.37 us per 4096-env step
   // (profiles/r02bd_probe_dispatch_order.log).
   p.dispatch_order = 1;
-  if (const char* m = getenv("HEIST_DISPATCH_ORDER")) p.dispatch_order = atoi(m) ? 1 : 0;
+  if (const char* m = getenv("HEIST_DISPATCH_ORDER")) p.dispatch_order = atoi(m) >= 2 ? 2 : (atoi(m) ? 1 : 0);
+  p.n_cu = n_cu;
   p.split_obs = 1;
   if (const char* m = getenv("HEIST_SPLIT_OBS")) p.split_obs = atoi(m) ? 1 : 0;
   for (int k = 0; k < 8; ++k) p.tile_lut[k] = k <= 5 ? (float)k / 5.0f : 0.0f;  // environment.py:319

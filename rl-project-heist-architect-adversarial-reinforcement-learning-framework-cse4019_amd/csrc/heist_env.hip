@@ -392,10 +392,18 @@ __device__ __forceinline__ uint64_t pk_fma_k(uint64_t d, uint64_t m) {
   return r;
 }
 
+// row * PC + col as one v_mad_u32_u24 (row < 2^24): with a compile-time PC the compiler
+// otherwise forms the product from a 64-bit funnel shift, a mask and an add (3 VALU)
+__device__ __forceinline__ uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(b), "v"(c));
+  return r;
+}
+
 template <int U, bool VM>
 __device__ __forceinline__ uint32_t fast_addr(uint32_t PC, uint64_t d, uint64_t m) {
   const uint64_t r = pk_fma_k<U + 1, VM>(d, m);
-  return __umul24((uint32_t)(r >> 32), PC) + (uint32_t)r;
+  return mad_u24((uint32_t)(r >> 32), PC, (uint32_t)r);
 }
 
 template <int NS, bool VM, int... Us>
@@ -2265,13 +2273,17 @@ struct LeanLds {
   uint8_t* act;
   LeanStage* stg;  // an env the shared fan serves: the next tick's fan entry
   IvlTable* ivl;   // any other env: the interval table (same LDS)
+  uint4* icam;     // interval fans, per camera: start angle, first cut, rays | tile << 16
+  double* icim;    //   and 1 / ray spacing
+  uint32_t* ivq;   //   the marching queue (128 entries)
   uint16_t* cone;
   float4* plane2;
 };
 // The lean kernel's plane gap D: the padded (R + 12) x (C + 12) plane in 1024 (up to 20 x 20)
 // or 2048 bytes (up to 33 x 33).
 __host__ __device__ constexpr int lean_gap(int R, int C) { return (R + 2 * kRing) * (C + 2 * kRing) <= 1024 ? 1024 : 2048; }
-__host__ __device__ inline size_t lean_carve(unsigned char* smem, int R, int C, int mg, int mp, int K, LeanLds* L) {
+__host__ __device__ inline size_t lean_carve(unsigned char* smem, int R, int C, int mc, int mg, int mp, int K,
+                                             LeanLds* L) {
   size_t o = 3 * (size_t)lean_gap(R, C);
   if (L) L->grid = smem + o;
   o += align16((size_t)R * C);
@@ -2282,6 +2294,12 @@ __host__ __device__ inline size_t lean_carve(unsigned char* smem, int R, int C, 
   if (L) L->stg = reinterpret_cast<LeanStage*>(smem + o);
   if (L) L->ivl = reinterpret_cast<IvlTable*>(smem + o);
   o += align16(kLeanUnion);
+  if (L) L->icam = reinterpret_cast<uint4*>(smem + o);
+  o += 16 * (size_t)(mc > 0 ? mc : 1);
+  if (L) L->icim = reinterpret_cast<double*>(smem + o);
+  o += align16(8 * (size_t)(mc > 0 ? mc : 1));
+  if (L) L->ivq = reinterpret_cast<uint32_t*>(smem + o);
+  o += 4 * 128;
   if (L) L->cone = reinterpret_cast<uint16_t*>(smem + o);
   o += 64 * (size_t)(mg > 0 ? mg : 1);
   if (L) L->plane2 = reinterpret_cast<float4*>(smem + o);
@@ -2289,7 +2307,7 @@ __host__ __device__ inline size_t lean_carve(unsigned char* smem, int R, int C, 
   return o;
 }
 static size_t lean_lds_bytes(const EnvParams& p, int K) {
-  const size_t lean = lean_carve(nullptr, p.R, p.C, p.max_guards, p.max_path, K, nullptr);
+  const size_t lean = lean_carve(nullptr, p.R, p.C, p.max_cams, p.max_guards, p.max_path, K, nullptr);
   const size_t generic = step_multi_lds(p, K);  // the envs that take step_multi_body
   return lean > generic ? lean : generic;
 }
@@ -2398,7 +2416,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
 
   // ---- prologue: the env's layout and state, once per launch
   LeanLds L;
-  lean_carve(smem, R_, C_, mg, mp, K, &L);
+  lean_carve(smem, R_, C_, mc, mg, mp, K, &L);
   uint8_t* const wall = smem;          // [0, D): the padded stop map
   uint8_t* const vis = smem + D;       // [D, 2D): the visibility plane; [2D, 3D): the sink
   const uint32_t base = (uint32_t)(uintptr_t)smem;  // LDS address of the stop map
@@ -2565,59 +2583,103 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     }
     stamp_cones(par);
   };
-  // this tick's visibility from the interval table (an env the shared fan does not serve):
-  // per camera, lane l takes interval jb + l (then + 64 ...) from the one holding the fan's
-  // first ray.  With t_i = i * su the ray angles past the camera's fixed-point start h0 (the
-  // reference's ray i at hmh + fov * i / n, security.py:70, within 2 units), and rel = cut j
-  // - h0: ic = the first ray above cut j + margin; interval j is marched iff ray ic lies
-  // below cut j+1 - its margin, and ray ic - 1 takes the exact path iff it lies within cut
-  // j's margin.  Neighbouring lanes compare the same products with the same bounds, so every
-  // ray is classified once (tests/test_fan_intervals.py restates this and checks it against
-  // the oracle's cones).
+  // this tick's visibility from the interval table (an env the shared fan does not serve).
+  // Ray i of a camera lies i * su angle units past its fixed-point start h0 (the reference's
+  // ray i at hmh + fov * i / n, security.py:70, within 2 units); with rel = cut j - h0 and m
+  // its margin, rays B_j = ceil((rel - m) / su) .. A_j - 1 = floor((rel + m) / su) lie within
+  // the margin (at most one: su > 2 m) and take the exact path, rays A_j .. B_j+1 - 1 lie
+  // inside interval j, which is marched once if there is one.  A and B are pure functions of
+  // the cut, the same in whichever lane evaluates them, so the classes partition the rays
+  // (tests/test_fan_intervals.py restates this and checks it against the oracle's cones).
+  // The env's cameras are packed: camera c needs the cuts jb_c .. je_c - 1 (jb: the last cut
+  // before its first ray, je: the first one past its last ray + margin), and the (camera, cut)
+  // pairs of all cameras fill the lanes 64 at a time; the intervals found to hold a ray go
+  // to an LDS queue that is marched 64 at a time with per-lane origins -- so a wave's lanes
+  // are busy whatever the fan widths, and an env's chain of chunks is as short as its cameras'
+  // total interval count allows.
   auto cast_ivl = [&](int par) {
 #pragma unroll
     for (int z = 0; z < D / 1024; ++z)  // 64 x 16 B per pass: the plane
       reinterpret_cast<uint4*>(vis)[lane + 64 * z] = make_uint4(0u, 0u, 0u, 0u);
-    const double hmh = heading - fovd / 2.0;  // camera lanes: security.py:64, :70
+    // camera lanes: the start angle, the cut range, the pair count
+    const double hmh = heading - fovd / 2.0;  // security.py:64, :70
     const double hu = (hmh < 0.0 ? hmh + 360.0 : hmh) * kFanUnitsPerDeg;
     const uint32_t h0v = hu >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)hu;
-    for (int m = 0; m < s.n_cams; ++m) {
-      const uint32_t h0 = (uint32_t)__builtin_amdgcn_readlane((int)h0v, m);
-      const double sm = uni_lane(su, m), im = uni_lane(isu, m);
-      const int n = __builtin_amdgcn_readlane(cam_n, m);
-      const double tn = (double)n * sm;
-      const uint32_t rcm = (uint32_t)__builtin_amdgcn_readlane((int)cam_rc, m);
-      const uint32_t row = rcm & 0xffu, col = rcm >> 8;
-      const uint32_t own = base + (row + kRing) * PC + col + kRing;
-      const float mx = __builtin_bit_cast(float, base + col + kRing), my = __builtin_bit_cast(float, row + kRing);
-      int jb = __builtin_amdgcn_readfirstlane((int)L.ivl->idx[__umulhi(h0, 360u)]) - 1;
-      if (jb < 0) jb += kFanCuts;
-      for (int c0 = 0; c0 < kFanCuts; c0 += 64) {
-        int j = jb + c0 + lane;
-        j = j >= kFanCuts ? j - kFanCuts : j;
-        j = j >= kFanCuts ? j - kFanCuts : j;
-        const int jn = j + 1 == kFanCuts ? 0 : j + 1;
-        const uint32_t cut = L.ivl->cut[j], cutn = L.ivl->cut[jn];
-        const double rel = (double)(int)(cut - h0), reln = (double)(int)(cutn - h0);
-        const double mj = (cut & 0x3FFFFFFFu) ? (double)kFanMarginTie : (double)kFanMarginAxis;
-        const double mn = (cutn & 0x3FFFFFFFu) ? (double)kFanMarginTie : (double)kFanMarginAxis;
-        const double lo = rel + mj;
-        int ic = lo < 0.0 ? 0 : (int)__builtin_floor(lo * im) + 1;
-        ic = ic > n + 1 ? n + 1 : ic;
-        if (ic >= 1 && (double)(ic - 1) * sm > lo) --ic;
-        if (ic <= n && (double)ic * sm <= lo) ++ic;
-        const bool valid = rel - mj <= tn;
-        const bool safe = valid && ic <= n && (double)ic * sm < reln - mn;
-        const bool near = valid && ic >= 1 && (double)(ic - 1) * sm >= rel - mj;
-        if (safe) {
-          const float2 d = L.ivl->dir[j];
-          march_fast<D, 2 * kTieMaxRange, false, false>(PC, own, d.x, d.y, mx, my, 2 * kTieMaxRange);
+    int cnt = 0;
+    if (live_cam) {
+      const int jb = (int)L.ivl->idx[__umulhi(h0v, 360u)] - 1;  // -1: cut 251 of the turn before
+      const uint64_t e64 = (uint64_t)h0v + (uint64_t)((double)cam_n * su) + (uint64_t)(kFanMarginAxis + 4);
+      const int je = (int)L.ivl->idx[__umulhi((uint32_t)e64, 360u) + 1u] + kFanCuts * (int)(e64 >> 32);
+      cnt = je - jb;
+      L.icam[lane] = make_uint4(h0v, (uint32_t)jb, (uint32_t)cam_n | (cam_rc << 16), 0u);
+      L.icim[lane] = isu;
+    }
+    // exclusive prefix of the pair counts over the camera lanes (bit slices: cnt < 1024)
+    int excl = 0, total = 0;
+#pragma unroll
+    for (int b = 0; b < 10; ++b) {
+      const unsigned long long mb = __ballot((cnt >> b) & 1);
+      excl += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u)) << b;
+      total += __popcll(mb) << b;
+    }
+    const int endv = excl + cnt;  // camera lanes: one past the camera's last pair
+    total = __builtin_amdgcn_readfirstlane(total);
+    int qn = 0;  // marching queue L.ivq: entries j | camera << 8
+    auto march_queue = [&](int n_q) {
+      if (lane < n_q) {
+        const uint32_t ent = L.ivq[lane];
+        const uint32_t rc = L.icam[ent >> 8].z >> 16, row = rc & 0xffu, col = rc >> 8;
+        const uint32_t own = base + (row + kRing) * PC + col + kRing;
+        const float mx = __builtin_bit_cast(float, base + col + kRing), my = __builtin_bit_cast(float, row + kRing);
+        const float2 d = L.ivl->dir[ent & 0xffu];
+        march_fast<D, 2 * kTieMaxRange, false, false, true>(PC, own, d.x, d.y, mx, my, 2 * kTieMaxRange);
+      }
+    };
+    for (int q0 = 0; q0 < total; q0 += 64) {
+      const int q = q0 + lane;
+      int c = 0, start = 0;  // the camera of pair q: those before it end at or below q
+      for (int m = 0; m + 1 < s.n_cams; ++m) {
+        const int em = __builtin_amdgcn_readlane(endv, m);
+        if (q >= em) {
+          c = m + 1;
+          start = em;
         }
-        if (__ballot(near))
-          ivl_tie_rays<D, PC>(smem, near ? ic - 1 : -1, uni_lane(hmh, m), uni_lane(fovd, m), n, rcm, p.half_deg);
-        if (!__builtin_amdgcn_readlane((int)valid, 63)) break;
+      }
+      const uint4 cu = L.icam[c];
+      const double im = L.icim[c];
+      const int n = (int)(cu.z & 0xffffu);
+      int j = (int)cu.y + (q - start);
+      j = j < 0 ? j + kFanCuts : (j >= kFanCuts ? j - kFanCuts : j);
+      const int jn = j + 1 == kFanCuts ? 0 : j + 1;
+      const uint32_t cut = L.ivl->cut[j], cutn = L.ivl->cut[jn];
+      const double rel = (double)(int)(cut - cu.x), reln = (double)(int)(cutn - cu.x);
+      const double mj = (cut & 0x3FFFFFFFu) ? (double)kFanMarginTie : (double)kFanMarginAxis;
+      const double mn = (cutn & 0x3FFFFFFFu) ? (double)kFanMarginTie : (double)kFanMarginAxis;
+      const int A = (int)__builtin_floor((rel + mj) * im) + 1;  // first ray past cut j's margin
+      const int B = (int)__builtin_ceil((rel - mj) * im);       // first ray inside it
+      const int Bn = (int)__builtin_ceil((reln - mn) * im);     // first ray inside cut j+1's
+      const int a0 = A > 0 ? A : 0;
+      const bool act = q < total;
+      const bool safe = act && a0 <= n && a0 < Bn;
+      const bool near = act && B < A && B >= 0 && B <= n;
+      if (__ballot(near)) {  // rare: this pair's camera emitter from its lane, the exact path
+        const double h_c = __shfl(hmh, c, 64), f_c = __shfl(fovd, c, 64);
+        ivl_tie_rays<D, PC>(smem, near ? B : -1, h_c, f_c, n, cu.z >> 16, p.half_deg);
+      }
+      const unsigned long long sb = __ballot(safe);
+      if (safe) {
+        const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(sb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sb, 0u));
+        L.ivq[pos] = (uint32_t)j | ((uint32_t)c << 8);
+      }
+      qn += __popcll(sb);
+      if (qn >= 64) {
+        march_queue(64);
+        const uint32_t rest = L.ivq[64 + lane];
+        if (lane < qn - 64) L.ivq[lane] = rest;
+        qn -= 64;
       }
     }
+    if (qn > 0) march_queue(qn);
     stamp_cones(par);
   };
   auto cast = [&](int k, int n_uniq, int n_tie, int par, bool staged, bool staged_wide) {
@@ -3286,7 +3348,24 @@ __global__ __launch_bounds__(1024) void order_kernel(EnvParams p) {
     }
   }
   __syncthreads();
-  for (int e = t; e < p.n_envs; e += 1024) p.order[atomicAdd(&bucket[key(e)], 1)] = e;
+  // rank i (heaviest first) -> block.  dispatch_order 1: block i.  2 (snake draft): the
+  // K-tick kernels keep every block of a launch resident (16 per CU), the k-th block a CU
+  // receives (block n_cu * k + cu) lands on SIMD k % 4, and a SIMD's time is the sum of its 4
+  // envs' ticks -- so ranks are dealt to the 4 n_cu SIMDs round by round in alternating
+  // direction (round r = rank / (4 n_cu)), which evens the SIMD sums (heaviest-first alone
+  // gives SIMD 0 of every CU the heaviest env of each round); a last partial round keeps its
+  // ranks.
+  const int S = 4 * p.n_cu, full = p.dispatch_order == 2 && p.n_cu > 0 ? p.n_envs / S * S : 0;
+  for (int e = t; e < p.n_envs; e += 1024) {
+    const int i = atomicAdd(&bucket[key(e)], 1);
+    int b = i;
+    if (i < full) {
+      const int r = i / S, pos = i - r * S, sl = (r & 1) ? S - 1 - pos : pos;
+      const int cu = sl % p.n_cu, simd = sl / p.n_cu;
+      b = p.n_cu * (4 * r + simd) + cu;
+    }
+    p.order[b] = e;
+  }
 }
 
 hipError_t launch_order(const EnvParams& p, hipStream_t st) {

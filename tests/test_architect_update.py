@@ -256,9 +256,13 @@ def test_architect_update_long_sequence_drift(gpu_device, monkeypatch):
     fp32 rounding differences get amplified wherever Adam meets a unit crossing its ReLU
     boundary at a different step: single weights part by tens to hundreds of lr and stay
     there, whichever fp32 summation order runs (eager, graph, kernel), while the function the
-    network computes does not drift.  So the bar is "as accurate as eager fp32": V(s0) and the
-    value loss within max(5e-4, 5x eager's own error) of float64, weights within
-    max(0.1, 3x eager's worst weight error); and the kernel bit-for-bit deterministic."""
+    network computes drifts far less.  On this sequence every path holds V(s0) and the value
+    loss within the north_star 1e-4 of float64 (measured: eager 1.7e-5, kernel 1.7e-5, graph
+    1.2e-5; profiles/r05c_arch_drift_seeds.log), and weights within max(0.1, 3x eager's worst
+    weight error); the kernel is bit-for-bit deterministic, so the bound is reproducible.
+    Across other reward sequences eager fp32 itself ends 1e-4 .. 2e-3 from float64 (the same
+    log: 6 seeds, kernel median 2.3e-4 vs eager 3.9e-4), so 1e-4 is this sequence's bound,
+    not an fp32 property (tools/probe_arch_drift_seeds.py)."""
     import torch.nn.functional as F
     n_sd = gd.load("nets.npz")
     sd = {k[len("architect/"):]: torch.from_numpy(n_sd[k]) for k in n_sd.files if k.startswith("architect/")}
@@ -310,8 +314,8 @@ def test_architect_update_long_sequence_drift(gpu_device, monkeypatch):
         m = ag.update_sequence(lp, v, r)
         w, dv, dl = errs(ag.network, m["architect_value_loss"])
         print("%s vs float64: max |param err| %.3g, |V(s0) err| %.3g, |loss err| %.3g" % (mode, w, dv, dl))
-        assert dv <= max(5e-4, 5 * ev), (mode, dv, ev)
-        assert dl <= max(5e-4, 5 * el) * max(1.0, l64), (mode, dl, el)
+        assert dv <= 1e-4, (mode, dv, ev)
+        assert dl <= 1e-4 * max(1.0, l64), (mode, dl, el)
         assert w <= max(0.1, 3 * ew), (mode, w, ew)
         if mode == "kernel":  # bit-for-bit deterministic
             b = agent()

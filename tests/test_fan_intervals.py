@@ -1,5 +1,5 @@
 """The lean K-tick kernel's interval fans (csrc/heist_fan_intervals.h, heist_env.hip
-`fan_lanes`), checked on CPU before any GPU run.
+`cast_ivl`), checked on CPU before any GPU run.
 
 1. The table: tools/gen_fan_intervals.py's cuts recomputed here in float64 (acos / asin of
    the 31 tie points j/k, j odd, k <= 12, plus the axes) equal the header's to within 2
@@ -74,41 +74,40 @@ def test_table_matches_float64_recomputation():
 
 
 def fan_lanes(heading, fov):
-    """The kernel's partition of one camera's rays (heist_env.hip fan_lanes, same
-    arithmetic): returns (intervals to march, near ray indices for the exact path)."""
+    """The kernel's partition of one camera's rays (heist_env.hip step_lean_kernel cast_ivl, same
+    arithmetic): returns (intervals to march, near ray indices for the exact path).  Ray i
+    sits i * s units past h0; cut j (rel units past h0, margin m) owns rays ceil((rel - m) / s)
+    .. floor((rel + m) / s) (exact path); interval j the rays after those up to the next cut's."""
     n = max(int(fov * 2), 30)  # security.py:67
     hmh = heading - fov / 2.0
     hw = hmh + 360.0 if hmh < 0.0 else hmh
     h0 = int(min(hw * UPD, 4294967295.0))
     s = (fov / float(n)) * UPD
     inv_s = 1.0 / s
-    tn = float(n) * s
     deg = (h0 * 360) >> 32
-    jb = (IDX[deg] - 1) % 252
+    jb = IDX[deg] - 1  # -1: cut 251 of the turn before
+    e64 = h0 + int(float(n) * s) + MA + 4  # past the last ray and its margin
+    je = IDX[((e64 % U) * 360 >> 32) + 1] + 252 * (e64 >> 32)
     march, near = [], []
-    for c in range(4):
-        last_valid = False
-        for lane in range(64):
-            j = (jb + 64 * c + lane) % 252
-            cut, cutn = CUT[j], CUT[(j + 1) % 252]
-            rel = ((cut - h0 + 2 ** 31) % U) - 2 ** 31
-            reln = ((cutn - h0 + 2 ** 31) % U) - 2 ** 31
-            mj = MA if cut % (U // 4) == 0 else MT
-            mn = MA if cutn % (U // 4) == 0 else MT
-            lo = float(rel) + float(mj)
-            ic = 0 if lo < 0.0 else min(int(math.floor(lo * inv_s)) + 1, n + 1)
-            if ic >= 1 and float(ic - 1) * s > lo:
-                ic -= 1
-            if ic <= n and float(ic) * s <= lo:
-                ic += 1
-            valid = float(rel) - float(mj) <= tn
-            if valid and ic <= n and float(ic) * s < float(reln) - float(mn):
-                march.append(j)
-            if valid and ic >= 1 and float(ic - 1) * s >= float(rel) - float(mj):
-                near.append(ic - 1)
-            last_valid = valid
-        if not last_valid:
-            break
+    for ju in range(jb, je):  # the camera's (camera, cut) pairs, packed over the lanes
+        j = ju % 252
+        cut, cutn = CUT[j], CUT[(j + 1) % 252]
+        rel = float(((cut - h0 + 2 ** 31) % U) - 2 ** 31)
+        reln = float(((cutn - h0 + 2 ** 31) % U) - 2 ** 31)
+        mj = float(MA if cut % (U // 4) == 0 else MT)
+        mn = float(MA if cutn % (U // 4) == 0 else MT)
+        A = math.floor((rel + mj) * inv_s) + 1
+        B = math.ceil((rel - mj) * inv_s)
+        Bn = math.ceil((reln - mn) * inv_s)
+        a0 = max(A, 0)
+        if a0 <= n and a0 < Bn:
+            march.append(j)
+        if B < A and 0 <= B <= n:
+            near.append(B)
+    # the pairs past je hold nothing: the next cut's margin starts past the last ray
+    j = je % 252
+    rel = float(((CUT[j] - h0 + 2 ** 31) % U) - 2 ** 31)
+    assert math.ceil((rel - float(MA if CUT[j] % (U // 4) == 0 else MT)) * inv_s) > n
     return march, near
 
 

@@ -2614,16 +2614,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       L.icam[lane] = make_uint4(h0v, (uint32_t)jb, (uint32_t)cam_n | (cam_rc << 16), 0u);
       L.icim[lane] = isu;
     }
-    // exclusive prefix of the pair counts over the camera lanes (bit slices: cnt < 1024)
-    int excl = 0, total = 0;
-#pragma unroll
-    for (int b = 0; b < 10; ++b) {
-      const unsigned long long mb = __ballot((cnt >> b) & 1);
-      excl += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mb, 0u)) << b;
-      total += __popcll(mb) << b;
-    }
-    const int endv = excl + cnt;  // camera lanes: one past the camera's last pair
-    total = __builtin_amdgcn_readfirstlane(total);
+    // the pair counts' running sums are scalar: a few cameras, summed where they are needed
+    int total = 0;
+    for (int m = 0; m < s.n_cams; ++m) total += __builtin_amdgcn_readlane(cnt, m);
     int qn = 0;  // marching queue L.ivq: entries j | camera << 8
     auto march_queue = [&](int n_q) {
       if (lane < n_q) {
@@ -2637,9 +2630,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     };
     for (int q0 = 0; q0 < total; q0 += 64) {
       const int q = q0 + lane;
-      int c = 0, start = 0;  // the camera of pair q: those before it end at or below q
+      int c = 0, start = 0, em = 0;  // the camera of pair q: those before it end at or below q
       for (int m = 0; m + 1 < s.n_cams; ++m) {
-        const int em = __builtin_amdgcn_readlane(endv, m);
+        em += __builtin_amdgcn_readlane(cnt, m);
         if (q >= em) {
           c = m + 1;
           start = em;

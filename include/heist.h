@@ -326,6 +326,28 @@ int heist_solver_head(const float* feat, const float* h_in, const float* c_in, i
                       int num_actions, uint64_t seed, uint64_t counter, float* logits_out, float* value_out,
                       int64_t* action_out, float* logp_out, float* h_out, float* c_out, heist_stream_t stream);
 
+/* The Solver backbone's fp32 training step (agents/solver.py:157-199 over networks.py:93-100:
+ * relu(conv1) -> relu(conv2) -> relu(conv3) -> AdaptiveAvgPool2d(4, 4), forward and backward)
+ * with the convolutions run without bias (MIOpen) and everything between them fused into one
+ * pass per layer.  Tensors are NHWC (channels_last) fp32, 16-byte aligned; n samples of rows x
+ * cols positions.
+ *   heist_bias_relu_nhwc: x[p][c] = relu(x[p][c] + bias[c]) in place (F.relu(conv + b)).
+ *   heist_bias_relu_pool_nhwc: the same for conv3 (64 channels) plus feat_out [n][64 * 16] =
+ *     adaptive_avg_pool2d(., (4, 4)) flattened C-major (the view fc_spatial reads).
+ *   heist_pool_relu_bwd_nhwc: the backward of the two: d_out = (y > 0) * (the pool's input
+ *     gradient of dfeat [n][1024]) (conv3's grad_output), dbias_out [64] = its sum over
+ *     samples and positions; partial: [n][64] floats of scratch.
+ *   heist_relu_bwd_nhwc: g = (y > 0) ? g : 0 in place (threshold_backward on the saved output)
+ *     and dbias_out [channels] its sum; partial [n][channels] scratch; 32 or 64 channels.
+ * Sums run in a fixed order (deterministic; fp32 rounding differs from torch's order). */
+int heist_bias_relu_nhwc(float* x, const float* bias, int64_t n_pos, int channels, heist_stream_t stream);
+int heist_bias_relu_pool_nhwc(float* x, const float* bias, int n, int rows, int cols, int channels, float* feat_out,
+                              heist_stream_t stream);
+int heist_pool_relu_bwd_nhwc(const float* dfeat, const float* y, int n, int rows, int cols, int channels, float* d_out,
+                             float* partial, float* dbias_out, heist_stream_t stream);
+int heist_relu_bwd_nhwc(float* g, const float* y, int n, int positions, int channels, float* partial, float* dbias_out,
+                        heist_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -57,6 +57,11 @@ hipError_t launch_solver_head_pack(const float* const* w, int A, void* packed, h
 hipError_t launch_solver_head(const float* feat, const float* h_in, const float* c_in, int n, const void* packed,
                               int A, uint64_t seed, uint64_t counter, float* logits_out, float* value_out,
                               int64_t* action_out, float* logp_out, float* h_out, float* c_out, hipStream_t st);
+hipError_t launch_bias_relu(float* x, const float* b, int64_t n_pos, int C, hipStream_t st);
+hipError_t launch_bias_relu_pool(float* x, const float* b, int n, int R, int W, int C, float* feat, hipStream_t st);
+hipError_t launch_pool_relu_bwd(const float* dfeat, const float* y, int n, int R, int W, int C, float* d, float* part,
+                                float* db, hipStream_t st);
+hipError_t launch_relu_bwd(float* g, const float* y, int n, int P, int C, float* part, float* db, hipStream_t st);
 bool arch_update_supported(int R, int C);
 void set_arch_stamps(unsigned long long* p);
 int64_t arch_update_workspace_bytes();
@@ -731,6 +736,45 @@ int heist_solver_head(const float* feat, const float* h_in, const float* c_in, i
   return check_hip(heist::launch_solver_head(feat, h_in, c_in, n, packed, num_actions, seed, counter, logits_out,
                                              value_out, action_out, logp_out, h_out, c_out, (hipStream_t)stream),
                    "heist_solver_head");
+}
+
+int heist_bias_relu_nhwc(float* x, const float* bias, int64_t n_pos, int channels, heist_stream_t stream) {
+  HEIST_REQUIRE(x && bias, "heist_bias_relu_nhwc: null pointer");
+  HEIST_REQUIRE(n_pos >= 0 && channels > 0 && channels % 4 == 0, "heist_bias_relu_nhwc: need n_pos >= 0, channels % 4 == 0");
+  HEIST_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)bias & 15) == 0, "heist_bias_relu_nhwc: 16-byte alignment");
+  if (n_pos == 0) return 0;
+  return check_hip(heist::launch_bias_relu(x, bias, n_pos, channels, (hipStream_t)stream), "heist_bias_relu_nhwc");
+}
+
+int heist_bias_relu_pool_nhwc(float* x, const float* bias, int n, int rows, int cols, int channels, float* feat_out,
+                              heist_stream_t stream) {
+  HEIST_REQUIRE(x && bias && feat_out, "heist_bias_relu_pool_nhwc: null pointer");
+  HEIST_REQUIRE(n >= 0 && rows >= 4 && cols >= 4 && channels == 64, "heist_bias_relu_pool_nhwc: need rows, cols >= 4, 64 channels");
+  HEIST_REQUIRE(((uintptr_t)x & 15) == 0 && ((uintptr_t)bias & 15) == 0, "heist_bias_relu_pool_nhwc: 16-byte alignment");
+  if (n == 0) return 0;
+  return check_hip(heist::launch_bias_relu_pool(x, bias, n, rows, cols, channels, feat_out, (hipStream_t)stream),
+                   "heist_bias_relu_pool_nhwc");
+}
+
+int heist_pool_relu_bwd_nhwc(const float* dfeat, const float* y, int n, int rows, int cols, int channels, float* d_out,
+                             float* partial, float* dbias_out, heist_stream_t stream) {
+  HEIST_REQUIRE(dfeat && y && d_out && partial && dbias_out, "heist_pool_relu_bwd_nhwc: null pointer");
+  HEIST_REQUIRE(n >= 1 && rows >= 4 && cols >= 4 && channels == 64, "heist_pool_relu_bwd_nhwc: need n >= 1, rows, cols >= 4, 64 channels");
+  HEIST_REQUIRE(((uintptr_t)y & 15) == 0 && ((uintptr_t)d_out & 15) == 0 && ((uintptr_t)partial & 15) == 0,
+                "heist_pool_relu_bwd_nhwc: 16-byte alignment");
+  return check_hip(heist::launch_pool_relu_bwd(dfeat, y, n, rows, cols, channels, d_out, partial, dbias_out,
+                                               (hipStream_t)stream),
+                   "heist_pool_relu_bwd_nhwc");
+}
+
+int heist_relu_bwd_nhwc(float* g, const float* y, int n, int positions, int channels, float* partial, float* dbias_out,
+                        heist_stream_t stream) {
+  HEIST_REQUIRE(g && y && partial && dbias_out, "heist_relu_bwd_nhwc: null pointer");
+  HEIST_REQUIRE(n >= 1 && positions >= 1 && (channels == 32 || channels == 64), "heist_relu_bwd_nhwc: need n >= 1, 32 or 64 channels");
+  HEIST_REQUIRE(((uintptr_t)g & 15) == 0 && ((uintptr_t)y & 15) == 0 && ((uintptr_t)partial & 15) == 0,
+                "heist_relu_bwd_nhwc: 16-byte alignment");
+  return check_hip(heist::launch_relu_bwd(g, y, n, positions, channels, partial, dbias_out, (hipStream_t)stream),
+                   "heist_relu_bwd_nhwc");
 }
 
 int heist_solver_stamps(uint64_t* buf) {

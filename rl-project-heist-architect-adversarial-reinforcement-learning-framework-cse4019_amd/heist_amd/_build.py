@@ -17,7 +17,8 @@ INCLUDE = os.path.join(REPO_ROOT, "include")
 LIB_PATH = os.environ.get("HEIST_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libheist_hip.so")
 BUILD_DIR = os.path.join(PKG_ROOT, "build")
 ARCH = os.environ.get("HEIST_OFFLOAD_ARCH", "gfx950")
-SOURCES = ["heist_env.hip", "heist_arch.hip", "heist_arch_update.hip", "heist_ppo.hip", "heist_policy.hip", "heist_capi.hip"]
+SOURCES = ["heist_env.hip", "heist_arch.hip", "heist_arch_update.hip", "heist_ppo.hip", "heist_policy.hip", "heist_train.hip",
+           "heist_capi.hip"]
 HEADERS = ["heist_device.h", "heist_trig.h", "heist_sincos_table.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # heist_env.hip: no SLP vectorization -- ROCm 7.2 clang miscompiles the packed-fp32

@@ -54,6 +54,10 @@ SIGNATURES = {
                                         _vp, _i, _vp, _d, _d, _d, _d, _d, _vp, _vp, _vp]),
     "heist_arch_update_timed_out": (_i, [_vp, ctypes.POINTER(_i), _vp]),
     "heist_arch_update_status": (_i, [_vp, ctypes.POINTER(_i), _vp]),
+    "heist_bias_relu_nhwc": (_i, [_vp, _vp, _i64, _i, _vp]),
+    "heist_bias_relu_pool_nhwc": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
+    "heist_pool_relu_bwd_nhwc": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    "heist_relu_bwd_nhwc": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
     "heist_arch_update_stamps": (_i, [_vp]),
     "heist_gae": (_i, [_vp, _vp, _vp, _vp, _i, _i, _d, _d, _vp, _vp, _vp]),
     "heist_adv_moments": (_i, [_vp, _i64, _i, _vp, _vp]),
@@ -109,6 +113,15 @@ def ptr(t):
         raise HeistError("expected a device tensor, got %s" % t.device)
     if not t.is_contiguous():
         raise HeistError("expected a contiguous tensor")
+    return _vp(t.data_ptr())
+
+
+def ptr_nhwc(t):
+    """Device address of a 4-D tensor laid out channels-last (NHWC), dense."""
+    if not t.is_cuda:
+        raise HeistError("expected a device tensor, got %s" % t.device)
+    if t.dim() != 4 or not t.is_contiguous(memory_format=torch.channels_last):
+        raise HeistError("expected a dense channels-last [N, C, H, W] tensor")
     return _vp(t.data_ptr())
 
 

@@ -16,6 +16,72 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 
+def _conv_nobias(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """3x3 / stride 1 / pad 1 convolution without its bias (MIOpen), channels-last out."""
+    y = torch.ops.aten.convolution(x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1)
+    return y.contiguous(memory_format=torch.channels_last)
+
+
+def _conv_bwd(g: torch.Tensor, x: torch.Tensor, w: torch.Tensor, need_input: bool):
+    gi, gw, _ = torch.ops.aten.convolution_backward(g, x, w, None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                                                    [need_input, True, False])
+    return gi, gw
+
+
+class _BackboneF32(torch.autograd.Function):
+    """SolverNetwork's conv stack (networks.py:93-100: relu(conv1) -> relu(conv2) ->
+    relu(conv3) -> AdaptiveAvgPool2d(4, 4), flattened) in fp32 with the tail of every layer
+    fused into one pass (csrc/heist_train.hip): the convolutions run on MIOpen WITHOUT their
+    bias, then one kernel adds the bias and applies ReLU in place (conv3's also pools); the
+    backward applies ReLU's mask (and, for conv3, the pool's gradient) in one pass that also
+    forms the bias gradient, and calls MIOpen's data / weight gradients.  Same arithmetic as
+    the unfused torch ops up to the order of the pool and bias-gradient sums.  Returns the
+    pooled features [B, C * 16]."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, w3, b3):
+        from . import _native as nat
+        L, st = nat.lib(), nat.stream(x.device)
+        n, _, R, C = x.shape
+        x = x.contiguous(memory_format=torch.channels_last)
+        a1 = _conv_nobias(x, w1)
+        nat.check(L.heist_bias_relu_nhwc(nat.ptr_nhwc(a1), nat.ptr(b1), n * R * C, a1.shape[1], st), "heist_bias_relu_nhwc")
+        a2 = _conv_nobias(a1, w2)
+        nat.check(L.heist_bias_relu_nhwc(nat.ptr_nhwc(a2), nat.ptr(b2), n * R * C, a2.shape[1], st), "heist_bias_relu_nhwc")
+        a3 = _conv_nobias(a2, w3)
+        feat = torch.empty(n, a3.shape[1] * 16, dtype=torch.float32, device=x.device)
+        nat.check(L.heist_bias_relu_pool_nhwc(nat.ptr_nhwc(a3), nat.ptr(b3), n, R, C, a3.shape[1], nat.ptr(feat), st),
+                  "heist_bias_relu_pool_nhwc")
+        ctx.save_for_backward(x, w1, w2, w3, a1, a2, a3)
+        return feat
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        from . import _native as nat
+        L = nat.lib()
+        x, w1, w2, w3, a1, a2, a3 = ctx.saved_tensors
+        st = nat.stream(x.device)
+        n, _, R, C = x.shape
+        dfeat = dfeat.contiguous()
+        part = torch.empty(n, 64, dtype=torch.float32, device=x.device)
+        db3 = torch.empty(a3.shape[1], dtype=torch.float32, device=x.device)
+        d3 = torch.empty_like(a3, memory_format=torch.channels_last)
+        nat.check(L.heist_pool_relu_bwd_nhwc(nat.ptr(dfeat), nat.ptr_nhwc(a3), n, R, C, a3.shape[1], nat.ptr_nhwc(d3),
+                                             nat.ptr(part), nat.ptr(db3), st), "heist_pool_relu_bwd_nhwc")
+        g2, dw3 = _conv_bwd(d3, a2, w3, True)
+        g2 = g2.contiguous(memory_format=torch.channels_last)
+        db2 = torch.empty(a2.shape[1], dtype=torch.float32, device=x.device)
+        nat.check(L.heist_relu_bwd_nhwc(nat.ptr_nhwc(g2), nat.ptr_nhwc(a2), n, R * C, a2.shape[1], nat.ptr(part), nat.ptr(db2), st),
+                  "heist_relu_bwd_nhwc")
+        g1, dw2 = _conv_bwd(g2, a1, w2, True)
+        g1 = g1.contiguous(memory_format=torch.channels_last)
+        db1 = torch.empty(a1.shape[1], dtype=torch.float32, device=x.device)
+        nat.check(L.heist_relu_bwd_nhwc(nat.ptr_nhwc(g1), nat.ptr_nhwc(a1), n, R * C, a1.shape[1], nat.ptr(part), nat.ptr(db1), st),
+                  "heist_relu_bwd_nhwc")
+        _, dw1 = _conv_bwd(g1, x, w1, False)
+        return None, dw1, db1, dw2, db2, dw3, db3
+
+
 class SolverNetwork(nn.Module):  # networks.py:13-131
     def __init__(self, grid_rows: int = 20, grid_cols: int = 20, num_actions: int = 5, hidden_dim: int = 256,
                  lstm_hidden: int = 128):
@@ -46,7 +112,25 @@ class SolverNetwork(nn.Module):  # networks.py:13-131
         z = torch.zeros(1, batch_size, self.lstm_hidden, device=device)
         return z, z.clone()
 
+    #: fp32 on a HIP device: the conv stack's bias / ReLU / pool (and their backward) fused
+    #: around MIOpen's bias-free convolutions (_BackboneF32); HEIST_FUSED_TRAIN=0 or False here
+    #: runs the plain torch ops
+    fused_tail = True
+
+    def _fused_tail_ok(self, state: torch.Tensor) -> bool:
+        import os
+        return (self.fused_tail and os.environ.get("HEIST_FUSED_TRAIN", "1") != "0" and state.is_cuda
+                and state.dtype == torch.float32 and state.dim() == 4 and state.shape[1] == 3
+                and state.shape[2] >= 4 and state.shape[3] >= 4 and state.shape[0] > 0
+                and self.conv1.weight.dtype == torch.float32
+                and not torch.is_autocast_enabled("cuda") and self.conv3.out_channels == 64
+                and tuple(self.pool.output_size) == (4, 4))
+
     def features(self, state: torch.Tensor) -> torch.Tensor:
+        if self._fused_tail_ok(state):
+            x = _BackboneF32.apply(state, self.conv1.weight, self.conv1.bias, self.conv2.weight, self.conv2.bias,
+                                   self.conv3.weight, self.conv3.bias)
+            return F.relu(self.fc_spatial(x))
         x = F.relu(self.conv1(state))
         x = F.relu(self.conv2(x))
         x = F.relu(self.conv3(x))

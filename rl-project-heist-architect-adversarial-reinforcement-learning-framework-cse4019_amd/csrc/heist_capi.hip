@@ -254,6 +254,8 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   p.dispatch_order = 1;
   if (const char* m = getenv("HEIST_DISPATCH_ORDER")) p.dispatch_order = atoi(m) >= 2 ? 2 : (atoi(m) ? 1 : 0);
   p.n_cu = n_cu;
+  p.prio_mode = 0;
+  if (const char* m = getenv("HEIST_PRIO_MODE")) p.prio_mode = atoi(m) < 0 ? 0 : (atoi(m) > 3 ? 3 : atoi(m));
   p.split_obs = 1;
   if (const char* m = getenv("HEIST_SPLIT_OBS")) p.split_obs = atoi(m) ? 1 : 0;
   for (int k = 0; k < 8; ++k) p.tile_lut[k] = k <= 5 ? (float)k / 5.0f : 0.0f;  // environment.py:319

@@ -147,6 +147,7 @@ struct EnvParams {
   int dispatch_order;          // 1: step/reset block b runs env order[b] (heaviest first); 2 (default): the
                                // same ranks snake-drafted over the SIMDs (order_kernel); 0: env b (HEIST_DISPATCH_ORDER)
   int n_cu;                    // compute units of the device (the snake draft's SIMD count / 4)
+  int prio_mode;               // K-tick lean kernel wave priority by cost rank (order_kernel; HEIST_PRIO_MODE)
   unsigned long long* stamps;          // optional [n_envs][waves][8]: step-kernel phase stamps (s_memtime), else null
   int obs_store;              // observation stores: 0 plain, 1 write-through (sc1), 2 nt, 3 sc1 nt (HEIST_OBS_STORE)
   int ray_mode;               // 0: fp32 fast path with exact fp64 re-cast of near-tie rays; 1: exact fp64 only

@@ -48,6 +48,12 @@ __device__ __forceinline__ double py_mod360(double x) {
 
 __host__ __device__ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
+// order[b] = env | wave priority << 24 (order_kernel); the env a step / reset block runs
+constexpr int32_t kOrderEnvMask = 0xFFFFFF;
+__device__ __forceinline__ int block_env(const EnvParams& p) {
+  return p.dispatch_order ? (p.order[blockIdx.x] & kOrderEnvMask) : (int)blockIdx.x;
+}
+
 // ---------------------------------------------------------------------------
 // LDS carve-up for one env
 // ---------------------------------------------------------------------------
@@ -1266,7 +1272,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
                                                        int8_t* __restrict__ status_out, int auto_reset) {
   constexpr int NT = 64 * W;
   extern __shared__ __align__(16) unsigned char smem[];
-  const int e = p.dispatch_order ? p.order[blockIdx.x] : (int)blockIdx.x;
+  const int e = block_env(p);
   const int t = threadIdx.x;
   const int probe = PROBE ? p.probe_mode : 0;
   if (probe == 6) return;  // profiling: launch + dispatch floor
@@ -2131,7 +2137,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
     EnvParams p, int K, const int64_t* __restrict__ actions, float* __restrict__ obs, float* __restrict__ rew,
     double* __restrict__ rew64, uint8_t* __restrict__ done_out, int8_t* __restrict__ status_out, int auto_reset) {
   extern __shared__ __align__(16) unsigned char smem[];
-  const int e = p.dispatch_order ? p.order[blockIdx.x] : (int)blockIdx.x;
+  const int e = block_env(p);
   step_multi_body<W, U, O, D, STAMP, PROBE>(p, K, actions, obs, rew, rew64, done_out, status_out, auto_reset, smem, e);
 }
 
@@ -2307,7 +2313,8 @@ __host__ __device__ inline size_t lean_carve(unsigned char* smem, int R, int C, 
   return o;
 }
 static size_t lean_lds_bytes(const EnvParams& p, int K) {
-  const size_t lean = lean_carve(nullptr, p.R, p.C, p.max_cams, p.max_guards, p.max_path, K, nullptr);
+  const size_t lean = align16(lean_carve(nullptr, p.R, p.C, p.max_cams, p.max_guards, p.max_path, K, nullptr)) +
+                      (p.stamps ? 80 : 0);  // the STAMP variant's segment sums
   const size_t generic = step_multi_lds(p, K);  // the envs that take step_multi_body
   return lean > generic ? lean : generic;
 }
@@ -2331,7 +2338,13 @@ struct LeanGuard {
   __device__ uint32_t pos0() const { return b >> 16; }
 };
 
-template <int R_, int C_>
+// STAMP (instrumentation, heist_step_stamps armed): lane 0 sums the shader clock spent in 9
+// tick segments over the launch (LEAN_SEGS in tools/probe_lean_stamps.py) in LDS after the
+// carve and writes [segment sums 0..8, lifetime, start clock, HW_ID, XCC_ID] to
+// stamps[env][0][16] (the generic K-tick body's layout); envs on the generic body record none.
+// PROBE (profiling only, HEIST_PROBE_MODE, results wrong): 21 no wait for the previous tick's
+// DMA, 22 no visibility cast, 23 no observation stores.
+template <int R_, int C_, bool STAMP = false, int PROBE = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void step_lean_kernel(
     EnvParams p, int K, const int64_t* __restrict__ actions, float* __restrict__ obs, float* __restrict__ rew,
     double* __restrict__ rew64, uint8_t* __restrict__ done_out, int8_t* __restrict__ status_out, int auto_reset) {
@@ -2345,7 +2358,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
   static_assert((R_ + 2 * kRing) * PC <= D, "the padded planes fit the 1024-byte gap");
   static_assert(C_ % 4 == 0 && R_ <= 64 && C_ <= 32 && (R_ + 2 * kRing) * PC <= 2048, "lean kernel geometry");
   extern __shared__ __align__(16) unsigned char smem[];
-  const int e = p.dispatch_order ? p.order[blockIdx.x] : (int)blockIdx.x;
+  const int e = block_env(p);
+  if (p.prio_mode && p.dispatch_order) {
+    const int pr = (int)((uint32_t)p.order[blockIdx.x] >> 24);
+    if (pr == 3) __builtin_amdgcn_s_setprio(3);
+    else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+    else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+  }
   const int lane = threadIdx.x;
   const int N = p.n_envs;
   const int mc = p.max_cams, mg = p.max_guards, n_slot = mc + mg, mp = p.max_path;
@@ -2416,7 +2435,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
 
   // ---- prologue: the env's layout and state, once per launch
   LeanLds L;
-  lean_carve(smem, R_, C_, mc, mg, mp, K, &L);
+  const size_t carved = lean_carve(smem, R_, C_, mc, mg, mp, K, &L);
+  unsigned long long* st_acc = reinterpret_cast<unsigned long long*>(smem + align16(carved));
+  unsigned long long st_last = 0, st_start = 0;
+  if (STAMP && lane == 0) {
+    st_start = st_last = __builtin_amdgcn_s_memtime();
+    for (int j = 0; j < 9; ++j) st_acc[j] = 0;
+  }
+#define LEAN_STAMP(seg)                                        \
+  do {                                                         \
+    if (STAMP && lane == 0) {                                  \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+      st_acc[(seg)] += now_ - st_last;                         \
+      st_last = now_;                                          \
+    }                                                          \
+  } while (0)
   uint8_t* const wall = smem;          // [0, D): the padded stop map
   uint8_t* const vis = smem + D;       // [D, 2D): the visibility plane; [2D, 3D): the sink
   const uint32_t base = (uint32_t)(uintptr_t)smem;  // LDS address of the stop map
@@ -2546,10 +2579,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
 #pragma unroll
     for (int z = 0; z < D / 1024; ++z)  // 64 x 16 B per pass: the plane
       reinterpret_cast<uint4*>(vis)[lane + 64 * z] = make_uint4(0u, 0u, 0u, 0u);
+    const FanTick* f = fan0 + k;
+    uint4 o4a = make_uint4(0u, 0u, 0u, 0u), o4b = o4a;
+    uint2 o2a = make_uint2(0u, 0u), o2b = o2a;
     if (s.n_cams > 0) {
-      const FanTick* f = fan0 + k;
-      uint4 o4a = make_uint4(0u, 0u, 0u, 0u), o4b = o4a;
-      uint2 o2a = make_uint2(0u, 0u), o2b = o2a;
       const bool want_b = n_uniq > 64;
       if (staged) {
         o4a = L.stg->off4[lane];
@@ -2571,6 +2604,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
         asm volatile("" ::"v"(__builtin_bit_cast(u32x4_t, o4a)), "v"(__builtin_bit_cast(u32x2_t, o2a)),
                      "v"(__builtin_bit_cast(u32x4_t, o4b)), "v"(__builtin_bit_cast(u32x2_t, o2b)));
       }
+    }
+    // the tick's fan entry is in registers, the staging free: tick k + 1's entry goes out now,
+    // a whole cast ahead of the next tick's wait for it (once the staging reads have returned)
+    if (staged && k + 1 < K) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::"v"(__builtin_bit_cast(u32x4_t, o4a)), "v"(__builtin_bit_cast(u32x2_t, o2a)),
+                   "v"(__builtin_bit_cast(u32x4_t, o4b)), "v"(__builtin_bit_cast(u32x2_t, o2b))
+                   : "memory");
+      dma_fan(k + 1, n_uniq > 64);
+    }
+    if (s.n_cams > 0) {
       for (int m = 0; m < s.n_cams; ++m) {
         const uint32_t rcm = (uint32_t)__builtin_amdgcn_readlane((int)cam_rc, m);
         const uint32_t corner = base + (rcm & 0xffu) * PC + (rcm >> 8);
@@ -2581,6 +2624,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       }
       if (n_tie > 0) lean_tie_rays<D, PC>(smem, f, n_tie, cam_rc, s.n_cams, p.half_deg);
     }
+    LEAN_STAMP(2);
     stamp_cones(par);
   };
   // this tick's visibility from the interval table (an env the shared fan does not serve).
@@ -2605,18 +2649,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     const double hmh = heading - fovd / 2.0;  // security.py:64, :70
     const double hu = (hmh < 0.0 ? hmh + 360.0 : hmh) * kFanUnitsPerDeg;
     const uint32_t h0v = hu >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)hu;
-    int cnt = 0;
+    int cnt = 0, jb = 0;
     if (live_cam) {
-      const int jb = (int)L.ivl->idx[__umulhi(h0v, 360u)] - 1;  // -1: cut 251 of the turn before
+      jb = (int)L.ivl->idx[__umulhi(h0v, 360u)] - 1;  // -1: cut 251 of the turn before
       const uint64_t e64 = (uint64_t)h0v + (uint64_t)((double)cam_n * su) + (uint64_t)(kFanMarginAxis + 4);
       const int je = (int)L.ivl->idx[__umulhi((uint32_t)e64, 360u) + 1u] + kFanCuts * (int)(e64 >> 32);
       cnt = je - jb;
       L.icam[lane] = make_uint4(h0v, (uint32_t)jb, (uint32_t)cam_n | (cam_rc << 16), 0u);
       L.icim[lane] = isu;
     }
-    // the pair counts' running sums are scalar: a few cameras, summed where they are needed
-    int total = 0;
-    for (int m = 0; m < s.n_cams; ++m) total += __builtin_amdgcn_readlane(cnt, m);
+    // the pair counts' running sums are scalar: a few cameras, summed where they are needed;
+    // camera lane m keeps jo = jb - (pairs of cameras 0 .. m-1), so pair q of camera m has cut
+    // jo + q, known before any LDS read (the chunk's loads then go out together)
+    int total = 0, jo_l = 0;
+    for (int m = 0; m < s.n_cams; ++m) {
+      if (lane == m) jo_l = jb - total;
+      total += __builtin_amdgcn_readlane(cnt, m);
+    }
     int qn = 0;  // marching queue L.ivq: entries j | camera << 8
     auto march_queue = [&](int n_q) {
       if (lane < n_q) {
@@ -2630,19 +2679,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     };
     for (int q0 = 0; q0 < total; q0 += 64) {
       const int q = q0 + lane;
-      int c = 0, start = 0, em = 0;  // the camera of pair q: those before it end at or below q
+      // the camera of pair q (those before it end at or below q) and its cut
+      int c = 0, jo = __builtin_amdgcn_readlane(jo_l, 0), em = 0;
       for (int m = 0; m + 1 < s.n_cams; ++m) {
         em += __builtin_amdgcn_readlane(cnt, m);
+        const int jo_m = __builtin_amdgcn_readlane(jo_l, m + 1);
         if (q >= em) {
           c = m + 1;
-          start = em;
+          jo = jo_m;
         }
       }
+      int j = jo + q;
+      j = j < 0 ? j + kFanCuts : (j >= kFanCuts ? j - kFanCuts : j);
       const uint4 cu = L.icam[c];
       const double im = L.icim[c];
       const int n = (int)(cu.z & 0xffffu);
-      int j = (int)cu.y + (q - start);
-      j = j < 0 ? j + kFanCuts : (j >= kFanCuts ? j - kFanCuts : j);
       const int jn = j + 1 == kFanCuts ? 0 : j + 1;
       const uint32_t cut = L.ivl->cut[j], cutn = L.ivl->cut[jn];
       const double rel = (double)(int)(cut - cu.x), reln = (double)(int)(cutn - cu.x);
@@ -2673,6 +2724,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       }
     }
     if (qn > 0) march_queue(qn);
+    LEAN_STAMP(2);
     stamp_cones(par);
   };
   auto cast = [&](int k, int n_uniq, int n_tie, int par, bool staged, bool staged_wide) {
@@ -2689,9 +2741,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     const int par = k & 1;
     if ((k & 63) == 0) vact = k + lane < K ? L.act[k + lane] : 0u;
     // the DMA issued a tick ago (older than the previous tick's kLeanStores stores) has landed
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLeanStores) : "memory");
+    if (PROBE == 21) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLeanStores) : "memory");
     const int n_uniq = ivl ? 0 : __builtin_amdgcn_readfirstlane(L.stg->hdr[2]);
     const int n_tie = ivl ? 0 : __builtin_amdgcn_readfirstlane(L.stg->hdr[3]);
+    LEAN_STAMP(0);  // 0: the tick's DMA wait, the fan header
     const bool staged_wide = wide;
     const bool frozen = s.done != 0;  // finished, no auto-reset: environment.py:232-233
     double reward = 0.0;
@@ -2723,11 +2777,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       // the slot after the guard's next move: row 15 of this tick's entry (staged a tick ago)
       if (cached) gd.nslot = L.cone[par * 16 * mg + 8 * mg + 8 * g + 7];
       if (k + 1 < K) dma_next_cone(par ^ 1);  // tick k + 1's entry if the env still acts then
+      LEAN_STAMP(1);  // 1: move, rotation, patrol
       // 3. visibility (environment.py:257-258)
-      cast(k, n_uniq, n_tie, par, true, staged_wide);
+      if (PROBE != 22) cast(k, n_uniq, n_tie, par, true, staged_wide);
+      LEAN_STAMP(3);  // 3: the cached guard cones (2: the cameras, inside cast)
     }
-    // the staging is free: tick k + 1's fan entry (a frozen env keeps its plane and skips it)
-    if (k + 1 < K && !frozen && !ivl) dma_fan(k + 1, n_uniq > 64);
+    // (tick k + 1's fan entry went out inside cast_fan; a frozen env keeps its plane and skips it)
     wide = n_uniq > 64;
     // the plane's channel-1 quads (also the detection test's byte)
     uint32_t v1[Q];
@@ -2737,6 +2792,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       v1[j] = *reinterpret_cast<const uint32_t*>(vis + OFF0 + r * PC + 4 * (qc - r * C4));
     }
     int done_now = s.done;
+    LEAN_STAMP(4);  // 4: next fan DMA, the channel-1 quads
     if (!frozen) {
       // 4. detection, vault, timeout (environment.py:271-297), in the reference's order
       const int sol = s.pos_r * C_ + s.pos_c, qs = sol >> 2;
@@ -2766,6 +2822,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       }
       done_now = s.done;
     }
+    LEAN_STAMP(5);  // 5: detection, vault, timeout
     if (auto_reset && done_now) {
       // 5. auto-reset (environment.py:183-214): headings kept, guards back to patrol point 0;
       // this row's observation is the next attempt's first one
@@ -2794,6 +2851,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       }
       if (k + 1 < K) dma_next_cone(par ^ 1);  // tick k + 1's entry from the reset pose
     }
+    LEAN_STAMP(6);  // 6: auto-reset
     // 6. tick k's stores (kLeanStores, unconditional; lanes with nothing to store pass an
     // offset past their buffer descriptor, which the hardware drops): observation channels
     // 0, 1, 2, the solver's quad of channel 2 again (same lane, program order: it lands
@@ -2810,6 +2868,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       const int qc = in ? q : N4 - 1;
       const uint32_t b = *reinterpret_cast<const uint32_t*>(L.grid + 4 * qc);
       // float32(tile) / 5 == float32(tile) * 0.2f for every tile type (environment.py:319)
+      if (PROBE == 23) continue;
       obs_put(rs, 2, in ? 16 * q : (int)kOOB,
               make_float4((float)(b & 0xff) * 0.2f, (float)((b >> 8) & 0xff) * 0.2f,
                           (float)((b >> 16) & 0xff) * 0.2f, (float)(b >> 24) * 0.2f));
@@ -2841,8 +2900,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)(int8_t)status,
                                          __builtin_amdgcn_make_buffer_rsrc(status_out + ko, (short)0, 1, 0x00020000),
                                          l0, 0, 0);
+    LEAN_STAMP(7);  // 7: the tick's stores
   }
   // epilogue: the state the next launch (or heist_export) starts from
+  if (STAMP && lane == 0) {
+    unsigned long long* q = p.stamps + (size_t)e * p.multi_waves * 16;
+    for (int j = 0; j < 9; ++j) q[j] = st_acc[j];
+    q[9] = __builtin_amdgcn_s_memtime() - st_start;
+    q[10] = st_start;
+    q[11] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+    q[12] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+  }
+#undef LEAN_STAMP
   if (lane == 0) p.scal[e] = s;
   if (live_cam) eb.cams[(uint32_t)lane].heading = heading;
   if (live_guard) {
@@ -2862,7 +2931,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
                                                         float* __restrict__ obs) {
   constexpr int NT = 64 * W;
   extern __shared__ __align__(16) unsigned char smem[];
-  const int e = p.dispatch_order ? p.order[blockIdx.x] : (int)blockIdx.x;
+  const int e = block_env(p);
   const int t = threadIdx.x;
   if (mask && !mask[e]) return;
   const EnvLds L = carve<D>(smem, p.R, p.C, p.max_cams + p.max_guards, 0, W, p.max_guards);
@@ -3357,7 +3426,16 @@ __global__ __launch_bounds__(1024) void order_kernel(EnvParams p) {
       const int cu = sl % p.n_cu, simd = sl / p.n_cu;
       b = p.n_cu * (4 * r + simd) + cu;
     }
-    p.order[b] = e;
+    // the wave priority (s_setprio) of the env's K-tick lean launch by cost rank i: the
+    // heaviest envs get the SIMD first, the light ones fill their latency gaps
+    // (prio_mode 1: quartiles 3 / 2 / 1 / 0; 2: top 1/16 -> 3, next 1/16 -> 2, next 1/8 -> 1;
+    // 3: top 1/8 -> 1)
+    const long long f16 = 16LL * i / (p.n_envs > 0 ? p.n_envs : 1);
+    int pr = 0;
+    if (p.prio_mode == 1) pr = 3 - (int)(f16 >> 2);
+    else if (p.prio_mode == 2) pr = f16 < 1 ? 3 : (f16 < 2 ? 2 : (f16 < 4 ? 1 : 0));
+    else if (p.prio_mode == 3) pr = f16 < 2 ? 1 : 0;
+    p.order[b] = e | (pr << 24);
   }
 }
 
@@ -3499,15 +3577,34 @@ hipError_t launch_step_multi(const EnvParams& p, int K, const int64_t* actions, 
   // whatever multi_waves says, the envs it cannot serve taking the one-wave generic body)
   const bool lean20 = p.multi_waves == 1 && p.R == 20 && p.C == 20 && p.vis_gap == 1024;
   const bool lean32 = p.R == 32 && p.C == 32 && p.vis_gap == 2048;
-  if (p.lean && (lean20 || lean32) && p.probe_mode == 0 && !p.stamps && !p.sample_counter && !p.redo_counter &&
+  if (p.lean && lean20 && p.probe_mode >= 21 && p.probe_mode <= 23 && !p.stamps &&
+      p.max_cams + p.max_guards <= kMaxEmitters) {  // profiling variants of the lean kernel
+    if (p.fan_on && p.fan_fill) hipLaunchKernelGGL(fan_kernel, dim3(kFanTicks), dim3(kFanRays), 0, st, p);
+    const size_t lds_l = lean_lds_bytes(p, K);
+#define HEIST_LEAN_PROBE(M)                                                                                       \
+  if (p.probe_mode == M)                                                                                          \
+    hipLaunchKernelGGL((step_lean_kernel<20, 20, false, M>), dim3(p.n_envs), dim3(64), lds_l, st, p, K, actions, obs, \
+                       rew, rew64, done_out, status_out, auto_reset);
+    HEIST_LEAN_PROBE(21) HEIST_LEAN_PROBE(22) HEIST_LEAN_PROBE(23)
+#undef HEIST_LEAN_PROBE
+    return hipGetLastError();
+  }
+  if (p.lean && (lean20 || lean32) && p.probe_mode == 0 && !p.sample_counter && !p.redo_counter &&
       p.max_cams + p.max_guards <= kMaxEmitters) {
     if (p.fan_on && p.fan_fill) hipLaunchKernelGGL(fan_kernel, dim3(kFanTicks), dim3(kFanRays), 0, st, p);
-    if (lean20)
-      hipLaunchKernelGGL((step_lean_kernel<20, 20>), dim3(p.n_envs), dim3(64), lean_lds_bytes(p, K), st, p, K, actions,
-                         obs, rew, rew64, done_out, status_out, auto_reset);
+    const size_t lds_l = lean_lds_bytes(p, K);
+    if (lean20 && p.stamps)
+      hipLaunchKernelGGL((step_lean_kernel<20, 20, true>), dim3(p.n_envs), dim3(64), lds_l, st, p, K, actions, obs, rew,
+                         rew64, done_out, status_out, auto_reset);
+    else if (lean20)
+      hipLaunchKernelGGL((step_lean_kernel<20, 20>), dim3(p.n_envs), dim3(64), lds_l, st, p, K, actions, obs, rew, rew64,
+                         done_out, status_out, auto_reset);
+    else if (p.stamps)
+      hipLaunchKernelGGL((step_lean_kernel<32, 32, true>), dim3(p.n_envs), dim3(64), lds_l, st, p, K, actions, obs, rew,
+                         rew64, done_out, status_out, auto_reset);
     else
-      hipLaunchKernelGGL((step_lean_kernel<32, 32>), dim3(p.n_envs), dim3(64), lean_lds_bytes(p, K), st, p, K, actions,
-                         obs, rew, rew64, done_out, status_out, auto_reset);
+      hipLaunchKernelGGL((step_lean_kernel<32, 32>), dim3(p.n_envs), dim3(64), lds_l, st, p, K, actions, obs, rew,
+                         rew64, done_out, status_out, auto_reset);
     return hipGetLastError();
   }
 #define HEIST_MULTI_CASE(W, U, O, D)                                                                        \

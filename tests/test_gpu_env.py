@@ -288,6 +288,41 @@ def test_step_stamps_instrumentation(gpu_device):
     envs[0].step_multi(acts)
 
 
+@pytest.mark.parametrize("R", [20, 32])
+def test_step_multi_stamps_lean(gpu_device, R):
+    """heist_step_stamps on the K-tick path: the stamped step_lean_kernel instance gives the
+    same results as the plain one, and each env's per-segment cycle sums (words 0..8) add up
+    to no more than its lifetime (word 9)."""
+    from heist_amd import _native as nat
+    n, K = 512, 8
+    cfg = EnvironmentConfig(grid_rows=R, grid_cols=R)
+    lays = synthetic_layouts(n, R, R, 15, seed=5)
+    envs = [HeistEnv(n, cfg, device=gpu_device) for _ in range(2)]
+    for e in envs:
+        e.set_layouts(lays, budget=15)
+        e.reset()
+    kc = envs[0].kernel_config()
+    if not kc["lean"]:
+        pytest.skip("lean K-tick kernel disabled")
+    W = kc["multi_waves"]
+    L = nat.lib()
+    words = max(int(L.heist_stamp_words(envs[0]._h, 0)), int(L.heist_stamp_words(envs[0]._h, 1)))
+    buf = torch.zeros(words, dtype=torch.int64, device=gpu_device)
+    g = torch.Generator(device="cpu").manual_seed(9)
+    for it in range(3):
+        acts = torch.randint(0, 5, (K, n), generator=g).to(gpu_device)
+        nat.check(L.heist_step_stamps(envs[0]._h, nat.ptr(buf), buf.numel()), "heist_step_stamps")
+        r0 = envs[0].step_multi(acts, reward64=True)
+        nat.check(L.heist_step_stamps(envs[0]._h, None, 0), "heist_step_stamps")
+        r1 = envs[1].step_multi(acts, reward64=True)
+        for x, y in zip(r0, r1):
+            assert torch.equal(x, y), it
+    s = buf[:n * W * 16].reshape(n, W, 16)[:, 0].cpu().numpy()
+    assert (s[:, :9] >= 0).all() and (s[:, 9] > 0).all()
+    assert (s[:, :9].sum(axis=1) <= s[:, 9]).all()
+    assert (s[:, 2] > 0).any() and (s[:, 7] > 0).all()
+
+
 @pytest.mark.parametrize("cones", [False, True], ids=["live_guards", "guard_cones"])
 def test_sample_counter_work_figure(cones, gpu_device):
     """heist_count_samples: an unobstructed camera ray evaluates all 2*range samples, a guard

@@ -2343,7 +2343,8 @@ struct LeanGuard {
 // carve and writes [segment sums 0..8, lifetime, start clock, HW_ID, XCC_ID] to
 // stamps[env][0][16] (the generic K-tick body's layout); envs on the generic body record none.
 // PROBE (profiling only, HEIST_PROBE_MODE, results wrong): 21 no wait for the previous tick's
-// DMA, 22 no visibility cast, 23 no observation stores.
+// DMA, 22 no visibility cast, 23 no observation stores, 24 / 25 shared-fan marches without
+// their visibility stores / stop-byte loads, 26 the observation stores without their LDS reads.
 template <int R_, int C_, bool STAMP = false, int PROBE = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void step_lean_kernel(
     EnvParams p, int K, const int64_t* __restrict__ actions, float* __restrict__ obs, float* __restrict__ rew,
@@ -2561,14 +2562,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
 #pragma unroll
     for (int u = 0; u < 12; ++u) a[u] = corner + ((u & 1) ? (ow[u >> 1] >> 16) : (ow[u >> 1] & 0xffffu));
 #pragma unroll
-    for (int u = 0; u < 12; ++u) w[u] = lds_ld(a[u]);
+    for (int u = 0; u < 12; ++u) w[u] = PROBE == 25 ? 0u : lds_ld(a[u]);
     const uint32_t own0 = (ow[0] & 0xffffu) == (uint32_t)OFF0, own1 = (ow[0] >> 16) == (uint32_t)OFF0;
     uint32_t stop = 0;
 #pragma unroll
     for (int u = 0; u < 12; ++u) {
       stop = u == 0 ? w[0] : or_b32(stop, w[u]);
       const uint32_t skip = u == 0 ? or_b32(stop, own0) : (u == 1 ? or_b32(stop, own1) : stop);
-      lds_st(__umul24(skip, (uint32_t)D) + a[u] + D, 1);
+      if (PROBE != 24) lds_st(__umul24(skip, (uint32_t)D) + a[u] + D, 1);
     }
   };
   // this tick's visibility into the cleared plane: every camera marches the shared fan's
@@ -2661,28 +2662,33 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     // the pair counts' running sums are scalar: a few cameras, summed where they are needed;
     // camera lane m keeps jo = jb - (pairs of cameras 0 .. m-1), so pair q of camera m has cut
     // jo + q, known before any LDS read (the chunk's loads then go out together)
-    int total = 0, jo_l = 0;
+    // and end_l = pairs of cameras 0 .. m (a chunk looks only at the cameras it overlaps)
+    int total = 0, jo_l = 0, end_l = 0;
     for (int m = 0; m < s.n_cams; ++m) {
       if (lane == m) jo_l = jb - total;
       total += __builtin_amdgcn_readlane(cnt, m);
+      if (lane == m) end_l = total;
     }
-    int qn = 0;  // marching queue L.ivq: entries j | camera << 8
+    int qn = 0;  // marching queue L.ivq: entries j | camera tile (row | col << 8) << 8
     auto march_queue = [&](int n_q) {
       if (lane < n_q) {
         const uint32_t ent = L.ivq[lane];
-        const uint32_t rc = L.icam[ent >> 8].z >> 16, row = rc & 0xffu, col = rc >> 8;
+        const uint32_t row = (ent >> 8) & 0xffu, col = ent >> 16;
         const uint32_t own = base + (row + kRing) * PC + col + kRing;
         const float mx = __builtin_bit_cast(float, base + col + kRing), my = __builtin_bit_cast(float, row + kRing);
         const float2 d = L.ivl->dir[ent & 0xffu];
         march_fast<D, 2 * kTieMaxRange, false, false, true>(PC, own, d.x, d.y, mx, my, 2 * kTieMaxRange);
       }
     };
+    int mb = 0;  // the first camera whose pairs reach this chunk
     for (int q0 = 0; q0 < total; q0 += 64) {
       const int q = q0 + lane;
+      while (__builtin_amdgcn_readlane(end_l, mb) <= q0) ++mb;
       // the camera of pair q (those before it end at or below q) and its cut
-      int c = 0, jo = __builtin_amdgcn_readlane(jo_l, 0), em = 0;
-      for (int m = 0; m + 1 < s.n_cams; ++m) {
-        em += __builtin_amdgcn_readlane(cnt, m);
+      int c = mb, jo = __builtin_amdgcn_readlane(jo_l, mb);
+      for (int m = mb; m + 1 < s.n_cams; ++m) {
+        const int em = __builtin_amdgcn_readlane(end_l, m);
+        if (em >= q0 + 64) break;
         const int jo_m = __builtin_amdgcn_readlane(jo_l, m + 1);
         if (q >= em) {
           c = m + 1;
@@ -2713,7 +2719,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       const unsigned long long sb = __ballot(safe);
       if (safe) {
         const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(sb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sb, 0u));
-        L.ivq[pos] = (uint32_t)j | ((uint32_t)c << 8);
+        L.ivq[pos] = (uint32_t)j | ((cu.z >> 16) << 8);
       }
       qn += __popcll(sb);
       if (qn >= 64) {
@@ -2743,8 +2749,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     // the DMA issued a tick ago (older than the previous tick's kLeanStores stores) has landed
     if (PROBE == 21) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLeanStores) : "memory");
-    const int n_uniq = ivl ? 0 : __builtin_amdgcn_readfirstlane(L.stg->hdr[2]);
-    const int n_tie = ivl ? 0 : __builtin_amdgcn_readfirstlane(L.stg->hdr[3]);
+    int n_uniq = 0, n_tie = 0;
+    if (!ivl) {  // one LDS read for both header words
+      const int2 h = *reinterpret_cast<const int2*>(&L.stg->hdr[2]);
+      n_uniq = __builtin_amdgcn_readfirstlane(h.x);
+      n_tie = __builtin_amdgcn_readfirstlane(h.y);
+    }
     LEAN_STAMP(0);  // 0: the tick's DMA wait, the fan header
     const bool staged_wide = wide;
     const bool frozen = s.done != 0;  // finished, no auto-reset: environment.py:232-233
@@ -2866,7 +2876,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       const int q = lane + 64 * j;
       const bool in = q < N4;
       const int qc = in ? q : N4 - 1;
-      const uint32_t b = *reinterpret_cast<const uint32_t*>(L.grid + 4 * qc);
+      const uint32_t b = PROBE == 26 ? 0x01020304u : *reinterpret_cast<const uint32_t*>(L.grid + 4 * qc);
       // float32(tile) / 5 == float32(tile) * 0.2f for every tile type (environment.py:319)
       if (PROBE == 23) continue;
       obs_put(rs, 2, in ? 16 * q : (int)kOOB,
@@ -2875,7 +2885,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       const uint32_t v = v1[j];
       obs_put(rs, 2, in ? 16 * (N4 + q) : (int)kOOB,
               make_float4((float)(v & 0xff), (float)((v >> 8) & 0xff), (float)((v >> 16) & 0xff), (float)(v >> 24)));
-      float4 c2 = L.plane2[qc];
+      float4 c2 = PROBE == 26 ? make_float4(0.f, 0.f, 0.f, 0.f) : L.plane2[qc];
       obs_put(rs, 2, in ? 16 * (2 * N4 + q) : (int)kOOB, c2);
       if (j == (qs >> 6)) {
         // the solver's cell of channel 2 is fl32(1 + g) for its static value g (heist_create's
@@ -3577,7 +3587,7 @@ hipError_t launch_step_multi(const EnvParams& p, int K, const int64_t* actions, 
   // whatever multi_waves says, the envs it cannot serve taking the one-wave generic body)
   const bool lean20 = p.multi_waves == 1 && p.R == 20 && p.C == 20 && p.vis_gap == 1024;
   const bool lean32 = p.R == 32 && p.C == 32 && p.vis_gap == 2048;
-  if (p.lean && lean20 && p.probe_mode >= 21 && p.probe_mode <= 23 && !p.stamps &&
+  if (p.lean && lean20 && p.probe_mode >= 21 && p.probe_mode <= 26 && !p.stamps &&
       p.max_cams + p.max_guards <= kMaxEmitters) {  // profiling variants of the lean kernel
     if (p.fan_on && p.fan_fill) hipLaunchKernelGGL(fan_kernel, dim3(kFanTicks), dim3(kFanRays), 0, st, p);
     const size_t lds_l = lean_lds_bytes(p, K);
@@ -3585,7 +3595,8 @@ hipError_t launch_step_multi(const EnvParams& p, int K, const int64_t* actions, 
   if (p.probe_mode == M)                                                                                          \
     hipLaunchKernelGGL((step_lean_kernel<20, 20, false, M>), dim3(p.n_envs), dim3(64), lds_l, st, p, K, actions, obs, \
                        rew, rew64, done_out, status_out, auto_reset);
-    HEIST_LEAN_PROBE(21) HEIST_LEAN_PROBE(22) HEIST_LEAN_PROBE(23)
+    HEIST_LEAN_PROBE(21) HEIST_LEAN_PROBE(22) HEIST_LEAN_PROBE(23) HEIST_LEAN_PROBE(24) HEIST_LEAN_PROBE(25)
+    HEIST_LEAN_PROBE(26)
 #undef HEIST_LEAN_PROBE
     return hipGetLastError();
   }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Lean kernel: early fan DMA + single-round-trip pair loads: env tests, then timings.
 cd "${GRAFT_REPO_ROOT:-.}" || exit 1
-OUT=gpurun_out/${TAG:-r05q}
+OUT=gpurun_out/${TAG:-r05s}
 mkdir -p $OUT
 export TMPDIR=/tmp
 fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }

@@ -408,8 +408,8 @@ int heist_step_multi(heist_t h, int K, const int64_t* actions, float* obs_out, f
   // K single ticks advance the headings)
   EnvParams q = h->p;
   const bool kt = heist::multi_variant_exists(q.multi_waves, q.ray_chunk, q.multi_occ, q.vis_gap) && (q.C & 3) == 0 &&
-                  (q.probe_mode == 0 || (q.probe_mode >= 21 && q.probe_mode <= 26)) && !q.sample_counter &&
-                  !q.redo_counter;  // 21-26: the lean kernel's profiling variants (shared fan kept)
+                  (q.probe_mode == 0 || (q.probe_mode >= 21 && q.probe_mode <= 28)) && !q.sample_counter &&
+                  !q.redo_counter;  // 21-28: the lean kernel's profiling variants (shared fan kept)
   q.fan_fill = 0;
   q.fan_base = 0;
   int next_pos = -1;

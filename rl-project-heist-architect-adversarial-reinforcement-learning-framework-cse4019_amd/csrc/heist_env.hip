@@ -2174,7 +2174,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(O))) voi
 
 // LDS-DMA of 16 bytes per active lane (global_load_lds_dwordx4: lane i's bytes land at
 // lds_dst + 16 i), issued as inline asm so that the compiler's vmcnt bookkeeping does not
-// see it: the lean kernel waits for these with its own counted s_waitcnt (kLeanStores).  M0
+// see it: the lean kernel waits for these with its own counted s_waitcnt (kStores).  M0
 // (the LDS destination base) is set and restored inside the statement.
 __device__ __forceinline__ void lds_dma16(const void* gsrc, uint32_t lds_dst) {
   unsigned keep;
@@ -2319,11 +2319,10 @@ static size_t lean_lds_bytes(const EnvParams& p, int K) {
   return lean > generic ? lean : generic;
 }
 
-// Stores the lean tick issues, every tick, after the LDS-DMA of the next tick's data:
-// observation channels 0, 1, 2 for two quads per lane (6), the solver's quad of channel 2,
-// reward, reward64, done, status.  The next tick's `s_waitcnt vmcnt(kLeanStores)` therefore
-// retires the DMA and never waits for a store.
-constexpr int kLeanStores = 11;
+// The lean tick issues its stores every tick after the LDS-DMA of the next tick's data:
+// observation channels 0, 1, 2 for Q quads per lane (3 Q), reward, reward64, done, status.
+// The next tick's `s_waitcnt vmcnt(3 Q + 4)` (kStores) therefore retires the DMA and never
+// waits for a store.
 
 // A cached guard's per-tick state packed in two registers: patrol index | step << 8 | len
 // << 16 | heading slot << 24, and position | position 0 << 16 (row | col << 8 each); the slot
@@ -2344,7 +2343,8 @@ struct LeanGuard {
 // stamps[env][0][16] (the generic K-tick body's layout); envs on the generic body record none.
 // PROBE (profiling only, HEIST_PROBE_MODE, results wrong): 21 no wait for the previous tick's
 // DMA, 22 no visibility cast, 23 no observation stores, 24 / 25 shared-fan marches without
-// their visibility stores / stop-byte loads, 26 the observation stores without their LDS reads.
+// their visibility stores / stop-byte loads, 26 the observation stores without their LDS reads,
+// 27 the stores alone (no move, cast, detection), 28 move + patrol + stores.
 template <int R_, int C_, bool STAMP = false, int PROBE = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void step_lean_kernel(
     EnvParams p, int K, const int64_t* __restrict__ actions, float* __restrict__ obs, float* __restrict__ rew,
@@ -2355,6 +2355,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
   constexpr int N4 = RC / 4;
   constexpr int C4 = C_ / 4;
   constexpr int Q = (N4 + 63) / 64;  // observation quads per lane (20 x 20: 2, 32 x 32: 4)
+  constexpr int kStores = 3 * Q + 4;  // a tick's stores (see 6. below)
   constexpr int OFF0 = kRing * PC + kRing;  // padded index of tile (0, 0); also a sample's offset on its own tile
   static_assert((R_ + 2 * kRing) * PC <= D, "the padded planes fit the 1024-byte gap");
   static_assert(C_ % 4 == 0 && R_ <= 64 && C_ <= 32 && (R_ + 2 * kRing) * PC <= 2048, "lean kernel geometry");
@@ -2484,7 +2485,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
   // tick ahead: the fan entry once the tick has marched its own (the staging is then free),
   // a cone entry once the guard's move is known (the pose after the next move; a finishing
   // env re-issues it for its reset pose; double-buffered by tick parity).  The tick's stores
-  // go last, so the next tick's counted wait for the DMA (kLeanStores younger operations)
+  // go last, so the next tick's counted wait for the DMA (kStores younger operations)
   // never waits for a store to reach memory.
   auto dma_fan = [&](int k, bool wide) {  // k < K
     const FanTick* f = fan0 + k;
@@ -2746,9 +2747,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
   for (int k = 0; k < K; ++k) {
     const int par = k & 1;
     if ((k & 63) == 0) vact = k + lane < K ? L.act[k + lane] : 0u;
-    // the DMA issued a tick ago (older than the previous tick's kLeanStores stores) has landed
+    // the DMA issued a tick ago (older than the previous tick's kStores stores) has landed
     if (PROBE == 21) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kLeanStores) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kStores) : "memory");
     int n_uniq = 0, n_tie = 0;
     if (!ivl) {  // one LDS read for both header words
       const int2 h = *reinterpret_cast<const int2*>(&L.stg->hdr[2]);
@@ -2760,7 +2761,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     const bool frozen = s.done != 0;  // finished, no auto-reset: environment.py:232-233
     double reward = 0.0;
     int status = kAlreadyDone, curr = 0;
-    if (!frozen) {
+    if (!frozen && PROBE != 27) {
       // 1. move (environment.py:239-246) and the reward terms that precede detection (:235, :261-269)
       const int a = __builtin_amdgcn_readlane((int)vact, k & 63);
       const int nr = s.pos_r + (a == 1 ? -1 : (a == 2 ? 1 : 0)), nc = s.pos_c + (a == 3 ? -1 : (a == 4 ? 1 : 0));
@@ -2789,7 +2790,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       if (k + 1 < K) dma_next_cone(par ^ 1);  // tick k + 1's entry if the env still acts then
       LEAN_STAMP(1);  // 1: move, rotation, patrol
       // 3. visibility (environment.py:257-258)
-      if (PROBE != 22) cast(k, n_uniq, n_tie, par, true, staged_wide);
+      if (PROBE != 22 && PROBE != 28) cast(k, n_uniq, n_tie, par, true, staged_wide);
       LEAN_STAMP(3);  // 3: the cached guard cones (2: the cameras, inside cast)
     }
     // (tick k + 1's fan entry went out inside cast_fan; a frozen env keeps its plane and skips it)
@@ -2803,7 +2804,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     }
     int done_now = s.done;
     LEAN_STAMP(4);  // 4: next fan DMA, the channel-1 quads
-    if (!frozen) {
+    if (!frozen && PROBE != 27 && PROBE != 28) {
       // 4. detection, vault, timeout (environment.py:271-297), in the reference's order
       const int sol = s.pos_r * C_ + s.pos_c, qs = sol >> 2;
       uint32_t vq = v1[0];  // the quad holding the solver's tile (register qs >> 6, wave-uniform)
@@ -2862,11 +2863,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       if (k + 1 < K) dma_next_cone(par ^ 1);  // tick k + 1's entry from the reset pose
     }
     LEAN_STAMP(6);  // 6: auto-reset
-    // 6. tick k's stores (kLeanStores, unconditional; lanes with nothing to store pass an
-    // offset past their buffer descriptor, which the hardware drops): observation channels
-    // 0, 1, 2, the solver's quad of channel 2 again (same lane, program order: it lands
-    // last), reward, reward64, done, status
+    // 6. tick k's stores (kStores, unconditional; lanes with nothing to store pass an offset
+    // past their buffer descriptor, which the hardware drops): observation channels 0, 1, 2
+    // (Q quads per lane each), reward, reward64, done, status
     asm volatile("" ::: "memory");
+    constexpr int pol = 2;  // nt (policy A/B: profiles/r02ba_probe_obs_store.log; sc1 nt 3 % slower here, r05w)
     float* o = obs + ((size_t)k * N + e) * 3 * RC;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(o, (short)0, 12 * RC, 0x00020000);
     const int sol = s.pos_r * C_ + s.pos_c, qs = sol >> 2;
@@ -2879,22 +2880,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       const uint32_t b = PROBE == 26 ? 0x01020304u : *reinterpret_cast<const uint32_t*>(L.grid + 4 * qc);
       // float32(tile) / 5 == float32(tile) * 0.2f for every tile type (environment.py:319)
       if (PROBE == 23) continue;
-      obs_put(rs, 2, in ? 16 * q : (int)kOOB,
+      obs_put(rs, pol, in ? 16 * q : (int)kOOB,
               make_float4((float)(b & 0xff) * 0.2f, (float)((b >> 8) & 0xff) * 0.2f,
                           (float)((b >> 16) & 0xff) * 0.2f, (float)(b >> 24) * 0.2f));
       const uint32_t v = v1[j];
-      obs_put(rs, 2, in ? 16 * (N4 + q) : (int)kOOB,
+      obs_put(rs, pol, in ? 16 * (N4 + q) : (int)kOOB,
               make_float4((float)(v & 0xff), (float)((v >> 8) & 0xff), (float)((v >> 16) & 0xff), (float)(v >> 24)));
       float4 c2 = PROBE == 26 ? make_float4(0.f, 0.f, 0.f, 0.f) : L.plane2[qc];
-      obs_put(rs, 2, in ? 16 * (2 * N4 + q) : (int)kOOB, c2);
-      if (j == (qs >> 6)) {
-        // the solver's cell of channel 2 is fl32(1 + g) for its static value g (heist_create's
-        // second plane), unless it is the vault, whose value wins
-        const int m = sol & 3;
-        const float g0 = m == 0 ? c2.x : (m == 1 ? c2.y : (m == 2 ? c2.z : c2.w));
-        if (sol != vault) patch4(c2, m, 1.0f + g0);
-        obs_put(rs, 2, (qs & 63) == lane ? 16 * (2 * N4 + qs) : (int)kOOB, c2);
-      }
+      // the solver's cell of channel 2 is fl32(1 + g) for its static value g (heist_create's
+      // second plane), unless it is the vault, whose value wins: patched in the register of
+      // the lane that stores its quad (one store per quad, no second write of the line)
+      const bool pl = q == qs && sol != vault;
+      const int m = sol & 3;
+      c2.x = pl && m == 0 ? 1.0f + c2.x : c2.x;
+      c2.y = pl && m == 1 ? 1.0f + c2.y : c2.y;
+      c2.z = pl && m == 2 ? 1.0f + c2.z : c2.z;
+      c2.w = pl && m == 3 ? 1.0f + c2.w : c2.w;
+      obs_put(rs, pol, in ? 16 * (2 * N4 + q) : (int)kOOB, c2);
     }
     const uint32_t ko = (uint32_t)((size_t)k * N + e);
     const int l0 = lane == 0 ? 0 : (int)kOOB;
@@ -3587,7 +3589,7 @@ hipError_t launch_step_multi(const EnvParams& p, int K, const int64_t* actions, 
   // whatever multi_waves says, the envs it cannot serve taking the one-wave generic body)
   const bool lean20 = p.multi_waves == 1 && p.R == 20 && p.C == 20 && p.vis_gap == 1024;
   const bool lean32 = p.R == 32 && p.C == 32 && p.vis_gap == 2048;
-  if (p.lean && lean20 && p.probe_mode >= 21 && p.probe_mode <= 26 && !p.stamps &&
+  if (p.lean && lean20 && p.probe_mode >= 21 && p.probe_mode <= 28 && !p.stamps &&
       p.max_cams + p.max_guards <= kMaxEmitters) {  // profiling variants of the lean kernel
     if (p.fan_on && p.fan_fill) hipLaunchKernelGGL(fan_kernel, dim3(kFanTicks), dim3(kFanRays), 0, st, p);
     const size_t lds_l = lean_lds_bytes(p, K);
@@ -3596,7 +3598,7 @@ hipError_t launch_step_multi(const EnvParams& p, int K, const int64_t* actions, 
     hipLaunchKernelGGL((step_lean_kernel<20, 20, false, M>), dim3(p.n_envs), dim3(64), lds_l, st, p, K, actions, obs, \
                        rew, rew64, done_out, status_out, auto_reset);
     HEIST_LEAN_PROBE(21) HEIST_LEAN_PROBE(22) HEIST_LEAN_PROBE(23) HEIST_LEAN_PROBE(24) HEIST_LEAN_PROBE(25)
-    HEIST_LEAN_PROBE(26)
+    HEIST_LEAN_PROBE(26) HEIST_LEAN_PROBE(27) HEIST_LEAN_PROBE(28)
 #undef HEIST_LEAN_PROBE
     return hipGetLastError();
   }

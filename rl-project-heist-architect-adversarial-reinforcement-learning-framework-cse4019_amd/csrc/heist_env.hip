@@ -2280,7 +2280,7 @@ struct LeanLds {
   LeanStage* stg;  // an env the shared fan serves: the next tick's fan entry
   IvlTable* ivl;   // any other env: the interval table (same LDS)
   uint4* icam;     // interval fans, per camera: start angle, first cut, rays | tile << 16
-  double* icim;    //   and 1 / ray spacing
+  int32_t* icim;   //   and 2^52 / ray spacing (rounded; < 2^31)
   uint32_t* ivq;   //   the marching queue (128 entries)
   uint16_t* cone;
   float4* plane2;
@@ -2302,7 +2302,7 @@ __host__ __device__ inline size_t lean_carve(unsigned char* smem, int R, int C, 
   o += align16(kLeanUnion);
   if (L) L->icam = reinterpret_cast<uint4*>(smem + o);
   o += 16 * (size_t)(mc > 0 ? mc : 1);
-  if (L) L->icim = reinterpret_cast<double*>(smem + o);
+  if (L) L->icim = reinterpret_cast<int32_t*>(smem + o);
   o += align16(8 * (size_t)(mc > 0 ? mc : 1));
   if (L) L->ivq = reinterpret_cast<uint32_t*>(smem + o);
   o += 4 * 128;
@@ -2386,7 +2386,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
   const bool live_cam = lane < s.n_cams, live_guard = g >= 0 && g < s.n_guards;
   bool cached = false;
   // interval fans (camera lanes): fov, the ray spacing in angle units and its reciprocal, rays
-  double fovd = 0.0, su = 1.0, isu = 1.0;
+  double fovd = 0.0, su = 1.0;
+  int32_t im_fx = 0;  // 2^52 / su rounded: the pair bounds as integer products (cast_ivl)
   int cam_n = 0;
   bool ivl = false;  // this env casts its cameras from the interval table (else from the shared fan)
   {
@@ -2420,8 +2421,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     // turn (signed angle differences) and rays farther apart than two axis margins (at most
     // one ray near any cut)
     const double su_ = (cm.fov / (double)cm.num_rays) * kFanUnitsPerDeg;
+    // (and spacing su >= 2^21 units, ~0.18 degrees, so that 2^52 / su fits an int32; every
+    // fov >= 5.3 degrees: security.py:67 spaces rays fov / max(2 fov, 30) apart)
     const bool ivl_cam = !live_cam || (cm.range == kTieMaxRange && cm.num_rays >= 1 && cm.fov > 0.0 &&
-                                       cm.fov < 179.0 && su_ > 2.0 * (double)kFanMarginAxis + 8.0);
+                                       cm.fov < 179.0 && su_ > 2.0 * (double)kFanMarginAxis + 8.0 &&
+                                       su_ >= 2097153.0);
     ivl = base_ok && !fan_ok && p.interval_fans && __ballot(!ivl_cam) == 0ull;
     if (!base_ok || (!fan_ok && !ivl)) {
       step_multi_body<1, 4, 4, D, false, 0>(p, K, actions, obs, rew, rew64, done_out, status_out, auto_reset, smem, e);
@@ -2430,7 +2434,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     if (live_cam) {
       fovd = cm.fov;
       su = su_;
-      isu = 1.0 / su_;
+      im_fx = (int32_t)__builtin_rint(4503599627370496.0 / su_);
       cam_n = cm.num_rays;
     }
   }
@@ -2658,7 +2662,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       const int je = (int)L.ivl->idx[__umulhi((uint32_t)e64, 360u) + 1u] + kFanCuts * (int)(e64 >> 32);
       cnt = je - jb;
       L.icam[lane] = make_uint4(h0v, (uint32_t)jb, (uint32_t)cam_n | (cam_rc << 16), 0u);
-      L.icim[lane] = isu;
+      L.icim[lane] = im_fx;
     }
     // the pair counts' running sums are scalar: a few cameras, summed where they are needed;
     // camera lane m keeps jo = jb - (pairs of cameras 0 .. m-1), so pair q of camera m has cut
@@ -2699,16 +2703,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       int j = jo + q;
       j = j < 0 ? j + kFanCuts : (j >= kFanCuts ? j - kFanCuts : j);
       const uint4 cu = L.icam[c];
-      const double im = L.icim[c];
+      const int im = L.icim[c];
       const int n = (int)(cu.z & 0xffffu);
       const int jn = j + 1 == kFanCuts ? 0 : j + 1;
       const uint32_t cut = L.ivl->cut[j], cutn = L.ivl->cut[jn];
-      const double rel = (double)(int)(cut - cu.x), reln = (double)(int)(cutn - cu.x);
-      const double mj = (cut & 0x3FFFFFFFu) ? (double)kFanMarginTie : (double)kFanMarginAxis;
-      const double mn = (cutn & 0x3FFFFFFFu) ? (double)kFanMarginTie : (double)kFanMarginAxis;
-      const int A = (int)__builtin_floor((rel + mj) * im) + 1;  // first ray past cut j's margin
-      const int B = (int)__builtin_ceil((rel - mj) * im);       // first ray inside it
-      const int Bn = (int)__builtin_ceil((reln - mn) * im);     // first ray inside cut j+1's
+      const int rel = (int)(cut - cu.x), reln = (int)(cutn - cu.x);
+      const int mj = (cut & 0x3FFFFFFFu) ? kFanMarginTie : kFanMarginAxis;
+      const int mn = (cutn & 0x3FFFFFFFu) ? kFanMarginTie : kFanMarginAxis;
+      // floor(x / su) as the high word of the 64-bit product x * im >> 20 (floor(x im / 2^52));
+      // ceil(x / su) = -floor(-x / su).  The product's error is below 2^31 * 2^-53 rays, ~1.4
+      // angle units at su = 0.5 degrees, far inside the 64- and 720-unit margins.
+      const int A = (__mulhi(rel + mj, im) >> 20) + 1;  // first ray past cut j's margin
+      const int B = -(__mulhi(mj - rel, im) >> 20);     // first ray inside it
+      const int Bn = -(__mulhi(mn - reln, im) >> 20);   // first ray inside cut j+1's
       const int a0 = A > 0 ? A : 0;
       const bool act = q < total;
       const bool safe = act && a0 <= n && a0 < Bn;

@@ -77,13 +77,20 @@ def fan_lanes(heading, fov):
     """The kernel's partition of one camera's rays (heist_env.hip step_lean_kernel cast_ivl, same
     arithmetic): returns (intervals to march, near ray indices for the exact path).  Ray i
     sits i * s units past h0; cut j (rel units past h0, margin m) owns rays ceil((rel - m) / s)
-    .. floor((rel + m) / s) (exact path); interval j the rays after those up to the next cut's."""
+    .. floor((rel + m) / s) (exact path); interval j the rays after those up to the next cut's.
+    The divisions are integer products: floor(x / s) = (mulhi(x, im) >> 20) with
+    im = rint(2^52 / s) (v_mul_hi_i32, an arithmetic shift), ceil(x / s) = -floor(-x / s)."""
     n = max(int(fov * 2), 30)  # security.py:67
     hmh = heading - fov / 2.0
     hw = hmh + 360.0 if hmh < 0.0 else hmh
     h0 = int(min(hw * UPD, 4294967295.0))
     s = (fov / float(n)) * UPD
-    inv_s = 1.0 / s
+    assert s >= 2097153.0  # the kernel's eligibility: im fits an int32
+    im = round(4503599627370496.0 / s)  # rint (ties to even, as round())
+    assert 0 < im < 2 ** 31
+
+    def fl(x):  # floor(x / s): high word of the signed 64-bit product, >> 20
+        return ((x * im) >> 32) >> 20
     deg = (h0 * 360) >> 32
     jb = IDX[deg] - 1  # -1: cut 251 of the turn before
     e64 = h0 + int(float(n) * s) + MA + 4  # past the last ray and its margin
@@ -92,13 +99,16 @@ def fan_lanes(heading, fov):
     for ju in range(jb, je):  # the camera's (camera, cut) pairs, packed over the lanes
         j = ju % 252
         cut, cutn = CUT[j], CUT[(j + 1) % 252]
-        rel = float(((cut - h0 + 2 ** 31) % U) - 2 ** 31)
-        reln = float(((cutn - h0 + 2 ** 31) % U) - 2 ** 31)
-        mj = float(MA if cut % (U // 4) == 0 else MT)
-        mn = float(MA if cutn % (U // 4) == 0 else MT)
-        A = math.floor((rel + mj) * inv_s) + 1
-        B = math.ceil((rel - mj) * inv_s)
-        Bn = math.ceil((reln - mn) * inv_s)
+        rel = ((cut - h0 + 2 ** 31) % U) - 2 ** 31
+        reln = ((cutn - h0 + 2 ** 31) % U) - 2 ** 31
+        mj = MA if cut % (U // 4) == 0 else MT
+        mn = MA if cutn % (U // 4) == 0 else MT
+        A = fl(rel + mj) + 1
+        B = -fl(mj - rel)
+        Bn = -fl(mn - reln)
+        # the products stay within a signed 64-bit word and agree with the exact quotients
+        # to far less than a margin (1.4 units at s = 0.5 degrees)
+        assert abs((rel + mj) - (A - 1) * s) <= s + 2 and abs(B * s - (rel - mj)) <= s + 2
         a0 = max(A, 0)
         if a0 <= n and a0 < Bn:
             march.append(j)
@@ -106,8 +116,8 @@ def fan_lanes(heading, fov):
             near.append(B)
     # the pairs past je hold nothing: the next cut's margin starts past the last ray
     j = je % 252
-    rel = float(((CUT[j] - h0 + 2 ** 31) % U) - 2 ** 31)
-    assert math.ceil((rel - float(MA if CUT[j] % (U // 4) == 0 else MT)) * inv_s) > n
+    rel = ((CUT[j] - h0 + 2 ** 31) % U) - 2 ** 31
+    assert -fl((MA if CUT[j] % (U // 4) == 0 else MT) - rel) > n
     return march, near
 
 

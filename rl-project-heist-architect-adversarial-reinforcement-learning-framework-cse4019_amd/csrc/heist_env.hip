@@ -2273,6 +2273,9 @@ constexpr IvlTable make_ivl_table() {
 }
 __constant__ IvlTable kIvlTable = make_ivl_table();
 constexpr size_t kLeanUnion = sizeof(LeanStage) > sizeof(IvlTable) ? sizeof(LeanStage) : sizeof(IvlTable);
+// a chunk of (camera, cut) pairs with at least this many intervals holding a ray marches them
+// in place, one per lane; sparser chunks go through the marching queue (cast_ivl)
+constexpr int kIvlDense = 56;
 struct LeanLds {
   uint8_t* grid;
   uint16_t* path;
@@ -2675,14 +2678,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       if (lane == m) end_l = total;
     }
     int qn = 0;  // marching queue L.ivq: entries j | camera tile (row | col << 8) << 8
+    // one interval's march from the camera tile rc (row | col << 8) along direction d
+    auto march_at = [&](uint32_t rc, float2 d) {
+      const uint32_t row = rc & 0xffu, col = rc >> 8;
+      const uint32_t own = base + (row + kRing) * PC + col + kRing;
+      const float mx = __builtin_bit_cast(float, base + col + kRing), my = __builtin_bit_cast(float, row + kRing);
+      march_fast<D, 2 * kTieMaxRange, false, false, true>(PC, own, d.x, d.y, mx, my, 2 * kTieMaxRange);
+    };
     auto march_queue = [&](int n_q) {
       if (lane < n_q) {
         const uint32_t ent = L.ivq[lane];
-        const uint32_t row = (ent >> 8) & 0xffu, col = ent >> 16;
-        const uint32_t own = base + (row + kRing) * PC + col + kRing;
-        const float mx = __builtin_bit_cast(float, base + col + kRing), my = __builtin_bit_cast(float, row + kRing);
-        const float2 d = L.ivl->dir[ent & 0xffu];
-        march_fast<D, 2 * kTieMaxRange, false, false, true>(PC, own, d.x, d.y, mx, my, 2 * kTieMaxRange);
+        march_at(ent >> 8, L.ivl->dir[ent & 0xffu]);
       }
     };
     int mb = 0;  // the first camera whose pairs reach this chunk
@@ -2707,6 +2713,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       const int n = (int)(cu.z & 0xffffu);
       const int jn = j + 1 == kFanCuts ? 0 : j + 1;
       const uint32_t cut = L.ivl->cut[j], cutn = L.ivl->cut[jn];
+      const float2 dj = L.ivl->dir[j];  // read with the cuts: a dense chunk marches in place
       const int rel = (int)(cut - cu.x), reln = (int)(cutn - cu.x);
       const int mj = (cut & 0x3FFFFFFFu) ? kFanMarginTie : kFanMarginAxis;
       const int mn = (cutn & 0x3FFFFFFFu) ? kFanMarginTie : kFanMarginAxis;
@@ -2725,7 +2732,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
         ivl_tie_rays<D, PC>(smem, near ? B : -1, h_c, f_c, n, cu.z >> 16, p.half_deg);
       }
       const unsigned long long sb = __ballot(safe);
-      if (safe) {
+      if (__popcll(sb) >= kIvlDense) {  // dense (most chunks: ~92 % of the pairs hold a ray): in place
+        if (safe) march_at(cu.z >> 16, dj);
+        continue;
+      }
+      if (safe) {  // sparse: through the queue, marched 64 at a time
         const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(sb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sb, 0u));
         L.ivq[pos] = (uint32_t)j | ((cu.z >> 16) << 8);
       }

@@ -2273,9 +2273,6 @@ constexpr IvlTable make_ivl_table() {
 }
 __constant__ IvlTable kIvlTable = make_ivl_table();
 constexpr size_t kLeanUnion = sizeof(LeanStage) > sizeof(IvlTable) ? sizeof(LeanStage) : sizeof(IvlTable);
-// a chunk of (camera, cut) pairs with at least this many intervals holding a ray marches them
-// in place, one per lane; sparser chunks go through the marching queue (cast_ivl)
-constexpr int kIvlDense = 56;
 struct LeanLds {
   uint8_t* grid;
   uint16_t* path;
@@ -2284,7 +2281,6 @@ struct LeanLds {
   IvlTable* ivl;   // any other env: the interval table (same LDS)
   uint4* icam;     // interval fans, per camera: start angle, first cut, rays | tile << 16
   int32_t* icim;   //   and 2^52 / ray spacing (rounded; < 2^31)
-  uint32_t* ivq;   //   the marching queue (128 entries)
   uint16_t* cone;
   float4* plane2;
 };
@@ -2307,8 +2303,6 @@ __host__ __device__ inline size_t lean_carve(unsigned char* smem, int R, int C, 
   o += 16 * (size_t)(mc > 0 ? mc : 1);
   if (L) L->icim = reinterpret_cast<int32_t*>(smem + o);
   o += align16(8 * (size_t)(mc > 0 ? mc : 1));
-  if (L) L->ivq = reinterpret_cast<uint32_t*>(smem + o);
-  o += 4 * 128;
   if (L) L->cone = reinterpret_cast<uint16_t*>(smem + o);
   o += 64 * (size_t)(mg > 0 ? mg : 1);
   if (L) L->plane2 = reinterpret_cast<float4*>(smem + o);
@@ -2646,10 +2640,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
   // (tests/test_fan_intervals.py restates this and checks it against the oracle's cones).
   // The env's cameras are packed: camera c needs the cuts jb_c .. je_c - 1 (jb: the last cut
   // before its first ray, je: the first one past its last ray + margin), and the (camera, cut)
-  // pairs of all cameras fill the lanes 64 at a time; the intervals found to hold a ray go
-  // to an LDS queue that is marched 64 at a time with per-lane origins -- so a wave's lanes
-  // are busy whatever the fan widths, and an env's chain of chunks is as short as its cameras'
-  // total interval count allows.
+  // pairs of all cameras fill the lanes 64 at a time, and each lane whose interval holds a
+  // ray marches it in place from its camera's tile -- so a wave's lanes are busy whatever the
+  // fan widths, and an env's chain of chunks is as short as its cameras' total cut count
+  // allows (about 92 % of the pairs of the synthetic mix hold a ray; packing the marches
+  // through an LDS queue, 64 per march, was slower: one more LDS round trip per march).
   auto cast_ivl = [&](int par) {
 #pragma unroll
     for (int z = 0; z < D / 1024; ++z)  // 64 x 16 B per pass: the plane
@@ -2677,19 +2672,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       total += __builtin_amdgcn_readlane(cnt, m);
       if (lane == m) end_l = total;
     }
-    int qn = 0;  // marching queue L.ivq: entries j | camera tile (row | col << 8) << 8
     // one interval's march from the camera tile rc (row | col << 8) along direction d
     auto march_at = [&](uint32_t rc, float2 d) {
       const uint32_t row = rc & 0xffu, col = rc >> 8;
       const uint32_t own = base + (row + kRing) * PC + col + kRing;
       const float mx = __builtin_bit_cast(float, base + col + kRing), my = __builtin_bit_cast(float, row + kRing);
       march_fast<D, 2 * kTieMaxRange, false, false, true>(PC, own, d.x, d.y, mx, my, 2 * kTieMaxRange);
-    };
-    auto march_queue = [&](int n_q) {
-      if (lane < n_q) {
-        const uint32_t ent = L.ivq[lane];
-        march_at(ent >> 8, L.ivl->dir[ent & 0xffu]);
-      }
     };
     int mb = 0;  // the first camera whose pairs reach this chunk
     for (int q0 = 0; q0 < total; q0 += 64) {
@@ -2713,7 +2701,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
       const int n = (int)(cu.z & 0xffffu);
       const int jn = j + 1 == kFanCuts ? 0 : j + 1;
       const uint32_t cut = L.ivl->cut[j], cutn = L.ivl->cut[jn];
-      const float2 dj = L.ivl->dir[j];  // read with the cuts: a dense chunk marches in place
+      const float2 dj = L.ivl->dir[j];  // read with the cuts
       const int rel = (int)(cut - cu.x), reln = (int)(cutn - cu.x);
       const int mj = (cut & 0x3FFFFFFFu) ? kFanMarginTie : kFanMarginAxis;
       const int mn = (cutn & 0x3FFFFFFFu) ? kFanMarginTie : kFanMarginAxis;
@@ -2731,24 +2719,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
         const double h_c = __shfl(hmh, c, 64), f_c = __shfl(fovd, c, 64);
         ivl_tie_rays<D, PC>(smem, near ? B : -1, h_c, f_c, n, cu.z >> 16, p.half_deg);
       }
-      const unsigned long long sb = __ballot(safe);
-      if (__popcll(sb) >= kIvlDense) {  // dense (most chunks: ~92 % of the pairs hold a ray): in place
-        if (safe) march_at(cu.z >> 16, dj);
-        continue;
-      }
-      if (safe) {  // sparse: through the queue, marched 64 at a time
-        const int pos = qn + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(sb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sb, 0u));
-        L.ivq[pos] = (uint32_t)j | ((cu.z >> 16) << 8);
-      }
-      qn += __popcll(sb);
-      if (qn >= 64) {
-        march_queue(64);
-        const uint32_t rest = L.ivq[64 + lane];
-        if (lane < qn - 64) L.ivq[lane] = rest;
-        qn -= 64;
-      }
+      if (safe) march_at(cu.z >> 16, dj);
     }
-    if (qn > 0) march_queue(qn);
     LEAN_STAMP(2);
     stamp_cones(par);
   };

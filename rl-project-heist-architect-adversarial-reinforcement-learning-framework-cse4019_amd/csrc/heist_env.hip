@@ -2338,7 +2338,8 @@ struct LeanGuard {
 // tick segments over the launch (LEAN_SEGS in tools/probe_lean_stamps.py) in LDS after the
 // carve and writes [segment sums 0..8, lifetime, start clock, HW_ID, XCC_ID] to
 // stamps[env][0][16] (the generic K-tick body's layout); envs on the generic body record none.
-// PROBE (profiling only, HEIST_PROBE_MODE, results wrong): 21 no wait for the previous tick's
+// PROBE (profiling only, HEIST_PROBE_MODE with a library built -DHEIST_LEAN_PROBES,
+// tools/build_variant.sh; results wrong): 21 no wait for the previous tick's
 // DMA, 22 no visibility cast, 23 no observation stores, 24 / 25 shared-fan marches without
 // their visibility stores / stop-byte loads, 26 the observation stores without their LDS reads,
 // 27 the stores alone (no move, cast, detection), 28 move + patrol + stores.
@@ -3579,8 +3580,9 @@ hipError_t launch_step_multi(const EnvParams& p, int K, const int64_t* actions, 
   // whatever multi_waves says, the envs it cannot serve taking the one-wave generic body)
   const bool lean20 = p.multi_waves == 1 && p.R == 20 && p.C == 20 && p.vis_gap == 1024;
   const bool lean32 = p.R == 32 && p.C == 32 && p.vis_gap == 2048;
+#ifdef HEIST_LEAN_PROBES  // profiling variants of the lean kernel (tools/build_variant.sh ... -DHEIST_LEAN_PROBES)
   if (p.lean && lean20 && p.probe_mode >= 21 && p.probe_mode <= 28 && !p.stamps &&
-      p.max_cams + p.max_guards <= kMaxEmitters) {  // profiling variants of the lean kernel
+      p.max_cams + p.max_guards <= kMaxEmitters) {
     if (p.fan_on && p.fan_fill) hipLaunchKernelGGL(fan_kernel, dim3(kFanTicks), dim3(kFanRays), 0, st, p);
     const size_t lds_l = lean_lds_bytes(p, K);
 #define HEIST_LEAN_PROBE(M)                                                                                       \
@@ -3592,6 +3594,7 @@ hipError_t launch_step_multi(const EnvParams& p, int K, const int64_t* actions, 
 #undef HEIST_LEAN_PROBE
     return hipGetLastError();
   }
+#endif
   if (p.lean && (lean20 || lean32) && p.probe_mode == 0 && !p.sample_counter && !p.redo_counter &&
       p.max_cams + p.max_guards <= kMaxEmitters) {
     if (p.fan_on && p.fan_fill) hipLaunchKernelGGL(fan_kernel, dim3(kFanTicks), dim3(kFanRays), 0, st, p);

@@ -894,6 +894,51 @@ def test_step_lean_interval_fans(gpu_device, monkeypatch, n, budget, auto_reset)
         assert torch.equal(sa[key], sb[key]), key
 
 
+def test_step_lean_interval_fans_narrow_fovs(gpu_device, monkeypatch):
+    """Cameras around the interval fans' ray-spacing bound (su >= 2^21 angle units: the integer
+    pair bounds need rint(2^52 / su) in an int32; fov / 30 rays below ~5.27 degrees sends the
+    env to the generic body): fovs 2 .. 16 degrees mixed with ordinary ones, 512 envs, == single
+    ticks and 16 envs == the C oracle over 60 ticks in launches of 20 and 40."""
+    rng = np.random.default_rng(17)
+    n, R, budget = 512, 20, 15
+    cfg = EnvironmentConfig(max_steps=30)
+    lays = []
+    for walls, cams, guards in synthetic_layouts(n, R, R, budget, seed=171):
+        cams = [dict(c) for c in cams]
+        for c in cams:
+            if rng.random() < 0.6:
+                c.update(fov_angle=float(rng.choice([2.0, 5.0, 5.25, 5.2734375, 5.3, 6.0, 10.0, 15.5])))
+        lays.append((walls, cams, guards))
+    monkeypatch.setenv("HEIST_MULTI_WAVES", "1")
+    envs = []
+    for _ in range(2):
+        env = HeistEnv(n, cfg, max_cams=5, max_guards=3, max_path=16, device=gpu_device)
+        v = env.set_layouts(lays, budget=budget)
+        env.reset()
+        envs.append((env, v))
+    (a, va), (b, vb) = envs
+    assert torch.equal(va, vb)
+    assert a.kernel_config()["lean"] == 1 and a.kernel_config()["multi_waves"] == 1
+    pick = np.random.default_rng(3).choice(np.nonzero(va.cpu().numpy().astype(bool))[0], 16, replace=False)
+    oracles = _oracle_envs(cfg, [lays[i] for i in pick], budget)
+    g = torch.Generator(device="cpu").manual_seed(91)
+    acts = torch.randint(0, 5, (60, n), generator=g).to(gpu_device)
+    k0 = 0
+    for kk in (20, 40):
+        obs, rew, done, status, r64 = a.step_multi(acts[k0:k0 + kk], reward64=True)
+        for k in range(kk):
+            o, r, d, s = b.step(acts[k0 + k])
+            assert torch.equal(obs[k], o) and torch.equal(r64[k], b.reward64), k0 + k
+            assert torch.equal(done[k], d) and torch.equal(status[k], s), k0 + k
+            for i, o_env in zip(pick, oracles):
+                r_, d_, s_ = o_env.step(int(acts[k0 + k, i]))
+                if d_:
+                    o_env.reset()
+                assert (float(r64[k, i]), bool(done[k, i]), int(status[k, i])) == (r_, d_, s_), (k0 + k, i)
+                assert obs[k, i].cpu().numpy().tobytes() == o_env.state_tensor().tobytes(), (k0 + k, i)
+        k0 += kk
+
+
 def test_step_lean_interval_fans_on_architect_layouts(gpu_device, monkeypatch):
     """The headline's Architect layouts with the shared fan table off (HEIST_SHARED_FAN=0):
     every env takes the interval fans instead; == single ticks, 60 ticks."""

@@ -1,5 +1,7 @@
-"""Time the K-tick lean kernel under the current HEIST_* knobs (profiling modes included,
-whose results are wrong: timing only) on bench.py's env workload: 4096 envs, K = 20,
+"""Time the K-tick lean kernel under the current HEIST_* knobs (profiling modes 21-28 need a
+library built with tools/build_variant.sh probes -DHEIST_LEAN_PROBES, loaded with
+HEIST_LIB=tools/variants/libheist_hip_probes.so; their results are wrong: timing only) on
+bench.py's env workload: 4096 envs, K = 20,
 PROBE_LAYOUTS architect (the headline) or synthetic.  HIP events around 100 launches after
 a clock settle; prints one JSON line (us per tick, median of 3 windows)."""
 import json

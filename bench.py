@@ -105,8 +105,10 @@ def cpu_baseline(layouts, cfg, budget, target_s=10.0, threads=1):
         with open(rf) as f:
             ratio = json.load(f)["oracle_over_reference"]
         out["python_reference_equivalent"] = {
-            "value": out["value"] / ratio, "unit": "env-steps/s", "oracle_over_reference": ratio,
-            "source": "profiles/cpu_ratio.json (tools/cpu_ratio.py: same layouts, one core of the build container)"}
+            "value": out["value"] / ratio, "unit": "env-steps/s", "oracle_over_reference": ratio, "estimate": True,
+            "source": "profiles/cpu_ratio.json (tools/cpu_ratio.py: same layouts, one core of the build container)",
+            "note": "derived, not timed here: this host's C-oracle rate divided by the oracle / Python-reference "
+                    "speed ratio measured on another machine (the reference itself cannot run on the GPU box)"}
     return out
 
 

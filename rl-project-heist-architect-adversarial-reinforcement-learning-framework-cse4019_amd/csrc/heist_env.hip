@@ -2420,9 +2420,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
     // one ray near any cut)
     const double su_ = (cm.fov / (double)cm.num_rays) * kFanUnitsPerDeg;
     // (and spacing su >= 2^21 units, ~0.18 degrees, so that 2^52 / su fits an int32; every
-    // fov >= 5.3 degrees: security.py:67 spaces rays fov / max(2 fov, 30) apart)
+    // fov >= 5.3 degrees: security.py:67 spaces rays fov / max(2 fov, 30) apart).  fov < 170:
+    // the farthest cut a camera's pairs look at lies at most fov + the widest cut gap (4.8
+    // degrees, between an axis and asin(1/12)) past h0, inside the int32 half turn
     const bool ivl_cam = !live_cam || (cm.range == kTieMaxRange && cm.num_rays >= 1 && cm.fov > 0.0 &&
-                                       cm.fov < 179.0 && su_ > 2.0 * (double)kFanMarginAxis + 8.0 &&
+                                       cm.fov < 170.0 && su_ > 2.0 * (double)kFanMarginAxis + 8.0 &&
                                        su_ >= 2097153.0);
     ivl = base_ok && !fan_ok && p.interval_fans && __ballot(!ivl_cam) == 0ull;
     if (!base_ok || (!fan_ok && !ivl)) {

@@ -99,6 +99,10 @@ def fan_lanes(heading, fov):
     for ju in range(jb, je):  # the camera's (camera, cut) pairs, packed over the lanes
         j = ju % 252
         cut, cutn = CUT[j], CUT[(j + 1) % 252]
+        # every cut lies ahead of h0 by less than the int32 half turn or a little behind it
+        # (cuts of h0's own degree): the kernel's signed offsets never wrap (fov < 170)
+        ahead = (cutn - h0) % U
+        assert ahead < 2 ** 31 - 2 * MA or ahead > U - 6 * UPD
         rel = ((cut - h0 + 2 ** 31) % U) - 2 ** 31
         reln = ((cutn - h0 + 2 ** 31) % U) - 2 ** 31
         mj = MA if cut % (U // 4) == 0 else MT
@@ -179,6 +183,19 @@ def test_partition_matches_oracle_random_cameras():
             n_near += nn
             heading = (heading + float(np.float32(rng.uniform(5, 35)))) % 360.0
     assert n_near < 0.002 * n_march, (n_near, n_march)
+
+
+def test_partition_widest_fans():
+    """fovs up to the eligibility bound (< 170 degrees): the signed cut offsets never wrap,
+    and the cones still equal the oracle's."""
+    rng = np.random.default_rng(13)
+    for t in range(120):
+        walls = rng.random((20, 20)) < 0.08
+        row, col = int(rng.integers(1, 19)), int(rng.integers(1, 19))
+        walls[row, col] = False
+        fov = float(np.float32(rng.uniform(150, 169.99)))
+        heading = float(np.float32(rng.uniform(0, 360)))
+        _check(walls, row, col, heading, fov)
 
 
 def test_partition_axis_and_cut_rays():

@@ -239,15 +239,15 @@ def time_env(env, actions, warmup, steps, K, world, settle_ms=0.0, extra_windows
         dist.barrier()
     torch.cuda.synchronize(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)  # a marker on the idle stream (no work): the wall clock starts after its host call
     t0 = time.perf_counter()
-    e0.record(stream)
     launches = run(warmup, steps, ready)
     e1.record(stream)
     issue_s = time.perf_counter() - t0
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if world > 1:  # one rank: no barrier, so the one synchronize closes the window
         dist.barrier()
-    torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / steps
     windows = []

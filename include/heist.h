@@ -41,7 +41,7 @@ int heist_abi_version(void);
 const char* heist_last_error(void);
 
 /* Replaces HeistEnvironment.__init__ / EnvironmentConfig (environment.py:18-97) for a
- * batch of n_envs independent environments.  R, C <= 64.  reward_consts (host) =
+ * batch of n_envs independent environments (1 <= n_envs <= 2^24).  R, C <= 64.  reward_consts (host) =
  * {reward_step, reward_detection, reward_vault}.  max_cams / max_guards / max_path bound
  * the per-env layout capacity. */
 int heist_create(int rows, int cols, int max_steps, int start_r, int start_c, int vault_r, int vault_c,

@@ -163,6 +163,8 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   HEIST_REQUIRE(sr >= 0 && sr < R && sc >= 0 && sc < C && vr >= 0 && vr < R && vc >= 0 && vc < C,
                 "heist_create: start/vault outside the grid");
   HEIST_REQUIRE(n_envs >= 1, "heist_create: n_envs must be >= 1");
+  // order[] packs the env index in 24 bits (a wave priority above it, order_kernel)
+  HEIST_REQUIRE(n_envs <= (1 << 24), "heist_create: n_envs must be <= 16777216");
   HEIST_REQUIRE(max_cams >= 0 && max_guards >= 0 && max_cams + max_guards <= heist::kMaxEmitters,
                 "heist_create: need max_cams + max_guards <= 64");
   HEIST_REQUIRE(max_path >= 1 && max_path <= 4096, "heist_create: need 1 <= max_path <= 4096");

@@ -19,7 +19,7 @@ from heist_amd import EnvironmentConfig, HeistEnv  # noqa: E402
 
 def main():
     import bench
-    n, K = 4096, 20
+    n, K = 4096, int(os.environ.get("PROBE_K", "20"))
     lay = os.environ.get("PROBE_LAYOUTS", "architect")
     env = HeistEnv(n, EnvironmentConfig(architect_budget=15), max_cams=5, max_guards=3, max_path=16, device="cuda")
     if lay == "synthetic":
@@ -46,7 +46,19 @@ def main():
         b.record()
         torch.cuda.synchronize()
         wins.append(a.elapsed_time(b) * 1e3 / (100 * K))
-    print(json.dumps({"layouts": lay, "us_per_tick": statistics.median(wins), "windows": wins,
+    # the single-tick form (heist_step, what a rollout calls) on the same handle
+    single = []
+    if os.environ.get("PROBE_SINGLE"):
+        for _ in range(3):
+            a_, b_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a_.record()
+            for _ in range(100):
+                env.step(acts[0])
+            b_.record()
+            torch.cuda.synchronize()
+            single.append(a_.elapsed_time(b_) * 1e3 / 100)
+    print(json.dumps({"layouts": lay, "K": K, "us_per_tick": statistics.median(wins), "windows": wins,
+                      "single_tick_us": statistics.median(single) if single else None,
                       "knobs": {k: v for k, v in os.environ.items() if k.startswith("HEIST_")}}), flush=True)
 
 

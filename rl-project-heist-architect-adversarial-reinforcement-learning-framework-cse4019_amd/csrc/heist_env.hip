@@ -2334,6 +2334,19 @@ struct LeanGuard {
   __device__ uint32_t pos0() const { return b >> 16; }
 };
 
+// The generic K-tick body for an env the lean loop does not serve, as a call rather than
+// inlined: the lean loop is then scheduled and register-allocated on its own (C2 5.78 ->
+// 5.64-5.71 us per tick; with the body removed altogether 5.66-5.69, profiles/r05as_*), at
+// the price of a call frame (scratch) on the rare generic path.
+template <int D>
+__device__ __attribute__((noinline)) void lean_generic_body(EnvParams p, int K, const int64_t* __restrict__ actions,
+                                                            float* __restrict__ obs, float* __restrict__ rew,
+                                                            double* __restrict__ rew64, uint8_t* __restrict__ done_out,
+                                                            int8_t* __restrict__ status_out, int auto_reset,
+                                                            unsigned char* smem, int e) {
+  step_multi_body<1, 4, 4, D, false, 0>(p, K, actions, obs, rew, rew64, done_out, status_out, auto_reset, smem, e);
+}
+
 // STAMP (instrumentation, heist_step_stamps armed): lane 0 sums the shader clock spent in 9
 // tick segments over the launch (LEAN_SEGS in tools/probe_lean_stamps.py) in LDS after the
 // carve and writes [segment sums 0..8, lifetime, start clock, HW_ID, XCC_ID] to
@@ -2428,7 +2441,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void st
                                        su_ >= 2097153.0);
     ivl = base_ok && !fan_ok && p.interval_fans && __ballot(!ivl_cam) == 0ull;
     if (!base_ok || (!fan_ok && !ivl)) {
-      step_multi_body<1, 4, 4, D, false, 0>(p, K, actions, obs, rew, rew64, done_out, status_out, auto_reset, smem, e);
+      lean_generic_body<D>(p, K, actions, obs, rew, rew64, done_out, status_out, auto_reset, smem, e);
       return;
     }
     if (live_cam) {

@@ -77,7 +77,12 @@ struct ConvGeom {
   static constexpr int NT2 = (MT + 1) / 2;                 // position tiles per wave (conv2/conv3)
   static constexpr int W2 = align16c(INVA + 16 * 4);       // conv2 fragments [2][18][64] x 16 B
   static constexpr int SINK = W2 + 2 * 18 * 64 * 16;       // [64] x 8 B: stores of positions >= RC
-  static constexpr int LDS = SINK + 64 * 8;
+  static constexpr int FLAG = SINK + 64 * 8;               // [2] int: conv3 split-tile hand-off (env index)
+  static constexpr int LDS = FLAG + 16;
+  // conv3's last position tile MT - 1 (mh = 0's) split by k-steps between the two waves of a
+  // channel half when MT is odd (the mh = 1 wave's last slot would be pure padding) and the
+  // tile holds <= 16 positions (its partial sums: 8 registers per lane)
+  static constexpr bool SPLIT3 = (MT & 1) && RC - 32 * (MT - 1) <= 16 && MT >= 5;
   static constexpr int QI = (RC + 255) / 256;              // obs cells per thread
   static_assert(LDS <= 160 * 1024, "one env's planes + conv2 fragments must fit the CU's 160 KiB LDS");
 };
@@ -281,6 +286,7 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
   float* bias = reinterpret_cast<float*>(smem + G::BIAS);
   const float b3v = gbias[96 + 32 * nh + lr];
   if (tid < 160) bias[tid] = gbias[tid];
+  if (tid < 2) reinterpret_cast<int*>(smem + G::FLAG)[tid] = -1;
   for (int i = tid; i < G::ZERO_END / 16; i += 256) reinterpret_cast<uint4*>(smem)[i] = make_uint4(0u, 0u, 0u, 0u);
   if (tid < 16) {
     const int ci = tid >> 2, cj = tid & 3;
@@ -399,23 +405,16 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
     // ---- conv3: D[pos][32 ch of nh] = im2col(act2) . W3, then Y[cell][ch] += P . relu(D).
     // The wave's (tile, k-step) sequence is one unrolled stream: A fragments run through a
     // ring of kPre LDS reads in flight across tile boundaries, and a tile's pooling (VALU +
-    // 2 MFMAs) interleaves with the next tile's chain.  Tiles past MT (the shorter wave's
-    // last slot) have all-zero pool membership and add nothing.
+    // 2 MFMAs) interleaves with the next tile's chain.  With G::SPLIT3 (20 x 20: 12.5 tiles)
+    // the half-empty last tile MT - 1 is split by k-steps: mh = 0 runs its k-steps [0, 18)
+    // last, mh = 1 its k-steps [18, 36) first (in place of its all-padding slot MT) and hands
+    // the partial sums over through LDS, so both waves run 6.5 tiles instead of 7.  Without
+    // it, tiles past MT (the shorter wave's last slot) have all-zero pool membership.
     f32x16 Y = {};
     {
-      constexpr int NT2 = G::NT2, NQ = NT2 * kW3Steps, kPre = HEIST_CONV3_PRE;
-      const unsigned char* base[NT2];
-#pragma unroll
-      for (int i = 0; i < NT2; ++i)
-        base[i] = smem + G::A2 + pos_off<R, C, G::S2, G::PB2>(32 * (mh + 2 * i) + lr) - G::PB2 - G::S2 + 16 * h;
-      auto rd = [&](int q) {
-        const int s = q % kW3Steps, tap = s >> 2;
-        return *reinterpret_cast<const bf16x8*>(base[q / kW3Steps] + (tap / 3) * G::PB2 + (tap % 3) * G::S2 +
-                                                (s & 3) * 32);
-      };
-      bf16x8 ring[kPre];
-#pragma unroll
-      for (int q = 0; q < kPre; ++q) ring[q] = rd(q);
+      constexpr int NT2 = G::NT2, kPre = HEIST_CONV3_PRE;
+      constexpr bool SP = G::SPLIT3;
+      constexpr int KS = kW3Steps / 2;
       // software pipeline: tile i's pooling epilogue (ReLU + bias, bf16 packing, the two
       // pooling MFMAs) is spread over the first k-steps of tile i + 1's MFMA chain, one
       // element per MFMA gap, so it issues under the matrix core instead of stalling it
@@ -431,23 +430,78 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
         if (s == 16) Y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf[0], x[0], Y, 0, 0, 0);
         if (s == 17) Y = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf[1], x[1], Y, 0, 0, 0);
       };
+      // the split tile's partial sums (rows 0..15 = registers 0..7, 32 B per lane) pass
+      // through the act1 cell of position 32 nh + lr: a cell of the mh = 0 reader's own conv1
+      // tile, so nothing else writes it (act1's conv2 reads ended at B3) before the reader's
+      // next-env conv1 below.  FLAG[nh] = e marks it complete: a wave's LDS operations
+      // execute in order, so the volatile stores (kept in program order) suffice.
+      // (LDS-typed pointers: a volatile access through a generic one stays a flat access)
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
+      typedef __attribute__((address_space(3))) f32x2 lds_f32x2;
+      typedef __attribute__((address_space(3))) int lds_int;
+      lds_f32x2* stash = (lds_f32x2*)(smem + G::A1 + pos_off<R, C, G::S1, G::PB1>(32 * nh + lr) + 8 * h);
+      lds_int* flag = (lds_int*)(smem + G::FLAG) + nh;
+      auto stream = [&](auto mhc) {
+        constexpr int MH = decltype(mhc)::value;
+        constexpr bool ST = SP && MH == 1;  // segment 0: the split tile's k-steps [KS, 36), stashed
+        constexpr int L0 = ST ? kW3Steps - KS : kW3Steps;
+        constexpr int NQ = SP ? (NT2 - 1) * kW3Steps + (MH ? kW3Steps - KS : KS) : NT2 * kW3Steps;
+        const unsigned char* base[NT2];  // segment g's tile
 #pragma unroll
-      for (int i = 0; i < NT2; ++i) {
-        f32x16 acc = {};
-#pragma unroll
-        for (int s = 0; s < kW3Steps; ++s) {
-          const int q = i * kW3Steps + s;
-          const bf16x8 f = ring[q % kPre];
-          if (q + kPre < NQ) ring[q % kPre] = rd(q + kPre);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, in_agpr(w3[s]), acc, 0, 0, 0);
-          if (i > 0 && s < 18) pool_piece(i - 1, s);
+        for (int g = 0; g < NT2; ++g) {
+          const int t = MH == 0 ? 2 * g : (ST ? (g == 0 ? G::MT - 1 : 2 * g - 1) : 2 * g + 1);
+          base[g] = smem + G::A2 + pos_off<R, C, G::S2, G::PB2>(32 * t + lr) - G::PB2 - G::S2 + 16 * h;
         }
-        prev = acc;
-      }
-      __builtin_amdgcn_sched_group_barrier(0x100, kPre, 0);
-      sched_ring<kW3Steps, 0>(std::make_integer_sequence<int, NQ>{});
+        auto rd = [&](int q) {
+          const int g = q < L0 ? 0 : 1 + (q - L0) / kW3Steps;
+          const int s = q < L0 ? (ST ? KS : 0) + q : (q - L0) % kW3Steps, tap = s >> 2;
+          return *reinterpret_cast<const bf16x8*>(base[g] + (tap / 3) * G::PB2 + (tap % 3) * G::S2 + (s & 3) * 32);
+        };
+        auto epi = [&](int g, int j) {  // piece j of segment g's epilogue (prev holds its sums)
+          if (ST && g == 0) {
+            if (j < 4) *(volatile lds_f32x2*)(stash + 2 * j) = f32x2{prev[2 * j], prev[2 * j + 1]};
+            if (j == 4) *(volatile lds_int*)flag = e;
+          } else {
+            pool_piece(ST ? g - 1 : g, j);
+          }
+        };
+        bf16x8 ring[kPre];
 #pragma unroll
-      for (int s = 0; s < 18; ++s) pool_piece(NT2 - 1, s);  // the last tile's epilogue
+        for (int q = 0; q < kPre; ++q) ring[q] = rd(q);
+#pragma unroll
+        for (int g = 0; g < NT2; ++g) {
+          const int k0 = ST && g == 0 ? KS : 0;
+          const int k1 = SP && MH == 0 && g == NT2 - 1 ? KS : kW3Steps;
+          const int q0 = g == 0 ? 0 : L0 + (g - 1) * kW3Steps;
+          f32x16 acc = {};
+#pragma unroll
+          for (int s = k0; s < k1; ++s) {
+            const int q = q0 + s - k0;
+            const bf16x8 f = ring[q % kPre];
+            if (q + kPre < NQ) ring[q % kPre] = rd(q + kPre);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, in_agpr(w3[s]), acc, 0, 0, 0);
+            if (g > 0 && s - k0 < 18) epi(g - 1, s - k0);
+          }
+          prev = acc;
+        }
+        __builtin_amdgcn_sched_group_barrier(0x100, kPre, 0);
+        sched_ring<kW3Steps, 0>(std::make_integer_sequence<int, NQ>{});
+        if constexpr (SP && MH == 0) {  // the partner's k-steps of the split tile
+          while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != e) __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x2 v = stash[2 * j];
+            prev[2 * j] += v.x;
+            prev[2 * j + 1] += v.y;
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 18; ++s) epi(NT2 - 1, s);  // the last segment's epilogue
+      };
+      if (mh == 0)
+        stream(std::integral_constant<int, 0>{});
+      else
+        stream(std::integral_constant<int, 1>{});
       // conv1 of the next env (its input plane was staged before B3): all reads first,
       // then tile by tile (also after the last env: harmless)
       {

@@ -343,10 +343,13 @@ SOLVER_BACKBONE_FLOP = solver_backbone_flop(20)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
 
 
-def measure_policy(dev, n, iters=50, warmup=5, R=20):
+def measure_policy(dev, n, iters=50, warmup=5, R=20, settle_ms=100.0):
     """Batched Solver select_action on the fused kernels (heist_solver_features +
     heist_solver_head) and the backbone kernel alone, timed with HIP events.  R = 32 runs
-    the row-band backbone (BASELINE C5's grid)."""
+    the row-band backbone (BASELINE C5's grid).  Each timed form runs after an untimed
+    clock-settle phase of settle_ms (as time_env's): the setup before it leaves the GPU
+    idle, and a 4096-env backbone launch timed from idle measured 0.184-0.19 ms against
+    0.158 ms once the clock had ramped (profiles/r05az_backbone_sweep.log)."""
     from heist_amd.agents import SolverAgent
     ag = SolverAgent(R, R, device=dev, rollout_precision="bf16")
     net = ag.network
@@ -354,9 +357,19 @@ def measure_policy(dev, n, iters=50, warmup=5, R=20):
     h = c = torch.zeros(1, n, 128, device=dev)
     st = torch.cuda.current_stream(dev)
 
+    settle = {}
+
     def timed(fn):
         for _ in range(warmup):
             fn()
+        ts, k = time.perf_counter(), 0
+        while (time.perf_counter() - ts) * 1e3 < settle_ms:
+            fn()
+            k += 1
+            if k % 8 == 0:
+                torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)
+        settle[fn] = k
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(st)
         for _ in range(iters):
@@ -364,13 +377,15 @@ def measure_policy(dev, n, iters=50, warmup=5, R=20):
         b.record(st)
         torch.cuda.synchronize(dev)
         return a.elapsed_time(b) / iters
-    ms_bb = timed(lambda: net.features_fused(obs))
-    ms_act = timed(lambda: ag.act(obs, (h, c)))
+    f_bb, f_act = (lambda: net.features_fused(obs)), (lambda: ag.act(obs, (h, c)))
+    ms_bb = timed(f_bb)
+    ms_act = timed(f_act)
     tf = solver_backbone_flop(R) * n / (ms_bb * 1e-3) / 1e12
     kern = "heist::solver_conv_kernel<20,20>" if R == 20 else "heist::solver_conv_band_kernel<32,8>"
     return {"value": n / (ms_act * 1e-3), "unit": "env-steps/s", "ms_per_step": ms_act, "envs": n,
             "grid": "%dx%d" % (R, R), "dtype": "bf16 MFMA (fp32 accumulate)",
             "note": "batched SolverAgent.act: fused conv backbone + fc/LSTM/heads/sample kernels",
+            "clock_settle": {"ms": settle_ms, "act_calls": settle[f_act], "backbone_calls": settle[f_bb]},
             "backbone_roofline": {"bound": "mfma", "kernel": kern,
                                   "kernel_ms": ms_bb, "achieved": tf, "peak": MFMA_BF16_PEAK_TFLOPS,
                                   "unit": "TFLOP/s", "frac": tf / MFMA_BF16_PEAK_TFLOPS,

@@ -384,7 +384,12 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
     // (conv2_pass), so only the last pass's epilogue is exposed.
     {
       constexpr int NT2 = G::NT2;
+#ifdef HEIST_CONV2_SASB  // build-time A/B of the pass boundaries, e.g. -DHEIST_CONV2_SASB=3,6
+      constexpr int SASB[2] = {HEIST_CONV2_SASB};  // 20 x 20 (NT2 = 7) only
+      constexpr int SA = NT2 == 7 ? SASB[0] : (NT2 * 3 + 6) / 7, SB = NT2 == 7 ? SASB[1] : SA + (NT2 - SA + 1) / 2;
+#else
       constexpr int SA = (NT2 * 3 + 6) / 7, SB = SA + (NT2 - SA + 1) / 2;
+#endif
       constexpr int NA = SA, NB = SB - SA > 0 ? SB - SA : 1, NC = NT2 - SB > 0 ? NT2 - SB : 1;
       const bf16x8* wl = reinterpret_cast<const bf16x8*>(smem + G::W2) + nh * kW2Steps * 64 + l;
       float4 b2v[4];

@@ -259,6 +259,19 @@ constexpr int kStamps = 10;
       stamps[((size_t)blockIdx.x * 4 + w) * kStamps + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 
+// The conv2 fragments global -> LDS (2 x 18 x 64 uint4 = 9 per thread): all 9 loads in
+// flight before the first store.  As a rolled loop every store waited for its load
+// (vmcnt(0)): nine serial L2 round trips in every launch's prologue.
+__device__ __forceinline__ void copy_w2(unsigned char* dst, const uint4* __restrict__ packed, int tid) {
+  constexpr int kPer = 2 * kW2Steps * 64 / 256;
+  static_assert(kPer * 256 == 2 * kW2Steps * 64, "conv2 fragments split evenly over 256 threads");
+  uint4 t[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) t[k] = packed[kOffW2 + tid + 256 * k];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) reinterpret_cast<uint4*>(dst)[tid + 256 * k] = t[k];
+}
+
 template <int R, int C>
 __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __restrict__ obs, int n,
                                                              const uint4* __restrict__ packed,
@@ -271,6 +284,11 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
   const int w = tid >> 6, l = tid & 63, h = l >> 5, lr = l & 31;
   const int nh = w & 1, mh = w >> 1;
 
+  // the first env's observation in flight under the weight loads
+  float pre[G::QI][3];
+  int e = blockIdx.x;
+  if (e < n) load_obs<G>(obs, e, pre);
+
   // ---- weights -> registers (MFMA fragments), tables -> LDS
   bf16x8 w1[kW1Steps], w3[kW3Steps];
 #pragma unroll
@@ -280,8 +298,7 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
     w3[s] = __builtin_bit_cast(bf16x8, packed[kOffW3 + (nh * kW3Steps + s) * 64 + l]);
     in_agpr(w3[s]);
   }
-  for (int i = tid; i < 2 * kW2Steps * 64; i += 256)  // conv2 fragments: LDS, read once per k-step
-    reinterpret_cast<uint4*>(smem + G::W2)[i] = packed[kOffW2 + i];
+  copy_w2(smem + G::W2, packed, tid);  // conv2 fragments: LDS, read once per k-step
   const float* gbias = reinterpret_cast<const float*>(packed + kOffBias);
   float* bias = reinterpret_cast<float*>(smem + G::BIAS);
   const float b3v = gbias[96 + 32 * nh + lr];
@@ -335,9 +352,6 @@ __global__ __launch_bounds__(256, 1) void solver_conv_kernel(const float* __rest
     off1b[s] = ((tb / 3) * PC + (tb % 3)) * G::S0;
   }
 
-  float pre[G::QI][3];
-  int e = blockIdx.x;
-  if (e < n) load_obs<G>(obs, e, pre);
   __builtin_amdgcn_s_waitcnt(0);  // weights landed: no conservative vmcnt waits inside the loop
   __syncthreads();
 
@@ -669,8 +683,7 @@ __global__ __launch_bounds__(256, 1) void solver_conv_band_kernel(const float* _
     w3[s] = __builtin_bit_cast(bf16x8, packed[kOffW3 + (nh * kW3Steps + s) * 64 + l]);
     in_agpr(w3[s]);
   }
-  for (int i = tid; i < 2 * kW2Steps * 64; i += 256)
-    reinterpret_cast<uint4*>(smem + G::W2)[i] = packed[kOffW2 + i];
+  copy_w2(smem + G::W2, packed, tid);
   const float* gbias = reinterpret_cast<const float*>(packed + kOffBias);
   float* bias = reinterpret_cast<float*>(smem + G::BIAS);
   const float b3v = gbias[96 + 32 * nh + lr];

@@ -24,7 +24,10 @@
 extern "C" {
 #endif
 
-#define HEIST_ABI_VERSION 3  /* 2: heist_step_stamps takes the buffer size; heist_stamp_words; 3: heist_arch_update_* */
+/* 2: heist_step_stamps takes the buffer size; heist_stamp_words; 3: heist_arch_update_*;
+ * 4: heist_arch_update_status, the heist_*_nhwc training passes, heist_get_config's 15th word
+ *    (heist_step on the lean kernel), the heist_train_* fp32-MFMA training convolutions */
+#define HEIST_ABI_VERSION 4
 #define HEIST_EINVAL 100000
 
 /* status_out codes of heist_step (environment.py:236-297 info["status"]). */
@@ -75,6 +78,8 @@ int heist_reset(heist_t h, const uint8_t* mask, float* obs_out, heist_stream_t s
  *   actions [N] int64 in 0..4;  obs_out [N][3][R][C] float32;  reward_out [N] float32
  *   (the float64 reward rounded, as agents/solver.py:138 stores it); reward64_out [N]
  *   float64 or NULL; done_out [N] uint8; status_out [N] int8 (HEIST_* codes).
+ * Where the lean K-tick kernel serves the handle (20 x 20 at one wave per env, 32 x 32; no
+ * instrumentation armed) the tick runs as heist_step_multi with K = 1, bit-identical.
  * auto_reset != 0: an env that finishes this tick is reset in the same launch and its
  * obs row holds the reset observation (training.py:515-520 next attempt), while reward,
  * done and status describe the finishing tick.  auto_reset == 0: finished envs answer
@@ -137,10 +142,11 @@ int64_t heist_stamp_words(heist_t h, int which);
 int heist_step_waves(heist_t h);
 
 /* The handle's effective kernel configuration, no reference counterpart (what a benchmark
- * records next to its numbers): out[0..n) with n <= 14 receives step_waves, ray_chunk,
+ * records next to its numbers): out[0..n) with n <= 15 receives step_waves, ray_chunk,
  * step_occ, vis_gap, obs_store, ray_mode, probe_mode, dispatch_order, split_obs,
  * guard_cones, multi_waves, fan_on, lean, interval_fans (the HEIST_* environment knobs as heist_create resolved them,
- * then any heist_set_* calls).  probe_mode != 0 selects the profiling step kernel, whose results are
+ * then any heist_set_* calls), step_lean (1: heist_step currently runs as a one-tick
+ * heist_step_multi launch on the lean kernel; HEIST_STEP_LEAN=0 at heist_create turns it off).  probe_mode != 0 selects the profiling step kernel, whose results are
  * wrong by design (phases skipped). */
 int heist_get_config(heist_t h, int32_t* out, int n);
 
@@ -347,6 +353,40 @@ int heist_pool_relu_bwd_nhwc(const float* dfeat, const float* y, int n, int rows
                              float* partial, float* dbias_out, heist_stream_t stream);
 int heist_relu_bwd_nhwc(float* g, const float* y, int n, int positions, int channels, float* partial, float* dbias_out,
                         heist_stream_t stream);
+
+/* The Solver backbone's fp32 training convolutions on fp32 MFMA (v_mfma_f32_16x16x4_f32, exact
+ * fp32), for the PPO update's forward and backward (agents/solver.py:157-199 over
+ * networks.py:93-100): every pass of relu(conv1) -> relu(conv2) -> relu(conv3) -> pool as one
+ * persistent kernel with the weights in registers and the activation bands in LDS, replacing
+ * MIOpen's convolutions.  20 x 20 grids (heist_train_conv_supported).  Activations are
+ * [n][rows][cols][P] float32 with P = channels + 4 (the 4 pad words are never read), the
+ * network input [n][rows][cols][4] (heist_train_obs_nhwc4), all 16-byte aligned.
+ *   heist_train_conv_pack: torch weights [co][ci][3][3] of layer 1 (3 -> 32, mode 0), 2 (32 -> 64)
+ *     or 3 (64 -> 64) -> frag (heist_train_conv_frag_floats floats); mode 0 the forward
+ *     convolution, mode 1 its data gradient (transposed, flipped taps).
+ *   heist_train_conv: mode 0 y = relu(conv(x) + bias); mode 1 (layers 2, 3) y = (mask > 0) ?
+ *     conv_data_grad(x) : 0 with x the gradient at the layer's output (64 channels) and mask the
+ *     saved activation of the layer's input (threshold_backward).  queue: 2 device ints, zero
+ *     before the first launch (the kernels leave them zero); one pair per launch in flight.
+ *   heist_train_conv_wgrad: dw [co][ci][3][3] and db [co] of layer 1-3 from dy (the gradient at
+ *     the layer's pre-activation output) and x (its input); partial:
+ *     heist_train_conv_partial_floats(layer, n, ...) floats of scratch.  Sums in a fixed order.
+ *   heist_train_obs_nhwc4: obs [n][3][rows][cols] with element strides -> [n][rows][cols][4].
+ *   heist_train_pool: feat [n][1024] = adaptive_avg_pool2d(a3, (4, 4)) flattened C-major.
+ *   heist_train_pool_bwd: d3 = (a3 > 0) * the pool's input gradient of dfeat [n][1024]. */
+int heist_train_conv_supported(int rows, int cols);
+int heist_train_conv_frag_floats(int layer, int mode);
+int heist_train_conv_pack(int layer, int mode, const float* w, float* frag, heist_stream_t stream);
+int heist_train_conv(int layer, int mode, const float* x, int n, int rows, int cols, const float* frag,
+                     const float* bias, const float* mask, float* y, int* queue, heist_stream_t stream);
+int64_t heist_train_conv_partial_floats(int layer, int n, int rows, int cols);
+int heist_train_conv_wgrad(int layer, const float* dy, const float* x, int n, int rows, int cols, float* partial,
+                           float* dw, float* db, int* queue, heist_stream_t stream);
+int heist_train_obs_nhwc4(const float* obs, int n, int rows, int cols, int64_t stride_n, int64_t stride_c,
+                          int64_t stride_h, int64_t stride_w, float* x4, heist_stream_t stream);
+int heist_train_pool(const float* a3, int n, int rows, int cols, float* feat, heist_stream_t stream);
+int heist_train_pool_bwd(const float* dfeat, const float* a3, int n, int rows, int cols, float* d3,
+                         heist_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -68,6 +68,16 @@ int64_t arch_update_workspace_bytes();
 hipError_t launch_arch_update(float* const* p, float* const* m, float* const* v, const float* grid, int R, int C,
                               const float* target, int k, const float* adam_sc, float* vloss, void* ws, double beta1,
                               double beta2, double eps, double max_norm, double value_coeff, hipStream_t st);
+int train_conv_frag_floats(int layer, int mode);
+int64_t train_conv_partial_floats(int layer, int n, int R, int C);
+hipError_t launch_train_conv_pack(int layer, int mode, const float* w, float* frag, hipStream_t st);
+hipError_t launch_train_conv(int layer, int mode, const float* x, int n, int R, int C, const float* frag,
+                             const float* bias, const float* mask, float* y, int* queue, hipStream_t st);
+hipError_t launch_train_conv_wgrad(int layer, const float* dy, const float* x, int n, int R, int C, float* partial,
+                                   float* dw, float* db, int* queue, hipStream_t st);
+hipError_t launch_obs_nhwc4(const float* obs, int n, int R, int C, const int64_t* strides, float* x4, hipStream_t st);
+hipError_t launch_train_pool(const float* a3, int n, int R, int C, float* feat, hipStream_t st);
+hipError_t launch_train_pool_bwd(const float* dfeat, const float* a3, int n, int R, int C, float* d3, hipStream_t st);
 hipError_t launch_gae(const float* r, const float* v, const uint8_t* d, const float* last_value, int T, int N,
                       double gamma, double lam, float* adv, float* ret, hipStream_t st);
 hipError_t launch_adv_moments(const float* x, int64_t n, int phase, double* acc, hipStream_t st);
@@ -90,6 +100,8 @@ struct heist_env {
   bool fan_used;           // a K-tick launch has been issued on fan_stream
   hipEvent_t fan_done;     // recorded behind every K-tick launch: a refill on another stream waits for it
   int64_t stamp_words;     // size of the stamp buffer armed by heist_step_stamps (uint64 words)
+  int step_lean;           // 1 (default): heist_step runs as a one-tick heist_step_multi launch wherever the
+                           // lean K-tick kernel serves the handle (HEIST_STEP_LEAN=0: the single-tick kernel)
 };
 
 namespace {
@@ -145,6 +157,17 @@ std::vector<double> heading_table(int R, int C) {
       t[(size_t)(dr + R - 1) * (2 * C - 1) + (dc + C - 1)] = py_mod(a * rad_to_deg, 360.0);
     }
   return t;
+}
+
+// heist_step's one-tick heist_step_multi route applies: the lean kernel (step_lean_kernel) takes
+// the launch (launch_step_multi's lean20 / lean32 test) and no instrumentation is armed (the
+// step kernel's stamp and counter layouts differ from the K-tick kernel's)
+bool lean_serves(const heist_env* h) {
+  const EnvParams& p = h->p;
+  const bool lean20 = p.multi_waves == 1 && p.R == 20 && p.C == 20 && p.vis_gap == 1024;
+  const bool lean32 = p.R == 32 && p.C == 32 && p.vis_gap == 2048;
+  return h->step_lean && p.lean && (lean20 || lean32) && p.probe_mode == 0 && !p.sample_counter &&
+         !p.redo_counter && !p.stamps && p.max_cams + p.max_guards <= heist::kMaxEmitters;
 }
 
 }  // namespace
@@ -319,6 +342,8 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   if (const char* f = getenv("HEIST_INTERVAL_FANS")) p.interval_fans = atoi(f) ? 1 : 0;
   p.guard_cones = 1;
   if (const char* gc = getenv("HEIST_GUARD_CONES")) p.guard_cones = atoi(gc) ? 1 : 0;
+  h->step_lean = 1;
+  if (const char* f = getenv("HEIST_STEP_LEAN")) h->step_lean = atoi(f) ? 1 : 0;
   std::vector<double> hrad(heist::kHalfDegN);
   for (int m = 0; m < heist::kHalfDegN; ++m) hrad[m] = (0.5 * (m - heist::kHalfDegN / 2)) * heist::kDegToRad;
 
@@ -387,6 +412,9 @@ int heist_step(heist_t h, const int64_t* actions, float* obs_out, float* reward_
   if (int rc = check_handle(h)) return rc;
   HEIST_REQUIRE(actions && obs_out && reward_out && done_out && status_out, "heist_step: null output/input");
   HEIST_REQUIRE(!h->p.stamps || h->stamp_words >= heist_stamp_words(h, 0), "heist_step: stamp buffer too small");
+  if (lean_serves(h))  // the training rollout's tick on the lean kernel: heist_step_multi with K = 1 is
+    return heist_step_multi(h, 1, actions, obs_out, reward_out, reward64_out, done_out, status_out, auto_reset,
+                            stream);  // bit-identical by the heist_step_multi contract (heist.h)
   h->fan_pos = -1;  // headings advanced outside the K-tick launches' accounting
   return check_hip(heist::launch_step(h->p, actions, obs_out, reward_out, reward64_out, done_out, status_out,
                                       auto_reset, (hipStream_t)stream),
@@ -486,11 +514,11 @@ int heist_step_waves(heist_t h) {
 
 int heist_get_config(heist_t h, int32_t* out, int n) {
   if (int rc = check_handle(h)) return rc;
-  HEIST_REQUIRE(out != nullptr && n >= 0 && n <= 14, "heist_get_config: need out != NULL and 0 <= n <= 14");
+  HEIST_REQUIRE(out != nullptr && n >= 0 && n <= 15, "heist_get_config: need out != NULL and 0 <= n <= 15");
   const EnvParams& p = h->p;
-  const int32_t v[14] = {p.step_waves, p.ray_chunk,  p.step_occ,       p.vis_gap,   p.obs_store,  p.ray_mode,
+  const int32_t v[15] = {p.step_waves, p.ray_chunk,  p.step_occ,       p.vis_gap,   p.obs_store,  p.ray_mode,
                          p.probe_mode, p.dispatch_order, p.split_obs, p.guard_cones, p.multi_waves, p.fan_on,
-                         p.lean,       p.interval_fans};
+                         p.lean,       p.interval_fans,  lean_serves(h) ? 1 : 0};
   for (int k = 0; k < n; ++k) out[k] = v[k];
   return 0;
 }
@@ -780,6 +808,78 @@ int heist_relu_bwd_nhwc(float* g, const float* y, int n, int positions, int chan
                 "heist_relu_bwd_nhwc: 16-byte alignment");
   return check_hip(heist::launch_relu_bwd(g, y, n, positions, channels, partial, dbias_out, (hipStream_t)stream),
                    "heist_relu_bwd_nhwc");
+}
+
+int heist_train_conv_supported(int rows, int cols) { return rows == 20 && cols == 20 ? 1 : 0; }
+
+int heist_train_conv_frag_floats(int layer, int mode) {
+  if (!((layer == 1 && mode == 0) || ((layer == 2 || layer == 3) && (mode == 0 || mode == 1)))) return -1;
+  return heist::train_conv_frag_floats(layer, mode);
+}
+
+int heist_train_conv_pack(int layer, int mode, const float* w, float* frag, heist_stream_t stream) {
+  HEIST_REQUIRE(w && frag, "heist_train_conv_pack: null pointer");
+  HEIST_REQUIRE(heist_train_conv_frag_floats(layer, mode) > 0, "heist_train_conv_pack: layer 1 (mode 0), 2 or 3");
+  return check_hip(heist::launch_train_conv_pack(layer, mode, w, frag, (hipStream_t)stream), "heist_train_conv_pack");
+}
+
+int heist_train_conv(int layer, int mode, const float* x, int n, int rows, int cols, const float* frag,
+                     const float* bias, const float* mask, float* y, int* queue, heist_stream_t stream) {
+  HEIST_REQUIRE(heist_train_conv_supported(rows, cols), "heist_train_conv: grid must be 20x20");
+  HEIST_REQUIRE(heist_train_conv_frag_floats(layer, mode) > 0, "heist_train_conv: layer 1 (mode 0), 2 or 3");
+  HEIST_REQUIRE(n >= 0, "heist_train_conv: n < 0");
+  HEIST_REQUIRE(x && frag && y && queue, "heist_train_conv: null pointer");
+  HEIST_REQUIRE(mode == 0 ? bias != nullptr : mask != nullptr, "heist_train_conv: mode 0 needs bias, mode 1 mask");
+  for (const void* p : {(const void*)x, (const void*)frag, (const void*)y, mode ? (const void*)mask : (const void*)bias})
+    HEIST_REQUIRE(((uintptr_t)p & 15) == 0, "heist_train_conv: 16-byte alignment");
+  if (n == 0) return 0;
+  return check_hip(heist::launch_train_conv(layer, mode, x, n, rows, cols, frag, bias, mask, y, queue,
+                                            (hipStream_t)stream),
+                   "heist_train_conv");
+}
+
+int64_t heist_train_conv_partial_floats(int layer, int n, int rows, int cols) {
+  return heist::train_conv_partial_floats(layer, n, rows, cols);
+}
+
+int heist_train_conv_wgrad(int layer, const float* dy, const float* x, int n, int rows, int cols, float* partial,
+                           float* dw, float* db, int* queue, heist_stream_t stream) {
+  HEIST_REQUIRE(heist_train_conv_supported(rows, cols), "heist_train_conv_wgrad: grid must be 20x20");
+  HEIST_REQUIRE(layer >= 1 && layer <= 3, "heist_train_conv_wgrad: layer 1, 2 or 3");
+  HEIST_REQUIRE(n >= 1, "heist_train_conv_wgrad: n < 1");
+  HEIST_REQUIRE(dy && x && partial && dw && db && queue, "heist_train_conv_wgrad: null pointer");
+  HEIST_REQUIRE(((uintptr_t)dy & 15) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)partial & 15) == 0,
+                "heist_train_conv_wgrad: 16-byte alignment");
+  return check_hip(heist::launch_train_conv_wgrad(layer, dy, x, n, rows, cols, partial, dw, db, queue,
+                                                  (hipStream_t)stream),
+                   "heist_train_conv_wgrad");
+}
+
+int heist_train_obs_nhwc4(const float* obs, int n, int rows, int cols, int64_t stride_n, int64_t stride_c,
+                          int64_t stride_h, int64_t stride_w, float* x4, heist_stream_t stream) {
+  HEIST_REQUIRE(obs && x4, "heist_train_obs_nhwc4: null pointer");
+  HEIST_REQUIRE(n >= 0 && rows >= 1 && cols >= 1, "heist_train_obs_nhwc4: bad sizes");
+  HEIST_REQUIRE(((uintptr_t)x4 & 15) == 0, "heist_train_obs_nhwc4: 16-byte alignment");
+  if (n == 0) return 0;
+  const int64_t st4[4] = {stride_n, stride_c, stride_h, stride_w};
+  return check_hip(heist::launch_obs_nhwc4(obs, n, rows, cols, st4, x4, (hipStream_t)stream), "heist_train_obs_nhwc4");
+}
+
+int heist_train_pool(const float* a3, int n, int rows, int cols, float* feat, heist_stream_t stream) {
+  HEIST_REQUIRE(a3 && feat, "heist_train_pool: null pointer");
+  HEIST_REQUIRE(n >= 0 && rows >= 4 && cols >= 4, "heist_train_pool: bad sizes");
+  if (n == 0) return 0;
+  return check_hip(heist::launch_train_pool(a3, n, rows, cols, feat, (hipStream_t)stream), "heist_train_pool");
+}
+
+int heist_train_pool_bwd(const float* dfeat, const float* a3, int n, int rows, int cols, float* d3,
+                         heist_stream_t stream) {
+  HEIST_REQUIRE(dfeat && a3 && d3, "heist_train_pool_bwd: null pointer");
+  HEIST_REQUIRE(n >= 0 && rows >= 4 && cols >= 4, "heist_train_pool_bwd: bad sizes");
+  HEIST_REQUIRE(((uintptr_t)a3 & 15) == 0 && ((uintptr_t)d3 & 15) == 0, "heist_train_pool_bwd: 16-byte alignment");
+  if (n == 0) return 0;
+  return check_hip(heist::launch_train_pool_bwd(dfeat, a3, n, rows, cols, d3, (hipStream_t)stream),
+                   "heist_train_pool_bwd");
 }
 
 int heist_solver_stamps(uint64_t* buf) {

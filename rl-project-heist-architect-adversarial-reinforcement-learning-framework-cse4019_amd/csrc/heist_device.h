@@ -144,8 +144,9 @@ struct EnvParams {
   const double* half_deg;      // [2][kHalfDegN] glibc-exact sin, cos of m/2 degrees (m = -1440 .. 1439)
   int32_t* order;              // [n_envs] env of step/reset block b: heaviest raycast first (order_kernel)
   int split_obs;               // 1 (default): step writes obs channels 0/2 before the raycast (HEIST_SPLIT_OBS)
-  int dispatch_order;          // 1: step/reset block b runs env order[b] (heaviest first); 2 (default): the
-                               // same ranks snake-drafted over the SIMDs (order_kernel); 0: env b (HEIST_DISPATCH_ORDER)
+  int dispatch_order;          // 1 (default): step/reset block b runs env order[b] (heaviest first); 2 (opt-in,
+                               // HEIST_DISPATCH_ORDER=2, measured and not kept): the same ranks snake-drafted over
+                               // the SIMDs (order_kernel); 0: env b
   int n_cu;                    // compute units of the device (the snake draft's SIMD count / 4)
   int prio_mode;               // K-tick lean kernel wave priority by cost rank (order_kernel; HEIST_PRIO_MODE)
   unsigned long long* stamps;          // optional [n_envs][waves][8]: step-kernel phase stamps (s_memtime), else null

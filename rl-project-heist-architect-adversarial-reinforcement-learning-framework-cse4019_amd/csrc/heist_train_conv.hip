@@ -1,0 +1,689 @@
+// heist_train_conv.hip -- the Solver backbone's fp32 training convolutions on fp32 MFMA.
+//
+// The PPO update (agents/solver.py:157-199) runs SolverNetwork.features (networks.py:93-100:
+// relu(conv1) -> relu(conv2) -> relu(conv3) -> AdaptiveAvgPool2d(4, 4), 3 -> 32 -> 64 -> 64
+// channels, 3 x 3, pad 1) forward and backward on 16,384-sample minibatches: ~2.2 TFLOP per
+// optimizer step, all of it in six convolution passes that MIOpen ran at 0.39-0.70 of the
+// 157 TF fp32 matrix peak (profiles/r05f_train_kernel_stats.csv).  Here every pass is one
+// persistent kernel on v_mfma_f32_16x16x4_f32 -- exact fp32: each MFMA is a k-ordered chain
+// of fmaf (cdna_hip_programming.md, 'FP32-input MFMA'), so results differ from MIOpen's or
+// the CPU's only by the order of the fp32 sums.
+//
+// Layout.  Activations are [n][R][C][P] fp32 with P = channels + 4 (channels 0..P-5 are
+// data, the 4 pad words are never read): a band of image rows is then one contiguous HBM
+// range that LDS-DMA (global_load_lds_dwordx4) copies straight into a padded LDS image whose
+// 16-byte reads are bank-conflict free (16 lanes at a 272- or 144-byte position pitch cover
+// all 64 banks).  The network input (3 channels) is [n][R][C][4], channel 3 zero.
+//
+// Work.  A unit is a BAND: 4 output rows of one sample (4C positions = C/4 tiles of 16).  The
+// kernels are persistent (one 512-thread workgroup per CU) and draw units from an atomic
+// queue, so a kernel that shares the chip with another (the Architect's update kernel holds
+// 64 CUs beside the Solver's update, training.py) keeps every CU it gets busy; every output
+// element is computed by exactly one wave, so results do not depend on the scheduling.
+//
+//  conv_a_kernel  (forward and data gradient: a 3 x 3 convolution with register weights)
+//    D[co][pos] = sum over (tap, ci) of W[co][tap][ci] * X[pos + tap][ci]: the weights are the
+//    MFMA's A operand, held in VGPRs for the whole kernel (144 per lane at 64 -> 64), the
+//    activations its B operand, one ds_read_b128 feeding 4 MFMA k-steps.  Wave w owns one
+//    16-channel output tile of one band of the unit for all its C/4 position tiles.  Epilogue:
+//    forward  y = relu(D + bias) (torch: conv + b rounded, then max(., 0));
+//    backward d = (a > 0) ? D : 0 with a the saved activation of the layer below (threshold_
+//             backward on the saved output), the data gradient being the convolution with the
+//             transposed, flipped weights (packed by conv_pack_kernel).
+//  conv_w_kernel  (weight and bias gradient)
+//    dW[co][tap][ci] = sum over samples and positions of dY[pos][co] * X[pos + tap][ci], and
+//    db[co] = sum of dY[pos][co] (one more MFMA tile whose B operand is 1.0): positions are
+//    the MFMA's k (4 per k-step), each wave accumulates one 16-channel row tile of dW over a
+//    CHUNK of 40 bands in registers and writes it as that chunk's partial; conv_w_reduce
+//    sums the partials in chunk order (deterministic, no float atomics).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#pragma clang fp contract(off)
+
+namespace heist {
+namespace tc {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+constexpr int kThreads = 512;  // 8 waves, 2 per SIMD
+constexpr int kChunkBands = 40;  // bands per weight-gradient partial (8 samples of 20 rows)
+
+template <int CH>
+struct Pitch {
+  static constexpr int v = CH == 4 ? 4 : CH + 4;
+};
+
+// LDS-DMA of 16 bytes per active lane: lane i's bytes land at lds_dst + 16 i (M0 holds the
+// wave-uniform base; set and restored inside the statement).  Waited for with an explicit
+// s_waitcnt vmcnt(0) before the barrier that publishes the buffer.
+__device__ __forceinline__ void lds_dma16(const void* gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+
+__device__ __forceinline__ void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
+
+typedef __attribute__((address_space(3))) float lds_float;
+typedef __attribute__((address_space(3))) f4 lds_f4_t;
+typedef __attribute__((address_space(3))) f2 lds_f2_t;
+
+// LDS reads through address-space-3 pointers (ds_read_*): a generic pointer that the compiler
+// cannot prove is LDS becomes a flat load (both counters, the slower path)
+__device__ __forceinline__ const lds_float* as_lds(const float* p) {
+  return reinterpret_cast<const lds_float*>((uint32_t)(uintptr_t)p);
+}
+__device__ __forceinline__ f4 lds_f4(const float* base, int off) { return *reinterpret_cast<const lds_f4_t*>(as_lds(base) + off); }
+__device__ __forceinline__ float lds_f1(const float* base, int off) { return as_lds(base)[off]; }
+__device__ __forceinline__ f2 lds_f2(const float* base, int off) {
+  return *reinterpret_cast<const lds_f2_t*>(as_lds(base) + off);
+}
+
+__device__ __forceinline__ f4 mfma(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+// Copy `bytes` (a multiple of 16) from global src to LDS dst, wave-instruction pieces of
+// 1 KB handed round-robin over the workgroup's waves starting at wave `w0` (wave-uniform).
+__device__ __forceinline__ void dma_range(const float* src, float* dst, int bytes, int piece0, int wid, int lane) {
+  const int pieces = (bytes + 1023) >> 10;
+  for (int k = (wid - piece0 % 8 + 8) % 8; k < pieces; k += 8) {
+    const int off = (k << 10) + (lane << 4);
+    if (off < bytes)
+      lds_dma16(reinterpret_cast<const char*>(src) + off,
+                (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds_addr(dst) + (uint32_t)(k << 10))));
+  }
+}
+
+// The work queue's exit: the last workgroup to leave resets both counters (queue[0] units
+// drawn, queue[1] workgroups done), so the next launch on the stream finds them zero.
+__device__ __forceinline__ void queue_exit(int* queue) {
+  if (threadIdx.x == 0 && atomicAdd(queue + 1, 1) == (int)gridDim.x - 1) {
+    atomicExch(queue, 0);
+    atomicExch(queue + 1, 0);
+  }
+}
+
+__device__ __forceinline__ void zero_range(float* dst, int bytes, int wid, int lane) {
+  for (int off = (wid * 64 + lane) * 16; off < bytes; off += kThreads * 16)
+    *reinterpret_cast<f4*>(reinterpret_cast<char*>(dst) + off) = f4{0.f, 0.f, 0.f, 0.f};
+}
+
+// Input band image of band gb (sample gb / NB, output rows 4(gb % NB) .. +3) into LDS
+// `img` [6][C + 2][PI]: padded row rr <- image row y0 - 1 + rr, interior columns only (the
+// two border columns were zeroed once); rows outside the image are zeroed.
+template <int CI, int R, int C>
+__device__ __forceinline__ void load_band(const float* x, float* img, int gb, int piece0, int wid, int lane) {
+  constexpr int PI = Pitch<CI>::v, RP = C + 2, NB = R / 4, ROWB = C * PI * 4;
+  const int smp = gb / NB, y0 = (gb % NB) * 4;
+#pragma unroll
+  for (int rr = 0; rr < 6; ++rr) {
+    const int y = y0 - 1 + rr;
+    float* dst = img + (rr * RP + 1) * PI;
+    if (y >= 0 && y < R)
+      dma_range(x + ((size_t)smp * R + y) * C * PI, dst, ROWB, piece0 + rr * ((ROWB + 1023) >> 10), wid, lane);
+    else
+      zero_range(dst, ROWB, wid, lane);
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// conv_a_kernel: y[p][co] = epilogue(sum_{tap, ci} W[co][tap][ci] x[p + tap][ci]).
+//   CI, CO input / output channels; S: the k (input channel) range split over S waves whose
+//   partial tiles are summed through LDS (S = 2 for 32 output channels, so that 8 waves have
+//   work); MODE 0 forward (bias, ReLU), 1 data gradient (mask by the saved activation > 0).
+struct ConvAArgs {
+  const float* x;       // [n][R][C][PI]
+  const float* frag;    // packed weights (conv_pack_kernel)
+  const float* bias;    // [CO] (MODE 0)
+  const float* mask;    // [n][R][C][PO] (MODE 1)
+  float* y;             // [n][R][C][PO]
+  int* queue;           // [2]: units drawn, workgroups done (zero between launches: queue_exit)
+  int n;
+};
+
+template <int CI, int CO, int S, int MODE, int R, int C>
+struct ConvAGeom {
+  static constexpr int PI = Pitch<CI>::v, PO = Pitch<CO>::v, NCT = CO / 16, BPU = 8 / (NCT * S);
+  static constexpr int PT = C / 4, RP = C + 2, NB = R / 4;
+  static constexpr int BAND_F = 6 * RP * PI, BUF_F = BPU * BAND_F;
+  static constexpr int KBW = CI == 4 ? 1 : (CI / 16) / S;  // 16-channel blocks per tap of a wave
+  static constexpr int NWR = CI == 4 ? 9 : 36 * KBW;       // weight registers per lane
+  static constexpr int LDS = 2 * BUF_F * 4 + 64;
+  static_assert(NCT * S * BPU == 8, "8 waves");
+  static_assert(C % 4 == 0 && R % 4 == 0, "bands of 4 rows, tiles of 16 positions");
+  static_assert(S == 1 || (PT * 256 <= C * PI && BPU * NCT <= 6), "a wave's k-split partials fit in a row interior");
+};
+
+template <int CI, int CO, int S, int MODE, int R, int C>
+__global__ __launch_bounds__(kThreads, 1) void conv_a_kernel(ConvAArgs a) {
+  using G = ConvAGeom<CI, CO, S, MODE, R, C>;
+  constexpr int PI = G::PI, PO = G::PO, NCT = G::NCT, BPU = G::BPU, PT = G::PT, RP = G::RP, NB = G::NB;
+  constexpr int KBW = G::KBW, NWR = G::NWR;
+  extern __shared__ f4 smem4[];
+  float* smem = reinterpret_cast<float*>(smem4);
+  float* buf[2] = {smem, smem + G::BUF_F};
+  int* slot = reinterpret_cast<int*>(smem + 2 * G::BUF_F);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c = wid % NCT, s = (wid / NCT) % S, bslot = wid / (NCT * S);
+  const int j = lane & 15, g = lane >> 4;
+  const int nbands = a.n * NB, nunits = (nbands + BPU - 1) / BPU;
+
+  // weights: lane (row i = j, k group g) of output tile c, k range s
+  float w[NWR];
+  {
+    const f4* wf = reinterpret_cast<const f4*>(a.frag) + (size_t)(c * S + s) * (NWR / 4 > 0 ? NWR / 4 : 1) * 64;
+    if constexpr (CI == 4) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t) w[t] = a.frag[(size_t)(c * 9 + t) * 64 + lane];
+    } else {
+#pragma unroll
+      for (int q = 0; q < NWR / 4; ++q) {
+        const f4 v = wf[q * 64 + lane];
+        w[4 * q] = v[0];
+        w[4 * q + 1] = v[1];
+        w[4 * q + 2] = v[2];
+        w[4 * q + 3] = v[3];
+      }
+    }
+  }
+  f4 bias4 = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (MODE == 0) bias4 = *reinterpret_cast<const f4*>(a.bias + 16 * c + 4 * g);
+
+  zero_range(smem, 2 * G::BUF_F * 4, wid, lane);  // border columns stay zero for the whole kernel
+  if (tid == 0) {
+    slot[0] = atomicAdd(a.queue, 1);
+    slot[1] = atomicAdd(a.queue, 1);
+  }
+  __syncthreads();
+  int cur = slot[0], nxt = slot[1];
+  auto issue = [&](int u, float* img0) {
+    for (int bb = 0; bb < BPU; ++bb) {
+      const int gb = u * BPU + bb;
+      if (gb < nbands) load_band<CI, R, C>(a.x, img0 + bb * G::BAND_F, gb, bb * 7, wid, lane);
+    }
+  };
+  if (cur < nunits) issue(cur, buf[0]);
+  // per-lane LDS offsets of the position tiles (tap (0, 0) corner, channel group g)
+  int pbase[PT];
+#pragma unroll
+  for (int t = 0; t < PT; ++t) {
+    const int q = 16 * t + j, y = q / C, xx = q % C;
+    pbase[t] = (y * RP + xx) * PI + (CI == 4 ? g : 4 * g + 16 * KBW * s);
+  }
+  for (int it = 0; cur < nunits; ++it) {
+    float* img = buf[it & 1] + bslot * G::BAND_F;
+    wait_dma();
+    __syncthreads();  // the unit's images are in LDS; everyone is done with the other buffer
+    if (nxt < nunits) issue(nxt, buf[(it + 1) & 1]);
+    if (tid == 0) slot[2 + (it & 1)] = atomicAdd(a.queue, 1);
+    const int gb = cur * BPU + bslot;
+    f4 acc[PT];
+#pragma unroll
+    for (int t = 0; t < PT; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+    if (gb < nbands) {
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int toff = ((tap / 3) * RP + tap % 3) * PI;
+        if constexpr (CI == 4) {
+          float xv[PT];
+#pragma unroll
+          for (int t = 0; t < PT; ++t) xv[t] = lds_f1(img, pbase[t] + toff);
+#pragma unroll
+          for (int t = 0; t < PT; ++t) acc[t] = mfma(w[tap], xv[t], acc[t]);
+        } else {
+#pragma unroll
+          for (int cb = 0; cb < KBW; ++cb) {
+            f4 xv[PT];
+#pragma unroll
+            for (int t = 0; t < PT; ++t) xv[t] = lds_f4(img, pbase[t] + toff + 16 * cb);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+#pragma unroll
+              for (int t = 0; t < PT; ++t) acc[t] = mfma(w[(tap * KBW + cb) * 4 + e], xv[t][e], acc[t]);
+          }
+        }
+      }
+    }
+    if constexpr (S == 2) {  // k halves: wave s = 1 hands its partial tiles to wave s = 0 through LDS
+      __syncthreads();       // every wave is done reading this unit's images
+      // the partials go to the interior of image row (band slot, c) of this buffer: the two
+      // border columns of every row stay zero for the rest of the kernel (the next images are
+      // DMA'd / zeroed over the interiors only)
+      float* part = buf[it & 1] + ((bslot * NCT + c) * RP + 1) * PI;
+      if (s == 1)
+#pragma unroll
+        for (int t = 0; t < PT; ++t) *reinterpret_cast<f4*>(part + t * 256 + lane * 4) = acc[t];
+      __syncthreads();
+      if (s == 0)
+#pragma unroll
+        for (int t = 0; t < PT; ++t) acc[t] += lds_f4(part, t * 256 + lane * 4);
+    }
+    if (s == 0 && gb < nbands) {
+      const int smp = gb / NB, y0 = (gb % NB) * 4;
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {
+        const int q = 16 * t + j, y = y0 + q / C, xx = q % C;
+        const size_t o = (((size_t)smp * R + y) * C + xx) * PO + 16 * c + 4 * g;
+        f4 v = acc[t];
+        if constexpr (MODE == 0) {
+          v += bias4;  // conv + b rounded once, then ReLU
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+        } else {
+          const f4 m = *reinterpret_cast<const f4*>(a.mask + o);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = m[r] > 0.f ? v[r] : 0.f;
+        }
+        *reinterpret_cast<f4*>(a.y + o) = v;
+      }
+    }
+    __syncthreads();  // slot written; this buffer free for the unit after next
+    cur = nxt;
+    nxt = slot[2 + (it & 1)];
+  }
+  queue_exit(a.queue);
+}
+
+// ---------------------------------------------------------------------------------------
+// conv_w_kernel: weight and bias gradient partials per chunk of kChunkBands bands.
+//   dY [n][R][C][PD] (PD = CO + 4), X [n][R][C][PI]; partial [chunk][WSZ] floats.
+//   CI >= 32: wave (m = row tile, h) holds tiles (tap, q) with the wave's QW input channels per
+//   lane j: ci = (CI / 16) j + QW h + qq (one ds_read of QW words per tap); CI == 4: wave
+//   (m, h < 3) holds column tile h of the 36 (tap, ci) pairs, h == 3 the bias tile.
+struct ConvWArgs {
+  const float* dy;
+  const float* x;
+  float* partial;
+  int* queue;
+  int n;
+};
+
+template <int CI, int CO, int R, int C>
+struct ConvWGeom {
+  static constexpr int PI = Pitch<CI>::v, PD = Pitch<CO>::v, MT = CO / 16, WPM = 8 / MT;
+  static constexpr int RP = C + 2, NB = R / 4, KS = C;  // k-steps (4 positions each) per band
+  static constexpr int XB_F = 6 * RP * PI, DB_F = 4 * C * PD, BUF_F = XB_F + DB_F;
+  static constexpr int QW = CI == 4 ? 1 : (CI / 16) / WPM;   // input channels per lane per tap
+  static constexpr int NTW = CI == 4 ? 1 : 9 * QW;           // column tiles per wave
+  static constexpr int NT_ALL = CI == 4 ? 3 : 9 * (CI / 16); // column tiles per row tile
+  static constexpr int WSZ = MT * NT_ALL * 256 + CO;         // partial floats per chunk
+  static constexpr int LDS = 2 * BUF_F * 4 + 64;
+  static_assert(CI == 4 ? WPM == 4 : (CI / 16) % WPM == 0, "wave split");
+};
+
+template <int CI, int CO, int R, int C>
+__global__ __launch_bounds__(kThreads, 1) void conv_w_kernel(ConvWArgs a) {
+  using G = ConvWGeom<CI, CO, R, C>;
+  constexpr int PI = G::PI, PD = G::PD, MT = G::MT, RP = G::RP, NB = G::NB, QW = G::QW, NTW = G::NTW;
+  extern __shared__ f4 smem4[];
+  float* smem = reinterpret_cast<float*>(smem4);
+  float* buf[2] = {smem, smem + G::BUF_F};
+  int* slot = reinterpret_cast<int*>(smem + 2 * G::BUF_F);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int m = wid % MT, h = wid / MT;
+  const int j = lane & 15, g = lane >> 4;
+  const int nbands = a.n * NB, nchunks = (nbands + kChunkBands - 1) / kChunkBands;
+  const bool has_bias = CI == 4 ? h == 3 : h == 0;
+  const bool has_cols = CI == 4 ? h < 3 : true;
+
+  // column offsets of this lane for the CI == 4 layout: column jj = 16 h + j <-> (tap, ci)
+  int coff = 0;
+  bool cval = true;
+  if constexpr (CI == 4) {
+    const int jj = 16 * (h < 3 ? h : 0) + j, tap = jj / 4, ci = jj % 4;
+    cval = jj < 36;
+    coff = cval ? ((tap / 3) * RP + tap % 3) * PI + ci : 0;
+  }
+  f4 acc[NTW];
+  f4 accb = {0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int gb, float* b0) {
+    if (gb >= nbands) return;
+    load_band<CI, R, C>(a.x, b0, gb, 0, wid, lane);
+    const int smp = gb / NB, y0 = (gb % NB) * 4;
+    dma_range(a.dy + ((size_t)smp * R + y0) * C * PD, b0 + G::XB_F, G::DB_F * 4, 5, wid, lane);
+  };
+  if (tid == 0) {
+    slot[0] = atomicAdd(a.queue, 1);
+    slot[1] = atomicAdd(a.queue, 1);
+  }
+  // zero both buffers (the X images' border columns stay zero) before any DMA lands
+  zero_range(smem, 2 * G::BUF_F * 4, wid, lane);
+  __syncthreads();
+  int chunk = slot[0], nchunk = slot[1];
+  if (chunk < nchunks) issue(chunk * kChunkBands, buf[0]);
+  int it = 0;
+  while (chunk < nchunks) {
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+    accb = f4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < kChunkBands; ++i, ++it) {
+      const int gb = chunk * kChunkBands + i;
+      float* xi = buf[it & 1];
+      const float* di = xi + G::XB_F;
+      wait_dma();
+      __syncthreads();
+      // next band: this chunk's, or the first of the next chunk (whose id was drawn ahead)
+      if (i + 1 < kChunkBands) {
+        issue(gb + 1, buf[(it + 1) & 1]);
+      } else {
+        if (nchunk < nchunks) issue(nchunk * kChunkBands, buf[(it + 1) & 1]);
+        if (tid == 0) slot[2] = atomicAdd(a.queue, 1);
+      }
+      if (gb < nbands) {
+        for (int ks = 0; ks < G::KS; ++ks) {
+          // positions 4 ks + g: one image row y (C % 4 == 0), column xx
+          const int q = 4 * ks + g, y = q / C, xx = q % C;
+          const float av = lds_f1(di, q * PD + 16 * m + j);
+          const int xb = (y * RP + xx) * PI;
+          if (has_cols) {
+            if constexpr (CI == 4) {
+              const float bv = cval ? lds_f1(xi, xb + coff) : 0.f;
+              acc[0] = mfma(av, bv, acc[0]);
+            } else {
+#pragma unroll
+              for (int tap = 0; tap < 9; ++tap) {
+                const int o = xb + ((tap / 3) * RP + tap % 3) * PI + (CI / 16) * j + QW * h;
+                if constexpr (QW == 2) {
+                  const f2 bv = lds_f2(xi, o);
+                  acc[tap * 2] = mfma(av, bv[0], acc[tap * 2]);
+                  acc[tap * 2 + 1] = mfma(av, bv[1], acc[tap * 2 + 1]);
+                } else {
+                  acc[tap] = mfma(av, lds_f1(xi, o), acc[tap]);
+                }
+              }
+            }
+          }
+          if (has_bias) accb = mfma(av, 1.0f, accb);
+        }
+      }
+      if (i + 1 == kChunkBands) {
+        __syncthreads();  // slot[2] visible
+      }
+    }
+    // this chunk's partial: tiles [m][tap][nq][lane][4], then the bias [CO]
+    float* p = a.partial + (size_t)chunk * G::WSZ;
+    if (has_cols) {
+      if constexpr (CI == 4) {
+        *reinterpret_cast<f4*>(p + ((size_t)m * 3 + h) * 256 + lane * 4) = acc[0];
+      } else {
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+          for (int qq = 0; qq < QW; ++qq)
+            *reinterpret_cast<f4*>(p + (((size_t)m * 9 + tap) * (CI / 16) + QW * h + qq) * 256 + lane * 4) =
+                acc[tap * QW + qq];
+      }
+    }
+    if (has_bias && j == 0) *reinterpret_cast<f4*>(p + MT * G::NT_ALL * 256 + 16 * m + 4 * g) = accb;
+    chunk = nchunk;
+    nchunk = slot[2];
+  }
+  queue_exit(a.queue);
+}
+
+// dW (torch layout [CO][CI_real][3][3]) and db [CO] = the partials summed in chunk order.
+template <int CI, int CO, int R, int C>
+__global__ __launch_bounds__(256) void conv_w_reduce_kernel(const float* __restrict__ partial, int nchunks, int ci_real,
+                                                            float* __restrict__ dw, float* __restrict__ db) {
+  using G = ConvWGeom<CI, CO, R, C>;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= G::WSZ) return;
+  float sum = 0.f;
+  for (int k = 0; k < nchunks; ++k) sum += partial[(size_t)k * G::WSZ + e];
+  const int tiles = G::MT * G::NT_ALL * 256;
+  if (e >= tiles) {
+    db[e - tiles] = sum;
+    return;
+  }
+  const int r = e & 3, lane = (e >> 2) & 63, tile = e >> 8, j = lane & 15, g = lane >> 4;
+  if constexpr (CI == 4) {
+    const int m = tile / 3, h = tile % 3, jj = 16 * h + j, tap = jj / 4, ci = jj % 4;
+    if (jj < 36 && ci < ci_real) dw[((size_t)(16 * m + 4 * g + r) * ci_real + ci) * 9 + tap] = sum;
+  } else {
+    const int m = tile / (9 * (CI / 16)), rest = tile % (9 * (CI / 16)), tap = rest / (CI / 16), nq = rest % (CI / 16);
+    const int co = 16 * m + 4 * g + r, ci = (CI / 16) * j + nq;
+    dw[((size_t)co * CI + ci) * 9 + tap] = sum;
+  }
+}
+
+// Weights [CO][CI][3][3] (torch) -> conv_a_kernel fragments.  transpose = 0: the forward
+// convolution (out = CO, in = CI); 1: its data gradient (out = CI, in = CO, taps flipped).
+// Fragment [c][s][tap][cbw][lane][e] = W'[16c + (lane & 15)][tap][16 (s KBW + cbw) + 4 (lane >> 4) + e];
+// for a 3-channel input (padded to 4) [c][tap][lane] = W'[16c + (lane & 15)][tap][lane >> 4].
+__global__ __launch_bounds__(256) void conv_pack_kernel(const float* __restrict__ w, int co_t, int ci_t, int transpose,
+                                                        int S, float* __restrict__ frag) {
+  const int OUT = transpose ? ci_t : co_t, IN = transpose ? co_t : ci_t;
+  const int in_pad = IN <= 4 ? 4 : IN;
+  const int total = OUT * 9 * in_pad;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  int o, tap, k;
+  if (in_pad == 4) {  // [c][tap][lane]
+    const int lane = idx & 63, t = (idx >> 6) % 9, c = (idx >> 6) / 9;
+    o = 16 * c + (lane & 15);
+    tap = t;
+    k = lane >> 4;
+  } else {
+    const int KBW = (IN / 16) / S;
+    const int e = idx & 3, lane = (idx >> 2) & 63;
+    int rest = idx >> 8;
+    const int cbw = rest % KBW;
+    rest /= KBW;
+    tap = rest % 9;
+    rest /= 9;
+    const int s = rest % S, c = rest / S;
+    o = 16 * c + (lane & 15);
+    k = 16 * (s * KBW + cbw) + 4 * (lane >> 4) + e;
+  }
+  float v = 0.f;
+  if (k < IN) {
+    if (!transpose) v = w[((size_t)o * ci_t + k) * 9 + tap];
+    else v = w[((size_t)k * ci_t + o) * 9 + (8 - tap)];
+  }
+  frag[idx] = v;
+}
+
+// obs [n][3][R][C] (any strides, in elements: the environment's NCHW observation or a
+// channels-last copy) -> x4 [n][R][C][4], channel 3 zero.
+__global__ __launch_bounds__(256) void obs_nhwc4_kernel(const float* __restrict__ obs, int64_t n_pos, int R, int C,
+                                                         int64_t sn, int64_t sc, int64_t sh, int64_t sw,
+                                                         float* __restrict__ x4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_pos; i += (int64_t)gridDim.x * 256) {
+    const int64_t smp = i / (R * C);
+    const int p = (int)(i % (R * C)), y = p / C, x = p % C;
+    const float* o = obs + smp * sn + y * sh + x * sw;
+    reinterpret_cast<f4*>(x4)[i] = f4{o[0], o[sc], o[2 * sc], 0.f};
+  }
+}
+
+// torch adaptive_avg_pool2d window [start, end) of output cell i (of 4) over n inputs
+__device__ __forceinline__ int win_start(int i, int n) { return (i * n) / 4; }
+__device__ __forceinline__ int win_end(int i, int n) { return ((i + 1) * n + 3) / 4; }
+
+// feat [n][64 * 16] = adaptive_avg_pool2d(a3, (4, 4)) flattened channel-major; a3 [n][R][C][68].
+// Thread = (sample, channel, cell): the window sum in row-major order / the window area.
+__global__ __launch_bounds__(256) void pool_kernel(const float* __restrict__ a3, int n, int R, int C,
+                                                   float* __restrict__ feat) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)n * 1024) return;
+  const int co = e & 63, cell = (e >> 6) & 15;
+  const int64_t smp = e >> 10;
+  const int cy = cell >> 2, cx = cell & 3;
+  const int y0 = win_start(cy, R), y1 = win_end(cy, R), x0 = win_start(cx, C), x1 = win_end(cx, C);
+  const float* s = a3 + smp * R * C * 68 + co;
+  float sum = 0.f;
+  for (int y = y0; y < y1; ++y)
+    for (int x = x0; x < x1; ++x) sum += s[(y * C + x) * 68];
+  feat[smp * 1024 + co * 16 + cell] = sum / (float)((y1 - y0) * (x1 - x0));
+}
+
+// d3 [n][R][C][68] = (a3 > 0) * (adaptive_avg_pool2d's input gradient of dfeat [n][1024]).
+__global__ __launch_bounds__(256) void pool_bwd_mask_kernel(const float* __restrict__ dfeat, const float* __restrict__ a3,
+                                                            int n, int R, int C, float* __restrict__ d3) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (sample, position, channel quad)
+  if (e >= (int64_t)n * R * C * 16) return;
+  const int q = e & 15;
+  const int64_t pe = e >> 4;
+  const int p = (int)(pe % (R * C));
+  const int64_t smp = pe / (R * C);
+  const int y = p / C, x = p % C;
+  f4 gsum = {0.f, 0.f, 0.f, 0.f};
+  for (int cy = 0; cy < 4; ++cy) {
+    const int y0 = win_start(cy, R), y1 = win_end(cy, R);
+    if (y < y0 || y >= y1) continue;
+    for (int cx = 0; cx < 4; ++cx) {
+      const int x0 = win_start(cx, C), x1 = win_end(cx, C);
+      if (x < x0 || x >= x1) continue;
+      const float area = (float)((y1 - y0) * (x1 - x0));
+      const float* df = dfeat + smp * 1024 + (4 * q) * 16 + cy * 4 + cx;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gsum[r] += df[r * 16] / area;
+    }
+  }
+  const f4 av = *reinterpret_cast<const f4*>(a3 + pe * 68 + 4 * q);
+  f4 v;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = av[r] > 0.f ? gsum[r] : 0.f;
+  *reinterpret_cast<f4*>(d3 + pe * 68 + 4 * q) = v;
+}
+
+}  // namespace tc
+
+// ---------------------------------------------------------------------------------------
+// launchers
+
+namespace {
+template <class K>
+hipError_t set_lds(K kern, int lds) {
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+}  // namespace
+
+int tc_workgroups() {
+  static int n_cu = 0;
+  if (!n_cu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n_cu = 256;
+  }
+  return n_cu;
+}
+
+template <int CI, int CO, int S, int MODE>
+static hipError_t launch_a(const tc::ConvAArgs& a, hipStream_t st) {
+  using G = tc::ConvAGeom<CI, CO, S, MODE, 20, 20>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = set_lds(&tc::conv_a_kernel<CI, CO, S, MODE, 20, 20>, G::LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((tc::conv_a_kernel<CI, CO, S, MODE, 20, 20>), dim3(tc_workgroups()), dim3(tc::kThreads), G::LDS,
+                     st, a);
+  return hipGetLastError();
+}
+
+// layer: 1 = conv1 (3 -> 32), 2 = conv2 (32 -> 64), 3 = conv3 (64 -> 64); mode 0 forward, 1 data
+// gradient (layers 2, 3: input = the gradient at the layer's output, 64 channels)
+hipError_t launch_train_conv(int layer, int mode, const float* x, int n, int R, int C, const float* frag,
+                             const float* bias, const float* mask, float* y, int* queue, hipStream_t st) {
+  if (R != 20 || C != 20) return hipErrorInvalidValue;
+  const tc::ConvAArgs a{x, frag, bias, mask, y, queue, n};
+  if (mode == 0) {
+    if (layer == 1) return launch_a<4, 32, 1, 0>(a, st);
+    if (layer == 2) return launch_a<32, 64, 1, 0>(a, st);
+    if (layer == 3) return launch_a<64, 64, 1, 0>(a, st);
+  } else {
+    if (layer == 3) return launch_a<64, 64, 1, 1>(a, st);
+    if (layer == 2) return launch_a<64, 32, 2, 1>(a, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+int train_conv_frag_floats(int layer, int mode) {
+  // forward: CO * 9 * max(CI, 4); gradient: CI * 9 * CO
+  if (layer == 1) return mode == 0 ? 32 * 9 * 4 : -1;
+  if (layer == 2) return 64 * 9 * 32;
+  if (layer == 3) return 64 * 9 * 64;
+  return -1;
+}
+
+hipError_t launch_train_conv_pack(int layer, int mode, const float* w, float* frag, hipStream_t st) {
+  const int total = train_conv_frag_floats(layer, mode);
+  if (total < 0) return hipErrorInvalidValue;
+  const int co = layer == 1 ? 32 : 64, ci = layer == 1 ? 3 : (layer == 2 ? 32 : 64);
+  const int S = (layer == 2 && mode == 1) ? 2 : 1;
+  hipLaunchKernelGGL(tc::conv_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w, co, ci, mode, S, frag);
+  return hipGetLastError();
+}
+
+template <int CI, int CO>
+static hipError_t launch_w(const float* dy, const float* x, int n, float* partial, float* dw, float* db, int* queue,
+                           int ci_real, hipStream_t st) {
+  using G = tc::ConvWGeom<CI, CO, 20, 20>;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = set_lds(&tc::conv_w_kernel<CI, CO, 20, 20>, G::LDS);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const tc::ConvWArgs a{dy, x, partial, queue, n};
+  hipLaunchKernelGGL((tc::conv_w_kernel<CI, CO, 20, 20>), dim3(tc_workgroups()), dim3(tc::kThreads), G::LDS, st, a);
+  const int nchunks = (n * G::NB + tc::kChunkBands - 1) / tc::kChunkBands;
+  hipLaunchKernelGGL((tc::conv_w_reduce_kernel<CI, CO, 20, 20>), dim3((G::WSZ + 255) / 256), dim3(256), 0, st, partial,
+                     nchunks, ci_real, dw, db);
+  return hipGetLastError();
+}
+
+int64_t train_conv_partial_floats(int layer, int n, int R, int C) {
+  if (R != 20 || C != 20 || n < 0) return -1;
+  const int64_t nchunks = ((int64_t)n * 5 + tc::kChunkBands - 1) / tc::kChunkBands;
+  int wsz = 0;
+  if (layer == 1) wsz = tc::ConvWGeom<4, 32, 20, 20>::WSZ;
+  else if (layer == 2) wsz = tc::ConvWGeom<32, 64, 20, 20>::WSZ;
+  else if (layer == 3) wsz = tc::ConvWGeom<64, 64, 20, 20>::WSZ;
+  else return -1;
+  return nchunks * wsz;
+}
+
+hipError_t launch_train_conv_wgrad(int layer, const float* dy, const float* x, int n, int R, int C, float* partial,
+                                   float* dw, float* db, int* queue, hipStream_t st) {
+  if (R != 20 || C != 20) return hipErrorInvalidValue;
+  if (layer == 1) return launch_w<4, 32>(dy, x, n, partial, dw, db, queue, 3, st);
+  if (layer == 2) return launch_w<32, 64>(dy, x, n, partial, dw, db, queue, 32, st);
+  if (layer == 3) return launch_w<64, 64>(dy, x, n, partial, dw, db, queue, 64, st);
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_obs_nhwc4(const float* obs, int n, int R, int C, const int64_t* strides, float* x4, hipStream_t st) {
+  const int64_t n_pos = (int64_t)n * R * C;
+  const int blocks = (int)std::min<int64_t>((n_pos + 255) / 256, 65536);
+  hipLaunchKernelGGL(tc::obs_nhwc4_kernel, dim3(blocks), dim3(256), 0, st, obs, n_pos, R, C, strides[0], strides[1],
+                     strides[2], strides[3], x4);
+  return hipGetLastError();
+}
+
+hipError_t launch_train_pool(const float* a3, int n, int R, int C, float* feat, hipStream_t st) {
+  const int64_t total = (int64_t)n * 1024;
+  hipLaunchKernelGGL(tc::pool_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a3, n, R, C, feat);
+  return hipGetLastError();
+}
+
+hipError_t launch_train_pool_bwd(const float* dfeat, const float* a3, int n, int R, int C, float* d3, hipStream_t st) {
+  const int64_t total = (int64_t)n * R * C * 16;
+  hipLaunchKernelGGL(tc::pool_bwd_mask_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, dfeat, a3, n, R,
+                     C, d3);
+  return hipGetLastError();
+}
+
+}  // namespace heist

@@ -5,7 +5,9 @@ multiplies into adds: the reference's raycast relies on separately rounded IEEE
 operations) and the library is linked against the HIP runtime that torch ships, so
 that torch tensors' device pointers and streams are valid inside it.
 """
+import hashlib
 import os
+import re
 import subprocess
 import sys
 
@@ -18,8 +20,8 @@ LIB_PATH = os.environ.get("HEIST_LIB") or os.path.join(os.path.dirname(os.path.a
 BUILD_DIR = os.path.join(PKG_ROOT, "build")
 ARCH = os.environ.get("HEIST_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["heist_env.hip", "heist_arch.hip", "heist_arch_update.hip", "heist_ppo.hip", "heist_policy.hip", "heist_train.hip",
-           "heist_capi.hip"]
-HEADERS = ["heist_device.h", "heist_trig.h", "heist_sincos_table.h"]
+           "heist_train_conv.hip", "heist_capi.hip"]
+# headers are found per source by following its #include "..." lines (_includes)
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # heist_env.hip: no SLP vectorization -- ROCm 7.2 clang miscompiles the packed-fp32
 # (v_pk_*_f32) forms of the fast raycast (see the fast path notes in heist_env.hip).  No
@@ -53,42 +55,103 @@ def _mtime(p):
     return os.path.getmtime(p) if os.path.exists(p) else -1.0
 
 
+_INCLUDE_RE = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _includes(path, seen=None):
+    """Every quoted header path reaches through #include "..." (csrc/ and include/), so a
+    generated header (heist_fan_intervals.h, heist_sincos_table.h) rebuilds its users."""
+    seen = set() if seen is None else seen
+    try:
+        with open(path) as f:
+            text = f.read()
+    except OSError:
+        return seen
+    for name in _INCLUDE_RE.findall(text):
+        for d in (os.path.dirname(path), CSRC, INCLUDE):
+            p = os.path.join(d, name)
+            if os.path.exists(p):
+                if p not in seen:
+                    seen.add(p)
+                    _includes(p, seen)
+                break
+    return seen
+
+
+def _command(src, obj):
+    return [HIPCC] + CFLAGS + FILE_FLAGS.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
+
+
+def _build_dir():
+    """Objects of the product library in build/, of any other library (HEIST_LIB) or flag
+    set in a directory of their own, so a variant build never links or overwrites the
+    product's objects."""
+    if not os.environ.get("HEIST_LIB"):
+        return BUILD_DIR
+    return os.path.join(BUILD_DIR, "variant_" + hashlib.sha1(LIB_PATH.encode()).hexdigest()[:12])
+
+
 def needs_build():
     if not os.path.exists(LIB_PATH):
         return True
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(INCLUDE, "heist.h"), __file__]
-    return max(_mtime(d) for d in deps) > _mtime(LIB_PATH)
+    deps = {__file__}
+    for src in SOURCES:
+        deps.add(os.path.join(CSRC, src))
+        deps |= _includes(os.path.join(CSRC, src))
+    if max(_mtime(d) for d in deps) > _mtime(LIB_PATH):
+        return True
+    bd = _build_dir()
+    return any(_cmd_changed(src, os.path.join(bd, src.replace(".hip", ".o"))) for src in SOURCES)
+
+
+def _cmd_file(obj):
+    return obj + ".cmd"
+
+
+def _cmd_changed(src, obj):
+    """The object was compiled with another command line (flags from HEIST_*_FLAGS or
+    HEIST_OFFLOAD_ARCH), recorded beside it."""
+    try:
+        with open(_cmd_file(obj)) as f:
+            return f.read() != " ".join(_command(src, obj))
+    except OSError:
+        return True
 
 
 def _stale(src, obj):
-    """obj needs compiling: older than its source, any shared header, or this script (the
-    flags).  heist_env.hip alone takes ~4 min, so an edit elsewhere does not rebuild it."""
-    deps = [os.path.join(CSRC, src), __file__] + [os.path.join(CSRC, f) for f in HEADERS]
-    if src == "heist_capi.hip":
-        deps.append(os.path.join(INCLUDE, "heist.h"))
-    return max(_mtime(d) for d in deps) > _mtime(obj)
+    """obj needs compiling: older than its source or any header it includes, or built with
+    another command line.  heist_env.hip alone takes ~4 min, so an edit elsewhere does not
+    rebuild it."""
+    deps = [os.path.join(CSRC, src)] + sorted(_includes(os.path.join(CSRC, src)))
+    return max(_mtime(d) for d in deps) > _mtime(obj) or _cmd_changed(src, obj)
 
 
 def build(force=False, verbose=False, jobs=4):
     if not force and not needs_build():
         return LIB_PATH
-    os.makedirs(BUILD_DIR, exist_ok=True)
+    bd = _build_dir()
+    os.makedirs(bd, exist_ok=True)
     procs, objs = [], []
     for src in SOURCES:
-        obj = os.path.join(BUILD_DIR, src.replace(".hip", ".o"))
+        obj = os.path.join(bd, src.replace(".hip", ".o"))
         objs.append(obj)
         if not force and not _stale(src, obj):
             continue
-        cmd = [HIPCC] + CFLAGS + FILE_FLAGS.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = _command(src, obj)
+        if os.path.exists(_cmd_file(obj)):
+            os.remove(_cmd_file(obj))
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
-        if len([p for _, p in procs if p.poll() is None]) >= jobs:
-            procs[0][1].wait()
-    for src, p in procs:
+        procs.append((src, obj, cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+        running = [p for _, _, _, p in procs if p.poll() is None]
+        if len(running) >= jobs:
+            running[0].wait()
+    for src, obj, cmd, p in procs:
         out, _ = p.communicate()
         if p.returncode != 0:
             raise RuntimeError("hipcc failed on %s:\n%s" % (src, out.decode(errors="replace")))
+        with open(_cmd_file(obj), "w") as f:
+            f.write(" ".join(cmd))
         if verbose and out:
             print(out.decode(errors="replace"), file=sys.stderr)
     tl = _torch_lib_dir()

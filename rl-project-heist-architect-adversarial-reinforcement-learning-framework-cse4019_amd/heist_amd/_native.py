@@ -71,6 +71,15 @@ SIGNATURES = {
     "heist_solver_head_packed_bytes": (_i, []),
     "heist_solver_head_pack": (_i, [_vp] * 14 + [_i, _vp, _vp]),
     "heist_solver_head": (_i, [_vp, _vp, _vp, _i, _vp, _i, ctypes.c_uint64, ctypes.c_uint64] + [_vp] * 7),
+    "heist_train_conv_supported": (_i, [_i, _i]),
+    "heist_train_conv_frag_floats": (_i, [_i, _i]),
+    "heist_train_conv_pack": (_i, [_i, _i, _vp, _vp, _vp]),
+    "heist_train_conv": (_i, [_i, _i, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "heist_train_conv_partial_floats": (_i64, [_i, _i, _i, _i]),
+    "heist_train_conv_wgrad": (_i, [_i, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]),
+    "heist_train_obs_nhwc4": (_i, [_vp, _i, _i, _i, _i64, _i64, _i64, _i64, _vp, _vp]),
+    "heist_train_pool": (_i, [_vp, _i, _i, _i, _vp, _vp]),
+    "heist_train_pool_bwd": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
 }
 
 

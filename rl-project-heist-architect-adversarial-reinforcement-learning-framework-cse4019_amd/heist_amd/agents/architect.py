@@ -430,7 +430,17 @@ class ArchitectAgent:  # agents/architect.py:16-170
         status word, copied behind it; the caller has synchronised with the launch)."""
         if not getattr(self, "_au_pending", 0):
             return False
-        return int(self._au_status[0]) != 0
+        code = int(self._au_status[0])
+        if dist_utils.is_multi():
+            # every rank replays the same steps (training.py's per-layout union): one rank's
+            # invalid launch must undo the launch on all of them, or the replicas drift apart
+            # (the fallback path's Adam forms its scalars differently), so the decision is
+            # the OR of the status words over ranks
+            t = torch.tensor([code & 1, code & 2], dtype=torch.int64, device=self.device)
+            dist_utils.allreduce_(t, "max")
+            code = int(t[0].item()) | int(t[1].item())
+            self._au_status[0] = code
+        return code != 0
 
     def _rerun_after_kernel_failure(self, r32: torch.Tensor) -> torch.Tensor:
         """Undo an invalid launch (weights, moments and step counters back to the snapshot

@@ -82,6 +82,99 @@ class _BackboneF32(torch.autograd.Function):
         return None, dw1, db1, dw2, db2, dw3, db3
 
 
+_TC_QUEUES = {}
+
+
+def _tc_queues(dev) -> torch.Tensor:
+    """8 work-queue counter pairs per device (one per launch site of _BackboneMFMA32), zero
+    between launches: each kernel's last workgroup resets its pair."""
+    q = _TC_QUEUES.get(dev)
+    if q is None:
+        q = _TC_QUEUES[dev] = torch.zeros(16, dtype=torch.int32, device=dev)
+    return q
+
+
+def _tc_act(n, R, C, ch, dev) -> torch.Tensor:
+    """[n][R][C][ch + 4] activation buffer (the 4 pad words per position are never read)."""
+    return torch.empty((n, R, C, ch + 4 if ch > 4 else 4), dtype=torch.float32, device=dev)
+
+
+class _BackboneMFMA32(torch.autograd.Function):
+    """SolverNetwork's conv stack (networks.py:93-100) forward and backward on the hand-written
+    fp32-MFMA kernels (csrc/heist_train_conv.hip, heist_train_* in include/heist.h): conv1-3
+    with bias + ReLU fused in their epilogues, the 4x4 adaptive pool; backward the pool's
+    gradient with conv3's ReLU mask, the data gradients of conv3 and conv2 with the ReLU masks
+    of their inputs fused, and the weight + bias gradients of all three (fixed-order sums).
+    Exact fp32 (MFMA f32 = an fmaf chain); differs from torch / MIOpen by summation order.
+    Returns the pooled features [B, 1024]."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, w3, b3):
+        from . import _native as nat
+        L, st = nat.lib(), nat.stream(x.device)
+        n, _, R, C = x.shape
+        dev = x.device
+        q = _tc_queues(dev)
+        P = lambda t: nat._vp(t.data_ptr())  # noqa: E731
+        frags = []
+        for layer, w in ((1, w1), (2, w2), (3, w3)):
+            f = torch.empty(L.heist_train_conv_frag_floats(layer, 0), dtype=torch.float32, device=dev)
+            nat.check(L.heist_train_conv_pack(layer, 0, P(w.detach().contiguous()), P(f), st), "heist_train_conv_pack")
+            frags.append(f)
+        x4 = _tc_act(n, R, C, 3, dev)
+        s = x.stride()
+        nat.check(L.heist_train_obs_nhwc4(P(x), n, R, C, s[0], s[1], s[2], s[3], P(x4), st), "heist_train_obs_nhwc4")
+        a1, a2, a3 = _tc_act(n, R, C, 32, dev), _tc_act(n, R, C, 64, dev), _tc_act(n, R, C, 64, dev)
+        for k, (layer, xi, yo, b) in enumerate(((1, x4, a1, b1), (2, a1, a2, b2), (3, a2, a3, b3))):
+            nat.check(L.heist_train_conv(layer, 0, P(xi), n, R, C, P(frags[k]), P(b.detach().contiguous()), None, P(yo),
+                                         P(q[2 * k:]), st), "heist_train_conv")
+        feat = torch.empty(n, 1024, dtype=torch.float32, device=dev)
+        nat.check(L.heist_train_pool(P(a3), n, R, C, P(feat), st), "heist_train_pool")
+        ctx.save_for_backward(x4, a1, a2, a3, w2, w3)
+        ctx.frags = frags  # the forward's packs stay alive until the kernels that read them ran
+        return feat
+
+    @staticmethod
+    def backward(ctx, dfeat):
+        from . import _native as nat
+        L = nat.lib()
+        x4, a1, a2, a3, w2, w3 = ctx.saved_tensors
+        n, R, C = x4.shape[0], x4.shape[1], x4.shape[2]
+        dev = x4.device
+        st = nat.stream(dev)
+        q = _tc_queues(dev)
+        P = lambda t: nat._vp(t.data_ptr())  # noqa: E731
+        dfeat = dfeat.contiguous()
+        d3 = _tc_act(n, R, C, 64, dev)
+        nat.check(L.heist_train_pool_bwd(P(dfeat), P(a3), n, R, C, P(d3), st), "heist_train_pool_bwd")
+        part = torch.empty(int(max(L.heist_train_conv_partial_floats(k, n, R, C) for k in (1, 2, 3))),
+                           dtype=torch.float32, device=dev)
+        grads = {}
+
+        def wgrad(layer, dy, xin, co, ci, qk):
+            dw = torch.empty(co, ci, 3, 3, dtype=torch.float32, device=dev)
+            db = torch.empty(co, dtype=torch.float32, device=dev)
+            nat.check(L.heist_train_conv_wgrad(layer, P(dy), P(xin), n, R, C, P(part), P(dw), P(db), P(q[qk:]), st),
+                      "heist_train_conv_wgrad")
+            grads[layer] = (dw, db)
+
+        def dgrad(layer, w, dy, mask, ch_out, qk):
+            f = torch.empty(L.heist_train_conv_frag_floats(layer, 1), dtype=torch.float32, device=dev)
+            nat.check(L.heist_train_conv_pack(layer, 1, P(w.detach().contiguous()), P(f), st), "heist_train_conv_pack")
+            d = _tc_act(n, R, C, ch_out, dev)
+            nat.check(L.heist_train_conv(layer, 1, P(dy), n, R, C, P(f), None, P(mask), P(d), P(q[qk:]), st),
+                      "heist_train_conv")
+            return d, f
+
+        d2, f3 = dgrad(3, w3, d3, a2, 64, 6)
+        wgrad(3, d3, a2, 64, 64, 8)
+        d1, f2 = dgrad(2, w2, d2, a1, 32, 10)
+        wgrad(2, d2, a1, 64, 32, 12)
+        wgrad(1, d1, x4, 32, 3, 14)
+        del f3, f2  # (stream-ordered: the caching allocator reuses them only behind the kernels)
+        return None, grads[1][0], grads[1][1], grads[2][0], grads[2][1], grads[3][0], grads[3][1]
+
+
 class SolverNetwork(nn.Module):  # networks.py:13-131
     def __init__(self, grid_rows: int = 20, grid_cols: int = 20, num_actions: int = 5, hidden_dim: int = 256,
                  lstm_hidden: int = 128):
@@ -122,11 +215,31 @@ class SolverNetwork(nn.Module):  # networks.py:13-131
         return (self.fused_tail and os.environ.get("HEIST_FUSED_TRAIN", "1") != "0" and state.is_cuda
                 and state.dtype == torch.float32 and state.dim() == 4 and state.shape[1] == 3
                 and state.shape[2] >= 4 and state.shape[3] >= 4 and state.shape[0] > 0
+                and not state.requires_grad  # _BackboneF32 forms no input gradient
                 and self.conv1.weight.dtype == torch.float32
                 and not torch.is_autocast_enabled("cuda") and self.conv3.out_channels == 64
                 and tuple(self.pool.output_size) == (4, 4))
 
+    #: fp32 on a HIP device at 20 x 20: every conv pass on the hand-written fp32-MFMA kernels
+    #: (_BackboneMFMA32); HEIST_TRAIN_CONV=0 or False here keeps MIOpen (_BackboneF32)
+    mfma_train = True
+
+    def _train_conv_ok(self, state: torch.Tensor) -> bool:
+        import os
+        if not (self.mfma_train and os.environ.get("HEIST_TRAIN_CONV", "1") != "0" and self._fused_tail_ok(state)):
+            return False
+        from . import _native
+        convs = (self.conv1, self.conv2, self.conv3)
+        return (bool(_native.lib().heist_train_conv_supported(state.shape[2], state.shape[3]))
+                and [(m.in_channels, m.out_channels) for m in convs] == [(3, 32), (32, 64), (64, 64)]
+                and all(m.kernel_size == (3, 3) and m.padding == (1, 1) and m.stride == (1, 1) and m.dilation == (1, 1)
+                        and m.groups == 1 and m.bias is not None for m in convs))
+
     def features(self, state: torch.Tensor) -> torch.Tensor:
+        if self._train_conv_ok(state):
+            x = _BackboneMFMA32.apply(state, self.conv1.weight, self.conv1.bias, self.conv2.weight, self.conv2.bias,
+                                      self.conv3.weight, self.conv3.bias)
+            return F.relu(self.fc_spatial(x))
         if self._fused_tail_ok(state):
             x = _BackboneF32.apply(state, self.conv1.weight, self.conv1.bias, self.conv2.weight, self.conv2.bias,
                                    self.conv3.weight, self.conv3.bias)

@@ -348,7 +348,8 @@ class HeistEnv:
         nat.check(nat.lib().heist_set_guard_cones(self._h, 1 if on else 0), "heist_set_guard_cones")
 
     CONFIG_KEYS = ("step_waves", "ray_chunk", "step_occ", "vis_gap", "obs_store", "ray_mode", "probe_mode",
-                   "dispatch_order", "split_obs", "guard_cones", "multi_waves", "fan_on", "lean", "interval_fans")
+                   "dispatch_order", "split_obs", "guard_cones", "multi_waves", "fan_on", "lean", "interval_fans",
+                   "step_lean")
 
     def kernel_config(self) -> dict:
         """The handle's effective kernel configuration (heist_get_config): the HEIST_* knobs as

@@ -25,10 +25,20 @@ def _cfg(tr):
                              vault_pos=tr["vault"], architect_budget=tr["budget"])
 
 
+@pytest.mark.parametrize("path", ["step_kernel", "lean_k1"])
 @pytest.mark.parametrize("cones", [True, False], ids=["guard_cones", "live_guards"])
 @pytest.mark.parametrize("tr", list(gd.env_traces()), ids=lambda t: t["name"])
-def test_golden_trace_bit_exact(tr, cones, gpu_device):
+def test_golden_trace_bit_exact(tr, cones, path, gpu_device, monkeypatch):
+    """Every golden trace on both single-tick paths: the step kernel (HEIST_STEP_LEAN=0) and,
+    where the lean K-tick kernel serves the grid (20 x 20 at one wave per env, 32 x 32),
+    heist_step as a one-tick heist_step_multi launch (the training rollout's tick)."""
+    if path == "lean_k1":
+        monkeypatch.setenv("HEIST_MULTI_WAVES", "1")
+    else:
+        monkeypatch.setenv("HEIST_STEP_LEAN", "0")
     env = HeistEnv(1, _cfg(tr), max_cams=16, max_guards=8, max_path=64, device=gpu_device, auto_reset=False)
+    lean_grid = (tr["R"], tr["C"]) in ((20, 20), (32, 32))
+    assert env.kernel_config()["step_lean"] == (1 if path == "lean_k1" and lean_grid else 0)
     env.set_guard_cones(cones)
     valid = env.set_layouts([(tr["walls"], tr["cams"], tr["guards"])], budget=tr["budget"])
     assert bool(valid[0]) == tr["valid"]
@@ -200,7 +210,9 @@ def test_full_size_sampled_vs_oracle(gpu_device):
 def test_full_size_c2_checkpoint_layouts_vs_oracle(gpu_device):
     """The bench's headline workload (BASELINE config 2: 4096 envs, 20x20, layouts sampled
     from checkpoints/architect_c2_fixed.pt at T = 1.0, budget 15): 48 envs replayed through
-    the oracle for 120 ticks with auto-reset, bit-exact, and batch-wide invariants for all."""
+    the oracle for 120 ticks with auto-reset, bit-exact, and batch-wide invariants for all.
+    heist_step runs here as a one-tick launch of the lean K-tick kernel (the training
+    rollout's tick at this batch size: step_lean == 1)."""
     import os
     from heist_amd.layouts import architect_checkpoint_layouts
     from heist_amd.training import _lb_rows
@@ -209,6 +221,7 @@ def test_full_size_c2_checkpoint_layouts_vs_oracle(gpu_device):
     n, budget = 4096, 15
     cfg = EnvironmentConfig(architect_budget=budget)
     env = HeistEnv(n, cfg, max_cams=5, max_guards=3, max_path=16, device=gpu_device)
+    assert env.kernel_config()["step_lean"] == 1
     lb, all_valid = architect_checkpoint_layouts(env, budget, seed=1234, ckpt=ckpt)
     assert all_valid
     env.reset()
@@ -595,10 +608,24 @@ def test_observation_store_forms_agree(R, n, gpu_device, monkeypatch):
             assert torch.equal(envs[0].reward64, envs[k].reward64), (t, k)
 
 
+def _step_kernel_env(*args, **kw):
+    """A handle whose heist_step runs the single-tick step kernel (HEIST_STEP_LEAN=0), the
+    independent reference of the K-tick comparisons (else heist_step is itself a one-tick
+    launch of the lean K-tick kernel wherever that kernel serves the handle)."""
+    import os
+    os.environ["HEIST_STEP_LEAN"] = "0"
+    try:
+        env = HeistEnv(*args, **kw)
+    finally:
+        del os.environ["HEIST_STEP_LEAN"]
+    assert env.kernel_config()["step_lean"] == 0
+    return env
+
+
 def _twin_envs(n, cfg, lays, budget, gpu_device, cones=True, **kw):
     envs = []
-    for _ in range(2):
-        env = HeistEnv(n, cfg, device=gpu_device, **kw)
+    for i in range(2):
+        env = (HeistEnv if i == 0 else _step_kernel_env)(n, cfg, device=gpu_device, **kw)
         env.set_guard_cones(cones)
         v = env.set_layouts(lays, budget=budget)
         env.reset()
@@ -811,7 +838,7 @@ def test_step_lean_wide_fans_and_many_guards(gpu_device, monkeypatch, fov, auto_
         assert torch.equal(sa[key], sb[key]), key
 
 
-def _interval_fan_layouts(n, R, budget, seed):
+def _interval_fan_layouts(n, R, budget, seed, **kw):
     """Synthetic layouts (every camera its own fov, heading, speed: the shared fan serves
     none) with some cameras forced onto the hard cases of the interval fans: the reference's
     default camera (heading 0, fov 60, speed 15: rays on whole and half degrees, on the axes),
@@ -820,7 +847,7 @@ def _interval_fan_layouts(n, R, budget, seed):
     rng = np.random.default_rng(seed)
     cuts = [0.0, 4.7885, 30.0, 41.4096, 45.0, 60.0, 90.0, 135.0, 180.0, 270.0]
     out = []
-    for walls, cams, guards in synthetic_layouts(n, R, R, budget, seed=seed):
+    for walls, cams, guards in synthetic_layouts(n, R, R, budget, seed=seed, **kw):
         cams = [dict(c) for c in cams]
         for c in cams:
             u = rng.random()
@@ -839,21 +866,25 @@ def _interval_fan_layouts(n, R, budget, seed):
 
 
 @pytest.mark.parametrize("auto_reset", [True, False], ids=["auto_reset", "no_reset"])
-@pytest.mark.parametrize("n,budget", [(4096, 15), (512, 40)], ids=["bench4096", "budget40"])
-def test_step_lean_interval_fans(gpu_device, monkeypatch, n, budget, auto_reset):
+@pytest.mark.parametrize("R,n,budget,kw", [(20, 4096, 15, {}), (20, 512, 40, {}),
+                                           (32, 2048, 40, {"n_cams": 4, "n_guards": 3})],
+                         ids=["bench4096", "budget40", "c5_32x32"])
+def test_step_lean_interval_fans(gpu_device, monkeypatch, R, n, budget, kw, auto_reset):
     """step_lean_kernel's interval fans (cameras the shared fan does not serve: the synthetic
-    mix) == single ticks, == the generic K-tick body (HEIST_INTERVAL_FANS=0), and 32 envs ==
-    the C oracle (reward, done, status, observation bytes) on every tick; short episodes,
-    launches of 1, 20, 63 and 70 ticks.  Reference environment.py:216-299, security.py:53-101."""
-    R = 20
-    cfg = EnvironmentConfig(max_steps=40, architect_budget=budget)
-    lays = _interval_fan_layouts(n, R, budget, 300 + budget)
+    mix) == single ticks of the step kernel, == the generic K-tick body (HEIST_INTERVAL_FANS=0),
+    and 32 envs == the C oracle (reward, done, status, observation bytes) on every tick; short
+    episodes, launches of 1, 20, 63 and 70 ticks; 20 x 20 and BASELINE C5's 32 x 32 (2048 envs,
+    exactly 4 cameras + 3 guards, budget 40: four observation quads per lane, 19 stores per
+    row).  Cameras forced onto the default heading, cuts, axes and wide fovs
+    (_interval_fan_layouts).  Reference environment.py:216-299, security.py:53-101."""
+    cfg = EnvironmentConfig(grid_rows=R, grid_cols=R, max_steps=40, architect_budget=budget)
+    lays = _interval_fan_layouts(n, R, budget, 300 + budget + R, **kw)
     envs = []
     monkeypatch.setenv("HEIST_MULTI_WAVES", "1")
-    for ivl in ("1", "0", "1"):
+    for i, ivl in enumerate(("1", "0", "1")):
         monkeypatch.setenv("HEIST_INTERVAL_FANS", ivl)
-        env = HeistEnv(n, cfg, max_cams=max(1, budget // 3), max_guards=max(1, budget // 5), max_path=16,
-                       device=gpu_device)
+        env = (HeistEnv if i < 2 else _step_kernel_env)(n, cfg, max_cams=max(1, budget // 3),
+                                                        max_guards=max(1, budget // 5), max_path=16, device=gpu_device)
         v = env.set_layouts(lays, budget=budget)
         env.reset()
         envs.append((env, v))
@@ -894,16 +925,18 @@ def test_step_lean_interval_fans(gpu_device, monkeypatch, n, budget, auto_reset)
         assert torch.equal(sa[key], sb[key]), key
 
 
-def test_step_lean_interval_fans_narrow_fovs(gpu_device, monkeypatch):
+@pytest.mark.parametrize("R,n,budget,kw", [(20, 512, 15, {}), (32, 2048, 40, {"n_cams": 4, "n_guards": 3})],
+                         ids=["20x20", "c5_32x32"])
+def test_step_lean_interval_fans_narrow_fovs(gpu_device, monkeypatch, R, n, budget, kw):
     """Cameras around the interval fans' ray-spacing bound (su >= 2^21 angle units: the integer
     pair bounds need rint(2^52 / su) in an int32; fov / 30 rays below ~5.27 degrees sends the
-    env to the generic body): fovs 2 .. 16 degrees mixed with ordinary ones, 512 envs, == single
-    ticks and 16 envs == the C oracle over 60 ticks in launches of 20 and 40."""
-    rng = np.random.default_rng(17)
-    n, R, budget = 512, 20, 15
-    cfg = EnvironmentConfig(max_steps=30)
+    env to the generic body): fovs 2 .. 16 degrees mixed with ordinary ones, 512 envs at 20 x 20
+    and 2048 C5 envs at 32 x 32, == single ticks of the step kernel and 16 envs == the C oracle
+    over 60 ticks in launches of 20 and 40."""
+    rng = np.random.default_rng(17 + R)
+    cfg = EnvironmentConfig(grid_rows=R, grid_cols=R, max_steps=30)
     lays = []
-    for walls, cams, guards in synthetic_layouts(n, R, R, budget, seed=171):
+    for walls, cams, guards in synthetic_layouts(n, R, R, budget, seed=171 + R, **kw):
         cams = [dict(c) for c in cams]
         for c in cams:
             if rng.random() < 0.6:
@@ -911,8 +944,9 @@ def test_step_lean_interval_fans_narrow_fovs(gpu_device, monkeypatch):
         lays.append((walls, cams, guards))
     monkeypatch.setenv("HEIST_MULTI_WAVES", "1")
     envs = []
-    for _ in range(2):
-        env = HeistEnv(n, cfg, max_cams=5, max_guards=3, max_path=16, device=gpu_device)
+    for i in range(2):
+        env = (HeistEnv if i == 0 else _step_kernel_env)(n, cfg, max_cams=max(5, budget // 3),
+                                                        max_guards=max(3, budget // 5), max_path=16, device=gpu_device)
         v = env.set_layouts(lays, budget=budget)
         env.reset()
         envs.append((env, v))

@@ -78,8 +78,9 @@ int heist_reset(heist_t h, const uint8_t* mask, float* obs_out, heist_stream_t s
  *   actions [N] int64 in 0..4;  obs_out [N][3][R][C] float32;  reward_out [N] float32
  *   (the float64 reward rounded, as agents/solver.py:138 stores it); reward64_out [N]
  *   float64 or NULL; done_out [N] uint8; status_out [N] int8 (HEIST_* codes).
- * Where the lean K-tick kernel serves the handle (20 x 20 at one wave per env, 32 x 32; no
- * instrumentation armed) the tick runs as heist_step_multi with K = 1, bit-identical.
+ * With HEIST_STEP_LEAN=1 at heist_create, where the lean K-tick kernel serves the handle
+ * (20 x 20 at one wave per env, 32 x 32; no instrumentation armed) the tick runs as
+ * heist_step_multi with K = 1, bit-identical (off by default: slower per tick).
  * auto_reset != 0: an env that finishes this tick is reset in the same launch and its
  * obs row holds the reset observation (training.py:515-520 next attempt), while reward,
  * done and status describe the finishing tick.  auto_reset == 0: finished envs answer
@@ -146,7 +147,7 @@ int heist_step_waves(heist_t h);
  * step_occ, vis_gap, obs_store, ray_mode, probe_mode, dispatch_order, split_obs,
  * guard_cones, multi_waves, fan_on, lean, interval_fans (the HEIST_* environment knobs as heist_create resolved them,
  * then any heist_set_* calls), step_lean (1: heist_step currently runs as a one-tick
- * heist_step_multi launch on the lean kernel; HEIST_STEP_LEAN=0 at heist_create turns it off).  probe_mode != 0 selects the profiling step kernel, whose results are
+ * heist_step_multi launch on the lean kernel; HEIST_STEP_LEAN=1 at heist_create turns it on).  probe_mode != 0 selects the profiling step kernel, whose results are
  * wrong by design (phases skipped). */
 int heist_get_config(heist_t h, int32_t* out, int n);
 

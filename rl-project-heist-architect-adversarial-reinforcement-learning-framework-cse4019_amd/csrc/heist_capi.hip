@@ -100,8 +100,10 @@ struct heist_env {
   bool fan_used;           // a K-tick launch has been issued on fan_stream
   hipEvent_t fan_done;     // recorded behind every K-tick launch: a refill on another stream waits for it
   int64_t stamp_words;     // size of the stamp buffer armed by heist_step_stamps (uint64 words)
-  int step_lean;           // 1 (default): heist_step runs as a one-tick heist_step_multi launch wherever the
-                           // lean K-tick kernel serves the handle (HEIST_STEP_LEAN=0: the single-tick kernel)
+  int step_lean;           // 1 (HEIST_STEP_LEAN=1): heist_step runs as a one-tick heist_step_multi launch wherever
+                           // the lean K-tick kernel serves the handle; 0 (default): the single-tick step kernel
+                           // (C2, 4096 envs: 15.1 us per tick against 18.9 for the one-tick lean launch, whose
+                           // per-launch prologue costs ~12 us: tools/probe_single_tick.py, gpurun_out r06b)
 };
 
 namespace {
@@ -342,7 +344,7 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   if (const char* f = getenv("HEIST_INTERVAL_FANS")) p.interval_fans = atoi(f) ? 1 : 0;
   p.guard_cones = 1;
   if (const char* gc = getenv("HEIST_GUARD_CONES")) p.guard_cones = atoi(gc) ? 1 : 0;
-  h->step_lean = 1;
+  h->step_lean = 0;
   if (const char* f = getenv("HEIST_STEP_LEAN")) h->step_lean = atoi(f) ? 1 : 0;
   std::vector<double> hrad(heist::kHalfDegN);
   for (int m = 0; m < heist::kHalfDegN; ++m) hrad[m] = (0.5 * (m - heist::kHalfDegN / 2)) * heist::kDegToRad;

@@ -294,10 +294,17 @@ __global__ __launch_bounds__(kThreads, 1) void conv_a_kernel(ConvAArgs a) {
 
 // ---------------------------------------------------------------------------------------
 // conv_w_kernel: weight and bias gradient partials per chunk of kChunkBands bands.
-//   dY [n][R][C][PD] (PD = CO + 4), X [n][R][C][PI]; partial [chunk][WSZ] floats.
-//   CI >= 32: wave (m = row tile, h) holds tiles (tap, q) with the wave's QW input channels per
-//   lane j: ci = (CI / 16) j + QW h + qq (one ds_read of QW words per tap); CI == 4: wave
-//   (m, h < 3) holds column tile h of the 36 (tap, ci) pairs, h == 3 the bias tile.
+//   dY [n][R][C][PD] (PD = CO + 4), X [n][R][C][PI]; partial [chunk][WSZ] floats.  An
+//   iteration takes BPI bands (one LDS buffer: their X images, then their dY rows), the next
+//   iteration's bands DMA'd into the other buffer meanwhile.  The band's k-steps (4 positions
+//   each) are unrolled, so every LDS address is a lane base plus an immediate.
+//   CI >= 32: wave (m = row tile, h) accumulates the tiles (tap, qq) whose column j holds input
+//   channel ci = col_ci(j, h, qq) -- a bank-conflict-free assignment: the 16 lanes of a k group
+//   read QW consecutive words each, and the next k group (the next position, 4 banks further)
+//   lands on the banks this one leaves free (ds_read_b64: 2 x 32-lane groups; ds_read_b32: 32
+//   banks).  CI == 4: wave (m, kg) takes every 4th k-step (k group kg) for all three column
+//   tiles of the 36 (tap, ci) pairs and the bias tile; the four k groups' tiles are summed in a
+//   fixed order through LDS at the chunk's end.
 struct ConvWArgs {
   const float* dy;
   const float* x;
@@ -310,47 +317,69 @@ template <int CI, int CO, int R, int C>
 struct ConvWGeom {
   static constexpr int PI = Pitch<CI>::v, PD = Pitch<CO>::v, MT = CO / 16, WPM = 8 / MT;
   static constexpr int RP = C + 2, NB = R / 4, KS = C;  // k-steps (4 positions each) per band
-  static constexpr int XB_F = 6 * RP * PI, DB_F = 4 * C * PD, BUF_F = XB_F + DB_F;
+  static constexpr int BPI = CI == 4 ? 4 : 1;           // bands per iteration (one LDS buffer)
+  static constexpr int XB_F = 6 * RP * PI, DB_F = 4 * C * PD, BUF_F = BPI * (XB_F + DB_F);
   static constexpr int QW = CI == 4 ? 1 : (CI / 16) / WPM;   // input channels per lane per tap
-  static constexpr int NTW = CI == 4 ? 1 : 9 * QW;           // column tiles per wave
+  static constexpr int NTW = CI == 4 ? 3 : 9 * QW;           // column tiles per wave
   static constexpr int NT_ALL = CI == 4 ? 3 : 9 * (CI / 16); // column tiles per row tile
   static constexpr int WSZ = MT * NT_ALL * 256 + CO;         // partial floats per chunk
   static constexpr int LDS = 2 * BUF_F * 4 + 64;
   static_assert(CI == 4 ? WPM == 4 : (CI / 16) % WPM == 0, "wave split");
+  static_assert(kChunkBands % BPI == 0, "whole iterations per chunk");
+  static_assert(CI != 4 || 8 * 4 * 256 <= BPI * DB_F, "the k groups' partial tiles fit the dY images");
 };
+
+// Input channel of column j of the wave's tile qq (CI >= 32, wave half h); for CI == 4 the
+// column jj = 16 tile + j is the pair (tap jj / 4, ci jj % 4).
+template <int CI>
+__host__ __device__ constexpr int col_ci(int j, int h, int qq) {
+  return CI == 64 ? 8 * (j >> 1) + 2 * (j & 1) + 4 * h + qq : 8 * (j >> 2) + (j & 3) + 4 * h;
+}
 
 template <int CI, int CO, int R, int C>
 __global__ __launch_bounds__(kThreads, 1) void conv_w_kernel(ConvWArgs a) {
   using G = ConvWGeom<CI, CO, R, C>;
   constexpr int PI = G::PI, PD = G::PD, MT = G::MT, RP = G::RP, NB = G::NB, QW = G::QW, NTW = G::NTW;
+  constexpr int BPI = G::BPI, KS = G::KS;
   extern __shared__ f4 smem4[];
   float* smem = reinterpret_cast<float*>(smem4);
-  float* buf[2] = {smem, smem + G::BUF_F};
   int* slot = reinterpret_cast<int*>(smem + 2 * G::BUF_F);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int m = wid % MT, h = wid / MT;
+  const int m = wid % MT, h = wid / MT;  // CI == 4: h is the k group
   const int j = lane & 15, g = lane >> 4;
   const int nbands = a.n * NB, nchunks = (nbands + kChunkBands - 1) / kChunkBands;
-  const bool has_bias = CI == 4 ? h == 3 : h == 0;
-  const bool has_cols = CI == 4 ? h < 3 : true;
+  const bool has_bias = CI == 4 ? true : h == 0;
 
-  // column offsets of this lane for the CI == 4 layout: column jj = 16 h + j <-> (tap, ci)
-  int coff = 0;
-  bool cval = true;
+  // this lane's column offsets within a position (word units)
+  int coff[CI == 4 ? 3 : QW];
+  bool cval[3] = {true, true, true};
   if constexpr (CI == 4) {
-    const int jj = 16 * (h < 3 ? h : 0) + j, tap = jj / 4, ci = jj % 4;
-    cval = jj < 36;
-    coff = cval ? ((tap / 3) * RP + tap % 3) * PI + ci : 0;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int jj = 16 * t + j, tap = jj / 4, ci = jj % 4;
+      cval[t] = jj < 36;
+      coff[t] = cval[t] ? ((tap / 3) * RP + tap % 3) * PI + ci : 0;
+    }
+  } else {
+#pragma unroll
+    for (int qq = 0; qq < QW; ++qq) coff[qq] = col_ci<CI>(j, h, qq);
   }
   f4 acc[NTW];
   f4 accb = {0.f, 0.f, 0.f, 0.f};
 
-  auto issue = [&](int gb, float* b0) {
-    if (gb >= nbands) return;
-    load_band<CI, R, C>(a.x, b0, gb, 0, wid, lane);
-    const int smp = gb / NB, y0 = (gb % NB) * 4;
-    dma_range(a.dy + ((size_t)smp * R + y0) * C * PD, b0 + G::XB_F, G::DB_F * 4, 5, wid, lane);
+  // iteration `it` of the WG's sequence reads buffer it & 1: BPI bands of chunk `ch` from `ib`
+  auto issue = [&](int ch, int ib, int par) {
+    float* b0 = smem + par * G::BUF_F;
+#pragma unroll
+    for (int bb = 0; bb < BPI; ++bb) {
+      const int gb = ch * kChunkBands + ib + bb;
+      if (gb >= nbands) break;
+      load_band<CI, R, C>(a.x, b0 + bb * G::XB_F, gb, bb * 3, wid, lane);
+      const int smp = gb / NB, y0 = (gb % NB) * 4;
+      dma_range(a.dy + ((size_t)smp * R + y0) * C * PD, b0 + BPI * G::XB_F + bb * G::DB_F, G::DB_F * 4, bb * 3 + 5, wid,
+                lane);
+    }
   };
   if (tid == 0) {
     slot[0] = atomicAdd(a.queue, 1);
@@ -360,86 +389,118 @@ __global__ __launch_bounds__(kThreads, 1) void conv_w_kernel(ConvWArgs a) {
   zero_range(smem, 2 * G::BUF_F * 4, wid, lane);
   __syncthreads();
   int chunk = slot[0], nchunk = slot[1];
-  if (chunk < nchunks) issue(chunk * kChunkBands, buf[0]);
+  if (chunk < nchunks) issue(chunk, 0, 0);
   int it = 0;
   while (chunk < nchunks) {
 #pragma unroll
     for (int t = 0; t < NTW; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
     accb = f4{0.f, 0.f, 0.f, 0.f};
-    for (int i = 0; i < kChunkBands; ++i, ++it) {
-      const int gb = chunk * kChunkBands + i;
-      float* xi = buf[it & 1];
-      const float* di = xi + G::XB_F;
+    for (int i = 0; i < kChunkBands; i += BPI, ++it) {
+      const float* xi0 = smem + (it & 1) * G::BUF_F;
+      const float* di0 = xi0 + BPI * G::XB_F;
       wait_dma();
       __syncthreads();
-      // next band: this chunk's, or the first of the next chunk (whose id was drawn ahead)
-      if (i + 1 < kChunkBands) {
-        issue(gb + 1, buf[(it + 1) & 1]);
+      // next iteration: this chunk's next bands, or the first of the next chunk (drawn ahead)
+      if (i + BPI < kChunkBands) {
+        issue(chunk, i + BPI, (it + 1) & 1);
       } else {
-        if (nchunk < nchunks) issue(nchunk * kChunkBands, buf[(it + 1) & 1]);
+        if (nchunk < nchunks) issue(nchunk, 0, (it + 1) & 1);
         if (tid == 0) slot[2] = atomicAdd(a.queue, 1);
       }
-      if (gb < nbands) {
-        for (int ks = 0; ks < G::KS; ++ks) {
+#pragma unroll
+      for (int bb = 0; bb < BPI; ++bb) {
+        if (chunk * kChunkBands + i + bb >= nbands) break;  // (uniform)
+        const float* xi = xi0 + bb * G::XB_F;
+        const float* di = di0 + bb * G::DB_F;
+#pragma unroll
+        for (int ks = (CI == 4 ? h : 0); ks < KS; ks += (CI == 4 ? 4 : 1)) {
           // positions 4 ks + g: one image row y (C % 4 == 0), column xx
-          const int q = 4 * ks + g, y = q / C, xx = q % C;
+          const int q = 4 * ks + g, y = (4 * ks) / C, xx = q - y * C;
           const float av = lds_f1(di, q * PD + 16 * m + j);
           const int xb = (y * RP + xx) * PI;
-          if (has_cols) {
-            if constexpr (CI == 4) {
-              const float bv = cval ? lds_f1(xi, xb + coff) : 0.f;
-              acc[0] = mfma(av, bv, acc[0]);
-            } else {
+          if constexpr (CI == 4) {
 #pragma unroll
-              for (int tap = 0; tap < 9; ++tap) {
-                const int o = xb + ((tap / 3) * RP + tap % 3) * PI + (CI / 16) * j + QW * h;
-                if constexpr (QW == 2) {
-                  const f2 bv = lds_f2(xi, o);
-                  acc[tap * 2] = mfma(av, bv[0], acc[tap * 2]);
-                  acc[tap * 2 + 1] = mfma(av, bv[1], acc[tap * 2 + 1]);
-                } else {
-                  acc[tap] = mfma(av, lds_f1(xi, o), acc[tap]);
-                }
+            for (int t = 0; t < 3; ++t) acc[t] = mfma(av, cval[t] ? lds_f1(xi, xb + coff[t]) : 0.f, acc[t]);
+          } else {
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+              const int o = xb + ((tap / 3) * RP + tap % 3) * PI;
+              if constexpr (QW == 2) {
+                const f2 bv = lds_f2(xi, o + coff[0]);
+                acc[tap * 2] = mfma(av, bv[0], acc[tap * 2]);
+                acc[tap * 2 + 1] = mfma(av, bv[1], acc[tap * 2 + 1]);
+              } else {
+                acc[tap] = mfma(av, lds_f1(xi, o + coff[0]), acc[tap]);
               }
             }
           }
           if (has_bias) accb = mfma(av, 1.0f, accb);
         }
       }
-      if (i + 1 == kChunkBands) {
-        __syncthreads();  // slot[2] visible
-      }
     }
-    // this chunk's partial: tiles [m][tap][nq][lane][4], then the bias [CO]
+    // this chunk's partial: tiles [m][tile][lane][4], then the bias [CO]
     float* p = a.partial + (size_t)chunk * G::WSZ;
-    if (has_cols) {
-      if constexpr (CI == 4) {
-        *reinterpret_cast<f4*>(p + ((size_t)m * 3 + h) * 256 + lane * 4) = acc[0];
-      } else {
+    if constexpr (CI == 4) {
+      // the k groups' tiles (3 column tiles + the bias tile each) summed in k-group order through
+      // the dY images of the buffer this iteration read (everyone is done with it after the
+      // barrier; the next DMA into it is issued after the next iteration's first barrier)
+      __syncthreads();
+      float* scr = smem + ((it - 1) & 1) * G::BUF_F + BPI * G::XB_F;
+      float* mine = scr + (m * 4 + h) * 4 * 256;
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap)
+      for (int t = 0; t < 3; ++t) *reinterpret_cast<f4*>(mine + t * 256 + lane * 4) = acc[t];
+      *reinterpret_cast<f4*>(mine + 3 * 256 + lane * 4) = accb;
+      __syncthreads();
+      if (h == 0) {
 #pragma unroll
-          for (int qq = 0; qq < QW; ++qq)
-            *reinterpret_cast<f4*>(p + (((size_t)m * 9 + tap) * (CI / 16) + QW * h + qq) * 256 + lane * 4) =
-                acc[tap * QW + qq];
+        for (int t = 0; t < 4; ++t) {
+          f4 v = lds_f4(scr, (m * 4 * 4 + t) * 256 + lane * 4);
+#pragma unroll
+          for (int k = 1; k < 4; ++k) v += lds_f4(scr, ((m * 4 + k) * 4 + t) * 256 + lane * 4);
+          if (t < 3) *reinterpret_cast<f4*>(p + ((size_t)m * 3 + t) * 256 + lane * 4) = v;
+          else if (j == 0) *reinterpret_cast<f4*>(p + MT * G::NT_ALL * 256 + 16 * m + 4 * g) = v;
+        }
       }
+    } else {
+      __syncthreads();  // slot[2] visible
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+        for (int qq = 0; qq < QW; ++qq)
+          *reinterpret_cast<f4*>(p + (((size_t)m * 9 + tap) * (CI / 16) + QW * h + qq) * 256 + lane * 4) =
+              acc[tap * QW + qq];
+      if (has_bias && j == 0) *reinterpret_cast<f4*>(p + MT * G::NT_ALL * 256 + 16 * m + 4 * g) = accb;
     }
-    if (has_bias && j == 0) *reinterpret_cast<f4*>(p + MT * G::NT_ALL * 256 + 16 * m + 4 * g) = accb;
     chunk = nchunk;
     nchunk = slot[2];
   }
   queue_exit(a.queue);
 }
 
-// dW (torch layout [CO][CI_real][3][3]) and db [CO] = the partials summed in chunk order.
+// dW (torch layout [CO][CI_real][3][3]) and db [CO] = the chunk partials summed in a fixed
+// order: workgroup = 64 consecutive partial elements; its 4 waves take the chunks k = 4 i + w,
+// each into 8 accumulators by (i mod 8) (8 loads in flight), which are added in order, then the
+// 4 waves' sums in order (deterministic; the association is fixed by nchunks alone).
 template <int CI, int CO, int R, int C>
 __global__ __launch_bounds__(256) void conv_w_reduce_kernel(const float* __restrict__ partial, int nchunks, int ci_real,
                                                             float* __restrict__ dw, float* __restrict__ db) {
   using G = ConvWGeom<CI, CO, R, C>;
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= G::WSZ) return;
-  float sum = 0.f;
-  for (int k = 0; k < nchunks; ++k) sum += partial[(size_t)k * G::WSZ + e];
+  __shared__ float wsum[4][64];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int e = blockIdx.x * 64 + l;
+  float acc8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (e < G::WSZ) {
+    const float* src = partial + e;
+    int i = 0;
+    for (; 4 * (i + 7) + w < nchunks; i += 8)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc8[u] += src[(size_t)(4 * (i + u) + w) * G::WSZ];
+    for (; 4 * i + w < nchunks; ++i) acc8[i & 7] += src[(size_t)(4 * i + w) * G::WSZ];
+  }
+  wsum[w][l] = ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
+  __syncthreads();
+  if (w != 0 || e >= G::WSZ) return;
+  const float sum = ((wsum[0][l] + wsum[1][l]) + wsum[2][l]) + wsum[3][l];
   const int tiles = G::MT * G::NT_ALL * 256;
   if (e >= tiles) {
     db[e - tiles] = sum;
@@ -447,11 +508,12 @@ __global__ __launch_bounds__(256) void conv_w_reduce_kernel(const float* __restr
   }
   const int r = e & 3, lane = (e >> 2) & 63, tile = e >> 8, j = lane & 15, g = lane >> 4;
   if constexpr (CI == 4) {
-    const int m = tile / 3, h = tile % 3, jj = 16 * h + j, tap = jj / 4, ci = jj % 4;
+    const int m = tile / 3, t = tile % 3, jj = 16 * t + j, tap = jj / 4, ci = jj % 4;
     if (jj < 36 && ci < ci_real) dw[((size_t)(16 * m + 4 * g + r) * ci_real + ci) * 9 + tap] = sum;
   } else {
-    const int m = tile / (9 * (CI / 16)), rest = tile % (9 * (CI / 16)), tap = rest / (CI / 16), nq = rest % (CI / 16);
-    const int co = 16 * m + 4 * g + r, ci = (CI / 16) * j + nq;
+    constexpr int NQ = CI / 16, QW = G::QW;
+    const int m = tile / (9 * NQ), rest = tile % (9 * NQ), tap = rest / NQ, nq = rest % NQ;
+    const int co = 16 * m + 4 * g + r, ci = col_ci<CI>(j, nq / QW, nq % QW);
     dw[((size_t)co * CI + ci) * 9 + tap] = sum;
   }
 }
@@ -640,7 +702,7 @@ static hipError_t launch_w(const float* dy, const float* x, int n, float* partia
   const tc::ConvWArgs a{dy, x, partial, queue, n};
   hipLaunchKernelGGL((tc::conv_w_kernel<CI, CO, 20, 20>), dim3(tc_workgroups()), dim3(tc::kThreads), G::LDS, st, a);
   const int nchunks = (n * G::NB + tc::kChunkBands - 1) / tc::kChunkBands;
-  hipLaunchKernelGGL((tc::conv_w_reduce_kernel<CI, CO, 20, 20>), dim3((G::WSZ + 255) / 256), dim3(256), 0, st, partial,
+  hipLaunchKernelGGL((tc::conv_w_reduce_kernel<CI, CO, 20, 20>), dim3((G::WSZ + 63) / 64), dim3(256), 0, st, partial,
                      nchunks, ci_real, dw, db);
   return hipGetLastError();
 }

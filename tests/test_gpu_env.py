@@ -34,6 +34,7 @@ def test_golden_trace_bit_exact(tr, cones, path, gpu_device, monkeypatch):
     heist_step as a one-tick heist_step_multi launch (the training rollout's tick)."""
     if path == "lean_k1":
         monkeypatch.setenv("HEIST_MULTI_WAVES", "1")
+        monkeypatch.setenv("HEIST_STEP_LEAN", "1")
     else:
         monkeypatch.setenv("HEIST_STEP_LEAN", "0")
     env = HeistEnv(1, _cfg(tr), max_cams=16, max_guards=8, max_path=64, device=gpu_device, auto_reset=False)
@@ -207,12 +208,14 @@ def test_full_size_sampled_vs_oracle(gpu_device):
             assert o_np[j].tobytes() == oracles[j].state_tensor().tobytes()
 
 
-def test_full_size_c2_checkpoint_layouts_vs_oracle(gpu_device):
+@pytest.mark.parametrize("step_lean", [0, 1], ids=["step_kernel", "lean_k1"])
+def test_full_size_c2_checkpoint_layouts_vs_oracle(gpu_device, monkeypatch, step_lean):
     """The bench's headline workload (BASELINE config 2: 4096 envs, 20x20, layouts sampled
     from checkpoints/architect_c2_fixed.pt at T = 1.0, budget 15): 48 envs replayed through
-    the oracle for 120 ticks with auto-reset, bit-exact, and batch-wide invariants for all.
-    heist_step runs here as a one-tick launch of the lean K-tick kernel (the training
-    rollout's tick at this batch size: step_lean == 1)."""
+    the oracle for 120 ticks with auto-reset, bit-exact, and batch-wide invariants for all;
+    heist_step on the single-tick step kernel and as a one-tick launch of the lean K-tick
+    kernel (HEIST_STEP_LEAN=1)."""
+    monkeypatch.setenv("HEIST_STEP_LEAN", str(step_lean))
     import os
     from heist_amd.layouts import architect_checkpoint_layouts
     from heist_amd.training import _lb_rows
@@ -221,7 +224,7 @@ def test_full_size_c2_checkpoint_layouts_vs_oracle(gpu_device):
     n, budget = 4096, 15
     cfg = EnvironmentConfig(architect_budget=budget)
     env = HeistEnv(n, cfg, max_cams=5, max_guards=3, max_path=16, device=gpu_device)
-    assert env.kernel_config()["step_lean"] == 1
+    assert env.kernel_config()["step_lean"] == step_lean
     lb, all_valid = architect_checkpoint_layouts(env, budget, seed=1234, ckpt=ckpt)
     assert all_valid
     env.reset()

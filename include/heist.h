@@ -365,28 +365,31 @@ int heist_relu_bwd_nhwc(float* g, const float* y, int n, int positions, int chan
  *   heist_train_conv_pack: torch weights [co][ci][3][3] of layer 1 (3 -> 32, mode 0), 2 (32 -> 64)
  *     or 3 (64 -> 64) -> frag (heist_train_conv_frag_floats floats); mode 0 the forward
  *     convolution, mode 1 its data gradient (transposed, flipped taps).
- *   heist_train_conv: mode 0 y = relu(conv(x) + bias); mode 1 (layers 2, 3) y = (mask > 0) ?
- *     conv_data_grad(x) : 0 with x the gradient at the layer's output (64 channels) and mask the
- *     saved activation of the layer's input (threshold_backward).  queue: 2 device ints, zero
+ *   heist_train_conv: mode 0 y = relu(conv(x) + bias) and, if mask_bits is not NULL, its ReLU
+ *     mask as bits (ReLU masks are [n][rows][cols][channels / 4] uint8: bit r of byte k =
+ *     channel 4 k + r is > 0); mode 1 (layers 2, 3) y = mask ? conv_data_grad(x) : 0 with x the
+ *     gradient at the layer's output (64 channels) and mask_bits the mask of the layer's input
+ *     (the forward's bits of the layer below: threshold_backward).  queue: 2 device ints, zero
  *     before the first launch (the kernels leave them zero); one pair per launch in flight.
  *   heist_train_conv_wgrad: dw [co][ci][3][3] and db [co] of layer 1-3 from dy (the gradient at
  *     the layer's pre-activation output) and x (its input); partial:
  *     heist_train_conv_partial_floats(layer, n, ...) floats of scratch.  Sums in a fixed order.
  *   heist_train_obs_nhwc4: obs [n][3][rows][cols] with element strides -> [n][rows][cols][4].
  *   heist_train_pool: feat [n][1024] = adaptive_avg_pool2d(a3, (4, 4)) flattened C-major.
- *   heist_train_pool_bwd: d3 = (a3 > 0) * the pool's input gradient of dfeat [n][1024]. */
+ *   heist_train_pool_bwd: d3 = mask3 * the pool's input gradient of dfeat [n][1024], mask3 the
+ *     ReLU mask bits of conv3's forward. */
 int heist_train_conv_supported(int rows, int cols);
 int heist_train_conv_frag_floats(int layer, int mode);
 int heist_train_conv_pack(int layer, int mode, const float* w, float* frag, heist_stream_t stream);
 int heist_train_conv(int layer, int mode, const float* x, int n, int rows, int cols, const float* frag,
-                     const float* bias, const float* mask, float* y, int* queue, heist_stream_t stream);
+                     const float* bias, uint8_t* mask_bits, float* y, int* queue, heist_stream_t stream);
 int64_t heist_train_conv_partial_floats(int layer, int n, int rows, int cols);
 int heist_train_conv_wgrad(int layer, const float* dy, const float* x, int n, int rows, int cols, float* partial,
                            float* dw, float* db, int* queue, heist_stream_t stream);
 int heist_train_obs_nhwc4(const float* obs, int n, int rows, int cols, int64_t stride_n, int64_t stride_c,
                           int64_t stride_h, int64_t stride_w, float* x4, heist_stream_t stream);
 int heist_train_pool(const float* a3, int n, int rows, int cols, float* feat, heist_stream_t stream);
-int heist_train_pool_bwd(const float* dfeat, const float* a3, int n, int rows, int cols, float* d3,
+int heist_train_pool_bwd(const float* dfeat, const uint8_t* mask3_bits, int n, int rows, int cols, float* d3,
                          heist_stream_t stream);
 
 #ifdef __cplusplus

@@ -72,12 +72,12 @@ int train_conv_frag_floats(int layer, int mode);
 int64_t train_conv_partial_floats(int layer, int n, int R, int C);
 hipError_t launch_train_conv_pack(int layer, int mode, const float* w, float* frag, hipStream_t st);
 hipError_t launch_train_conv(int layer, int mode, const float* x, int n, int R, int C, const float* frag,
-                             const float* bias, const float* mask, float* y, int* queue, hipStream_t st);
+                             const float* bias, uint8_t* mask_bits, float* y, int* queue, hipStream_t st);
 hipError_t launch_train_conv_wgrad(int layer, const float* dy, const float* x, int n, int R, int C, float* partial,
                                    float* dw, float* db, int* queue, hipStream_t st);
 hipError_t launch_obs_nhwc4(const float* obs, int n, int R, int C, const int64_t* strides, float* x4, hipStream_t st);
 hipError_t launch_train_pool(const float* a3, int n, int R, int C, float* feat, hipStream_t st);
-hipError_t launch_train_pool_bwd(const float* dfeat, const float* a3, int n, int R, int C, float* d3, hipStream_t st);
+hipError_t launch_train_pool_bwd(const float* dfeat, const uint8_t* m3, int n, int R, int C, float* d3, hipStream_t st);
 hipError_t launch_gae(const float* r, const float* v, const uint8_t* d, const float* last_value, int T, int N,
                       double gamma, double lam, float* adv, float* ret, hipStream_t st);
 hipError_t launch_adv_moments(const float* x, int64_t n, int phase, double* acc, hipStream_t st);
@@ -826,16 +826,16 @@ int heist_train_conv_pack(int layer, int mode, const float* w, float* frag, heis
 }
 
 int heist_train_conv(int layer, int mode, const float* x, int n, int rows, int cols, const float* frag,
-                     const float* bias, const float* mask, float* y, int* queue, heist_stream_t stream) {
+                     const float* bias, uint8_t* mask_bits, float* y, int* queue, heist_stream_t stream) {
   HEIST_REQUIRE(heist_train_conv_supported(rows, cols), "heist_train_conv: grid must be 20x20");
   HEIST_REQUIRE(heist_train_conv_frag_floats(layer, mode) > 0, "heist_train_conv: layer 1 (mode 0), 2 or 3");
   HEIST_REQUIRE(n >= 0, "heist_train_conv: n < 0");
   HEIST_REQUIRE(x && frag && y && queue, "heist_train_conv: null pointer");
-  HEIST_REQUIRE(mode == 0 ? bias != nullptr : mask != nullptr, "heist_train_conv: mode 0 needs bias, mode 1 mask");
-  for (const void* p : {(const void*)x, (const void*)frag, (const void*)y, mode ? (const void*)mask : (const void*)bias})
+  HEIST_REQUIRE(mode == 0 ? bias != nullptr : mask_bits != nullptr, "heist_train_conv: mode 0 needs bias, mode 1 mask_bits");
+  for (const void* p : {(const void*)x, (const void*)frag, (const void*)y, mode ? (const void*)mask_bits : (const void*)bias})
     HEIST_REQUIRE(((uintptr_t)p & 15) == 0, "heist_train_conv: 16-byte alignment");
   if (n == 0) return 0;
-  return check_hip(heist::launch_train_conv(layer, mode, x, n, rows, cols, frag, bias, mask, y, queue,
+  return check_hip(heist::launch_train_conv(layer, mode, x, n, rows, cols, frag, bias, mask_bits, y, queue,
                                             (hipStream_t)stream),
                    "heist_train_conv");
 }
@@ -874,13 +874,13 @@ int heist_train_pool(const float* a3, int n, int rows, int cols, float* feat, he
   return check_hip(heist::launch_train_pool(a3, n, rows, cols, feat, (hipStream_t)stream), "heist_train_pool");
 }
 
-int heist_train_pool_bwd(const float* dfeat, const float* a3, int n, int rows, int cols, float* d3,
+int heist_train_pool_bwd(const float* dfeat, const uint8_t* mask3_bits, int n, int rows, int cols, float* d3,
                          heist_stream_t stream) {
-  HEIST_REQUIRE(dfeat && a3 && d3, "heist_train_pool_bwd: null pointer");
+  HEIST_REQUIRE(dfeat && mask3_bits && d3, "heist_train_pool_bwd: null pointer");
   HEIST_REQUIRE(n >= 0 && rows >= 4 && cols >= 4, "heist_train_pool_bwd: bad sizes");
-  HEIST_REQUIRE(((uintptr_t)a3 & 15) == 0 && ((uintptr_t)d3 & 15) == 0, "heist_train_pool_bwd: 16-byte alignment");
+  HEIST_REQUIRE(((uintptr_t)d3 & 15) == 0, "heist_train_pool_bwd: 16-byte alignment");
   if (n == 0) return 0;
-  return check_hip(heist::launch_train_pool_bwd(dfeat, a3, n, rows, cols, d3, (hipStream_t)stream),
+  return check_hip(heist::launch_train_pool_bwd(dfeat, mask3_bits, n, rows, cols, d3, (hipStream_t)stream),
                    "heist_train_pool_bwd");
 }
 

@@ -25,8 +25,11 @@
 //    D[co][pos] = sum over (tap, ci) of W[co][tap][ci] * X[pos + tap][ci]: the weights are the
 //    MFMA's A operand, held in VGPRs for the whole kernel (144 per lane at 64 -> 64), the
 //    activations its B operand, one ds_read_b128 feeding 4 MFMA k-steps.  Wave w owns one
-//    16-channel output tile of one band of the unit for all its C/4 position tiles.  Epilogue:
-//    forward  y = relu(D + bias) (torch: conv + b rounded, then max(., 0));
+//    16-channel output tile of one band of the unit for all its C/4 position tiles; a lane ends
+//    with 4 consecutive channels of one position per tile (one 16-byte store).  (The transposed
+//    orientation, D[pos][co] with the activations as A, would let a pool MFMA sum over the
+//    positions of D's rows; measured 3-8 % slower on every pass, it was not kept.)  Epilogue:
+//    forward  y = relu(D + bias) (torch: conv + b rounded, then max(., 0)), and the ReLU mask bits;
 //    backward d = (a > 0) ? D : 0 with a the saved activation of the layer below (threshold_
 //             backward on the saved output), the data gradient being the convolution with the
 //             transposed, flipped weights (packed by conv_pack_kernel).
@@ -73,6 +76,7 @@ __device__ __forceinline__ void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" :
 __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
 
 typedef __attribute__((address_space(3))) float lds_float;
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
 typedef __attribute__((address_space(3))) f4 lds_f4_t;
 typedef __attribute__((address_space(3))) f2 lds_f2_t;
 
@@ -138,11 +142,16 @@ __device__ __forceinline__ void load_band(const float* x, float* img, int gb, in
 //   CI, CO input / output channels; S: the k (input channel) range split over S waves whose
 //   partial tiles are summed through LDS (S = 2 for 32 output channels, so that 8 waves have
 //   work); MODE 0 forward (bias, ReLU), 1 data gradient (mask by the saved activation > 0).
+//   ReLU masks travel as bits: [n][R][C][CO / 4] uint8, bit r of byte k = channel 4 k + r > 0
+//   (a lane's own 4 channels: no cross-lane gather).  The forward writes its output's
+//   (mask_out, optional); the data gradient reads its output channels' (mask_in: the layer
+//   below's), DMA'd into LDS with the band, so its epilogue waits for no global load.
 struct ConvAArgs {
   const float* x;       // [n][R][C][PI]
   const float* frag;    // packed weights (conv_pack_kernel)
   const float* bias;    // [CO] (MODE 0)
-  const float* mask;    // [n][R][C][PO] (MODE 1)
+  const uint8_t* mask_in;  // [n][R][C][CO / 4] (MODE 1)
+  uint8_t* mask_out;       // [n][R][C][CO / 4] or null (MODE 0)
   float* y;             // [n][R][C][PO]
   int* queue;           // [2]: units drawn, workgroups done (zero between launches: queue_exit)
   int n;
@@ -153,10 +162,13 @@ struct ConvAGeom {
   static constexpr int PI = Pitch<CI>::v, PO = Pitch<CO>::v, NCT = CO / 16, BPU = 8 / (NCT * S);
   static constexpr int PT = C / 4, RP = C + 2, NB = R / 4;
   static constexpr int BAND_F = 6 * RP * PI, BUF_F = BPU * BAND_F;
+  static constexpr int MASK_B = 4 * C * CO / 4;            // mask bytes per band (MODE 1)
+  static constexpr int MASK_F = MODE == 1 ? BPU * MASK_B / 4 : 0;  // floats per buffer
   static constexpr int KBW = CI == 4 ? 1 : (CI / 16) / S;  // 16-channel blocks per tap of a wave
   static constexpr int NWR = CI == 4 ? 9 : 36 * KBW;       // weight registers per lane
-  static constexpr int LDS = 2 * BUF_F * 4 + 64;
+  static constexpr int LDS = 2 * (BUF_F + MASK_F) * 4 + 64;
   static_assert(NCT * S * BPU == 8, "8 waves");
+  static_assert(MASK_B % 16 == 0, "mask rows are whole DMA lanes");
   static_assert(C % 4 == 0 && R % 4 == 0, "bands of 4 rows, tiles of 16 positions");
   static_assert(S == 1 || (PT * 256 <= C * PI && BPU * NCT <= 6), "a wave's k-split partials fit in a row interior");
 };
@@ -169,7 +181,8 @@ __global__ __launch_bounds__(kThreads, 1) void conv_a_kernel(ConvAArgs a) {
   extern __shared__ f4 smem4[];
   float* smem = reinterpret_cast<float*>(smem4);
   float* buf[2] = {smem, smem + G::BUF_F};
-  int* slot = reinterpret_cast<int*>(smem + 2 * G::BUF_F);
+  float* mbuf = smem + 2 * G::BUF_F;  // [2][BPU][MASK_B] uint8 (MODE 1)
+  int* slot = reinterpret_cast<int*>(smem + 2 * (G::BUF_F + G::MASK_F));
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c = wid % NCT, s = (wid / NCT) % S, bslot = wid / (NCT * S);
@@ -194,7 +207,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv_a_kernel(ConvAArgs a) {
       }
     }
   }
-  f4 bias4 = {0.f, 0.f, 0.f, 0.f};
+  f4 bias4 = {0.f, 0.f, 0.f, 0.f};  // this lane's output channels 16 c + 4 g + r
   if constexpr (MODE == 0) bias4 = *reinterpret_cast<const f4*>(a.bias + 16 * c + 4 * g);
 
   zero_range(smem, 2 * G::BUF_F * 4, wid, lane);  // border columns stay zero for the whole kernel
@@ -204,13 +217,19 @@ __global__ __launch_bounds__(kThreads, 1) void conv_a_kernel(ConvAArgs a) {
   }
   __syncthreads();
   int cur = slot[0], nxt = slot[1];
-  auto issue = [&](int u, float* img0) {
+  auto issue = [&](int u, int par) {
     for (int bb = 0; bb < BPU; ++bb) {
       const int gb = u * BPU + bb;
-      if (gb < nbands) load_band<CI, R, C>(a.x, img0 + bb * G::BAND_F, gb, bb * 7, wid, lane);
+      if (gb >= nbands) continue;
+      load_band<CI, R, C>(a.x, buf[par] + bb * G::BAND_F, gb, bb * 7, wid, lane);
+      if constexpr (MODE == 1) {
+        const int smp = gb / NB, y0 = (gb % NB) * 4;
+        dma_range(reinterpret_cast<const float*>(a.mask_in + ((size_t)smp * R + y0) * C * (CO / 4)),
+                  mbuf + (par * BPU + bb) * (G::MASK_B / 4), G::MASK_B, 3 + bb, wid, lane);
+      }
     }
   };
-  if (cur < nunits) issue(cur, buf[0]);
+  if (cur < nunits) issue(cur, 0);
   // per-lane LDS offsets of the position tiles (tap (0, 0) corner, channel group g)
   int pbase[PT];
 #pragma unroll
@@ -222,7 +241,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv_a_kernel(ConvAArgs a) {
     float* img = buf[it & 1] + bslot * G::BAND_F;
     wait_dma();
     __syncthreads();  // the unit's images are in LDS; everyone is done with the other buffer
-    if (nxt < nunits) issue(nxt, buf[(it + 1) & 1]);
+    if (nxt < nunits) issue(nxt, (it + 1) & 1);
     if (tid == 0) slot[2 + (it & 1)] = atomicAdd(a.queue, 1);
     const int gb = cur * BPU + bslot;
     f4 acc[PT];
@@ -267,22 +286,31 @@ __global__ __launch_bounds__(kThreads, 1) void conv_a_kernel(ConvAArgs a) {
         for (int t = 0; t < PT; ++t) acc[t] += lds_f4(part, t * 256 + lane * 4);
     }
     if (s == 0 && gb < nbands) {
+      // D[co][pos]: lane (j, g) holds channels 16 c + 4 g + r of band position 16 t + j; the band's
+      // rows are contiguous, so band position q is image position (smp R + y0) C + q
       const int smp = gb / NB, y0 = (gb % NB) * 4;
+      const size_t bandpos = ((size_t)smp * R + y0) * C;
+      const lds_u8* mk = reinterpret_cast<const lds_u8*>(as_lds(mbuf)) + ((it & 1) * BPU + bslot) * G::MASK_B;
 #pragma unroll
       for (int t = 0; t < PT; ++t) {
-        const int q = 16 * t + j, y = y0 + q / C, xx = q % C;
-        const size_t o = (((size_t)smp * R + y) * C + xx) * PO + 16 * c + 4 * g;
+        const int q = 16 * t + j;
+        const size_t pos = bandpos + q;
         f4 v = acc[t];
         if constexpr (MODE == 0) {
           v += bias4;  // conv + b rounded once, then ReLU
+          uint32_t bits = 0;  // bit r: channel 16 c + 4 g + r of position q > 0
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+          for (int r = 0; r < 4; ++r) {
+            bits |= (uint32_t)(v[r] > 0.f) << r;
+            v[r] = v[r] > 0.f ? v[r] : 0.f;
+          }
+          if (a.mask_out) a.mask_out[pos * (CO / 4) + 4 * c + g] = (uint8_t)bits;
         } else {
-          const f4 m = *reinterpret_cast<const f4*>(a.mask + o);
+          const uint32_t bits = (uint32_t)mk[q * (CO / 4) + 4 * c + g];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = m[r] > 0.f ? v[r] : 0.f;
+          for (int r = 0; r < 4; ++r) v[r] = (bits >> r) & 1u ? v[r] : 0.f;
         }
-        *reinterpret_cast<f4*>(a.y + o) = v;
+        *reinterpret_cast<f4*>(a.y + pos * PO + 16 * c + 4 * g) = v;
       }
     }
     __syncthreads();  // slot written; this buffer free for the unit after next
@@ -589,8 +617,9 @@ __global__ __launch_bounds__(256) void pool_kernel(const float* __restrict__ a3,
   feat[smp * 1024 + co * 16 + cell] = sum / (float)((y1 - y0) * (x1 - x0));
 }
 
-// d3 [n][R][C][68] = (a3 > 0) * (adaptive_avg_pool2d's input gradient of dfeat [n][1024]).
-__global__ __launch_bounds__(256) void pool_bwd_mask_kernel(const float* __restrict__ dfeat, const float* __restrict__ a3,
+// d3 [n][R][C][68] = (a3 > 0) * (adaptive_avg_pool2d's input gradient of dfeat [n][1024]), the
+// mask from conv3's forward bits m3 [n][R][C][16] (uint8 per 4 channels).
+__global__ __launch_bounds__(256) void pool_bwd_mask_kernel(const float* __restrict__ dfeat, const uint8_t* __restrict__ m3,
                                                             int n, int R, int C, float* __restrict__ d3) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (sample, position, channel quad)
   if (e >= (int64_t)n * R * C * 16) return;
@@ -612,10 +641,10 @@ __global__ __launch_bounds__(256) void pool_bwd_mask_kernel(const float* __restr
       for (int r = 0; r < 4; ++r) gsum[r] += df[r * 16] / area;
     }
   }
-  const f4 av = *reinterpret_cast<const f4*>(a3 + pe * 68 + 4 * q);
+  const uint32_t bits = (uint32_t)m3[pe * 16 + q];
   f4 v;
 #pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = av[r] > 0.f ? gsum[r] : 0.f;
+  for (int r = 0; r < 4; ++r) v[r] = (bits >> r) & 1u ? gsum[r] : 0.f;
   *reinterpret_cast<f4*>(d3 + pe * 68 + 4 * q) = v;
 }
 
@@ -658,9 +687,9 @@ static hipError_t launch_a(const tc::ConvAArgs& a, hipStream_t st) {
 // layer: 1 = conv1 (3 -> 32), 2 = conv2 (32 -> 64), 3 = conv3 (64 -> 64); mode 0 forward, 1 data
 // gradient (layers 2, 3: input = the gradient at the layer's output, 64 channels)
 hipError_t launch_train_conv(int layer, int mode, const float* x, int n, int R, int C, const float* frag,
-                             const float* bias, const float* mask, float* y, int* queue, hipStream_t st) {
+                             const float* bias, uint8_t* mask_bits, float* y, int* queue, hipStream_t st) {
   if (R != 20 || C != 20) return hipErrorInvalidValue;
-  const tc::ConvAArgs a{x, frag, bias, mask, y, queue, n};
+  const tc::ConvAArgs a{x, frag, bias, mode == 1 ? mask_bits : nullptr, mode == 0 ? mask_bits : nullptr, y, queue, n};
   if (mode == 0) {
     if (layer == 1) return launch_a<4, 32, 1, 0>(a, st);
     if (layer == 2) return launch_a<32, 64, 1, 0>(a, st);
@@ -741,9 +770,9 @@ hipError_t launch_train_pool(const float* a3, int n, int R, int C, float* feat, 
   return hipGetLastError();
 }
 
-hipError_t launch_train_pool_bwd(const float* dfeat, const float* a3, int n, int R, int C, float* d3, hipStream_t st) {
+hipError_t launch_train_pool_bwd(const float* dfeat, const uint8_t* m3, int n, int R, int C, float* d3, hipStream_t st) {
   const int64_t total = (int64_t)n * R * C * 16;
-  hipLaunchKernelGGL(tc::pool_bwd_mask_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, dfeat, a3, n, R,
+  hipLaunchKernelGGL(tc::pool_bwd_mask_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, dfeat, m3, n, R,
                      C, d3);
   return hipGetLastError();
 }

@@ -99,12 +99,18 @@ def _tc_act(n, R, C, ch, dev) -> torch.Tensor:
     return torch.empty((n, R, C, ch + 4 if ch > 4 else 4), dtype=torch.float32, device=dev)
 
 
+def _tc_mask(n, R, C, ch, dev) -> torch.Tensor:
+    """[n][R][C][ch / 4] ReLU mask bits (uint8: bit r of byte k = channel 4 k + r > 0)."""
+    return torch.empty((n, R, C, ch // 4), dtype=torch.uint8, device=dev)
+
+
 class _BackboneMFMA32(torch.autograd.Function):
     """SolverNetwork's conv stack (networks.py:93-100) forward and backward on the hand-written
     fp32-MFMA kernels (csrc/heist_train_conv.hip, heist_train_* in include/heist.h): conv1-3
-    with bias + ReLU fused in their epilogues, the 4x4 adaptive pool; backward the pool's
-    gradient with conv3's ReLU mask, the data gradients of conv3 and conv2 with the ReLU masks
-    of their inputs fused, and the weight + bias gradients of all three (fixed-order sums).
+    with bias + ReLU fused in their epilogues (which also write each ReLU mask as bits), the
+    4x4 adaptive pool; backward the pool's gradient with conv3's mask, the data gradients of
+    conv3 and conv2 with the masks of their inputs fused, and the weight + bias gradients of all
+    three (fixed-order sums).
     Exact fp32 (MFMA f32 = an fmaf chain); differs from torch / MIOpen by summation order.
     Returns the pooled features [B, 1024]."""
 
@@ -125,12 +131,14 @@ class _BackboneMFMA32(torch.autograd.Function):
         s = x.stride()
         nat.check(L.heist_train_obs_nhwc4(P(x), n, R, C, s[0], s[1], s[2], s[3], P(x4), st), "heist_train_obs_nhwc4")
         a1, a2, a3 = _tc_act(n, R, C, 32, dev), _tc_act(n, R, C, 64, dev), _tc_act(n, R, C, 64, dev)
-        for k, (layer, xi, yo, b) in enumerate(((1, x4, a1, b1), (2, a1, a2, b2), (3, a2, a3, b3))):
-            nat.check(L.heist_train_conv(layer, 0, P(xi), n, R, C, P(frags[k]), P(b.detach().contiguous()), None, P(yo),
-                                         P(q[2 * k:]), st), "heist_train_conv")
+        m1, m2, m3 = _tc_mask(n, R, C, 32, dev), _tc_mask(n, R, C, 64, dev), _tc_mask(n, R, C, 64, dev)
+        for k, (layer, xi, yo, b, mo) in enumerate(((1, x4, a1, b1, m1), (2, a1, a2, b2, m2), (3, a2, a3, b3, m3))):
+            nat.check(L.heist_train_conv(layer, 0, P(xi), n, R, C, P(frags[k]), P(b.detach().contiguous()), P(mo),
+                                         P(yo), P(q[2 * k:]), st), "heist_train_conv")
         feat = torch.empty(n, 1024, dtype=torch.float32, device=dev)
         nat.check(L.heist_train_pool(P(a3), n, R, C, P(feat), st), "heist_train_pool")
-        ctx.save_for_backward(x4, a1, a2, a3, w2, w3)
+        del a3  # only its pool and its mask bits are needed later
+        ctx.save_for_backward(x4, a1, a2, m1, m2, m3, w2, w3)
         ctx.frags = frags  # the forward's packs stay alive until the kernels that read them ran
         return feat
 
@@ -138,7 +146,7 @@ class _BackboneMFMA32(torch.autograd.Function):
     def backward(ctx, dfeat):
         from . import _native as nat
         L = nat.lib()
-        x4, a1, a2, a3, w2, w3 = ctx.saved_tensors
+        x4, a1, a2, m1, m2, m3, w2, w3 = ctx.saved_tensors
         n, R, C = x4.shape[0], x4.shape[1], x4.shape[2]
         dev = x4.device
         st = nat.stream(dev)
@@ -146,7 +154,7 @@ class _BackboneMFMA32(torch.autograd.Function):
         P = lambda t: nat._vp(t.data_ptr())  # noqa: E731
         dfeat = dfeat.contiguous()
         d3 = _tc_act(n, R, C, 64, dev)
-        nat.check(L.heist_train_pool_bwd(P(dfeat), P(a3), n, R, C, P(d3), st), "heist_train_pool_bwd")
+        nat.check(L.heist_train_pool_bwd(P(dfeat), P(m3), n, R, C, P(d3), st), "heist_train_pool_bwd")
         part = torch.empty(int(max(L.heist_train_conv_partial_floats(k, n, R, C) for k in (1, 2, 3))),
                            dtype=torch.float32, device=dev)
         grads = {}
@@ -166,9 +174,9 @@ class _BackboneMFMA32(torch.autograd.Function):
                       "heist_train_conv")
             return d, f
 
-        d2, f3 = dgrad(3, w3, d3, a2, 64, 6)
+        d2, f3 = dgrad(3, w3, d3, m2, 64, 6)
         wgrad(3, d3, a2, 64, 64, 8)
-        d1, f2 = dgrad(2, w2, d2, a1, 32, 10)
+        d1, f2 = dgrad(2, w2, d2, m1, 32, 10)
         wgrad(2, d2, a1, 64, 32, 12)
         wgrad(1, d1, x4, 32, 3, 14)
         del f3, f2  # (stream-ordered: the caching allocator reuses them only behind the kernels)

@@ -189,9 +189,16 @@ def test_mfma_passes_match_torch(gpu_device, n):
         f = torch.empty(L.heist_train_conv_frag_floats(layer, 0), device=dev)
         nat.check(L.heist_train_conv_pack(layer, 0, P(w[layer - 1].contiguous()), P(f), st), "pack")
         y = _tc_act(n, R, C, ch, dev)
-        nat.check(L.heist_train_conv(layer, 0, P(ins[layer]), n, R, C, P(f), P(b[layer - 1]), None, P(y), P(q), st),
+        mo = torch.empty((n, R, C, ch // 4), dtype=torch.uint8, device=dev)
+        nat.check(L.heist_train_conv(layer, 0, P(ins[layer]), n, R, C, P(f), P(b[layer - 1]), P(mo), P(y), P(q), st),
                   "conv")
         _close(back(y, ch), refs[layer], 1e-5, "forward %d" % layer)
+        got = mo.to(torch.int32)[..., None] >> torch.arange(4, device=dev, dtype=torch.int32) & 1
+        assert torch.equal(got.reshape(n, R, C, ch).bool(), (back(y, ch) > 0).permute(0, 2, 3, 1)), layer
+    # the pool of conv3's output (the training forward's form)
+    feat = torch.empty(n, 1024, device=dev)
+    nat.check(L.heist_train_pool(P(ours(a3, 64)), n, R, C, P(feat), st), "pool")
+    _close(feat, F.adaptive_avg_pool2d(a3, (4, 4)).reshape(n, -1), 1e-5, "pool")
     d3 = torch.randn_like(a3) * (a3 > 0)
     gi2, gw3, gb3 = torch.ops.aten.convolution_backward(d3, a2, w[2], [64], [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
                                                         [True, True, True])
@@ -201,7 +208,11 @@ def test_mfma_passes_match_torch(gpu_device, n):
     d1 = gi1 * (a1 > 0)
     _, gw1, gb1 = torch.ops.aten.convolution_backward(d1, x, w[0], [32], [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
                                                       [False, True, True])
-    for layer, dy, mask, ch, ref in ((3, ours(d3, 64), ins[3], 64, d2), (2, ours(d2, 64), ins[2], 32, d1)):
+    def bits(t):  # [n][ch][R][C] -> the ReLU mask bits [n][R][C][ch / 4] (uint8: bit r = channel 4 k + r)
+        b = (t > 0).permute(0, 2, 3, 1).reshape(n, R, C, t.shape[1] // 4, 4).to(torch.int32)
+        return (b << torch.arange(4, device=dev, dtype=torch.int32)).sum(-1).to(torch.uint8).contiguous()
+
+    for layer, dy, mask, ch, ref in ((3, ours(d3, 64), bits(a2), 64, d2), (2, ours(d2, 64), bits(a1), 32, d1)):
         f = torch.empty(L.heist_train_conv_frag_floats(layer, 1), device=dev)
         nat.check(L.heist_train_conv_pack(layer, 1, P(w[layer - 1].contiguous()), P(f), st), "pack")
         y = _tc_act(n, R, C, ch, dev)

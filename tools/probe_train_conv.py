@@ -73,12 +73,13 @@ def main():
         return lambda: nat.check(L.heist_train_conv_wgrad(layer, P(dy), P(xin), n, R, C, P(part), P(dw), P(db), P(q), st),
                                  "wgrad")
     y32, y64 = _tc_act(n, R, C, 32, dev), _tc_act(n, R, C, 64, dev)
+    mk = {c: torch.randint(0, 16, (n, R, C, c // 4), dtype=torch.uint8, device=dev) for c in (32, 64)}
     passes = {
-        "conv1_fwd": (conv(1, 0, x4, frags[(1, 0)], net.conv1.bias, None, y32), flop[1]),
-        "conv2_fwd": (conv(2, 0, acts[32], frags[(2, 0)], net.conv2.bias, None, y64), flop[2]),
-        "conv3_fwd": (conv(3, 0, acts[64], frags[(3, 0)], net.conv3.bias, None, y64), flop[3]),
-        "conv3_dgrad": (conv(3, 1, a3, frags[(3, 1)], None, acts[64], y64), flop[3]),
-        "conv2_dgrad": (conv(2, 1, a3, frags[(2, 1)], None, acts[32], y32), flop[2]),
+        "conv1_fwd": (conv(1, 0, x4, frags[(1, 0)], net.conv1.bias, mk[32], y32), flop[1]),
+        "conv2_fwd": (conv(2, 0, acts[32], frags[(2, 0)], net.conv2.bias, mk[64], y64), flop[2]),
+        "conv3_fwd": (conv(3, 0, acts[64], frags[(3, 0)], net.conv3.bias, mk[64], y64), flop[3]),
+        "conv3_dgrad": (conv(3, 1, a3, frags[(3, 1)], None, mk[64], y64), flop[3]),
+        "conv2_dgrad": (conv(2, 1, a3, frags[(2, 1)], None, mk[32], y32), flop[2]),
         "conv3_wgrad": (wgrad(3, a3, acts[64], 64, 64), flop[3]),
         "conv2_wgrad": (wgrad(2, a3, acts[32], 64, 32), flop[2]),
         "conv1_wgrad": (wgrad(1, acts[32], x4, 32, 3), flop[1]),

@@ -321,6 +321,13 @@ def measure_env_config(dev, R, n, budget, steps=100, warmup=10, K=1, **kw):
     acts = torch.randint(0, 5, (warmup + steps, n), device=dev, dtype=torch.int64)
     K = max(1, min(K, steps))
     _, ms, _, _ = time_env(env, acts, warmup, steps, K, 1, settle_ms=10.0)
+    cnt = torch.zeros(n, dtype=torch.int64, device=dev)  # ray samples per env-step (SURVEY 8(d)'s ALU figure)
+    env.count_samples(cnt)
+    n_count = 20
+    for k in range(n_count):
+        env.step(acts[k])
+    env.count_samples(None)
+    samples = float(cnt.sum().item()) / (n_count * n)
     st = env.export()
     ncam, ngu = float(st["n_cams"].double().mean()), float(st["n_guards"].double().mean())
     b = algorithmic_bytes_per_env_step(R, R, ncam, ngu)
@@ -330,6 +337,7 @@ def measure_env_config(dev, R, n, budget, steps=100, warmup=10, K=1, **kw):
     return {"value": n / (ms * 1e-3), "unit": "env-steps/s", "kernel_ms": ms, "envs": n, "grid": "%dx%d" % (R, R),
             "budget": budget, "mean_cameras": ncam, "mean_guards": ngu, "ticks_per_launch": K,
             "shared_fan_frac": fan,
+            "ray_samples_per_env_step": samples, "ray_samples_per_s": samples * n / (ms * 1e-3),
             "kernel": kname,
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_env_step": b}}
@@ -650,6 +658,7 @@ def main():
                              "max": max(b_step * N / (w * 1e-3) / 1e9 / HBM_PEAK_GBS for w in windows + [kern_ms])},
                          "algorithmic_bytes_per_env_step": b_step,
                          "ray_samples_per_env_step": samples_per_step,
+                         "ray_samples_per_s": samples_per_step * N / (kern_ms * 1e-3),
                          "exact_path_rays_per_env_step": exact_rays_per_step,
                          "host_issue_us_per_step": issue_s / args.steps * 1e6,
                          "note": "achieved = algorithmic bytes per env-step (SURVEY 8d) x envs / mean tick duration "

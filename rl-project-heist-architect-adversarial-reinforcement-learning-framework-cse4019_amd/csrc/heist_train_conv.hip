@@ -257,18 +257,41 @@ __global__ __launch_bounds__(kThreads, 1) void conv_a_kernel(ConvAArgs a) {
           for (int t = 0; t < PT; ++t) xv[t] = lds_f1(img, pbase[t] + toff);
 #pragma unroll
           for (int t = 0; t < PT; ++t) acc[t] = mfma(w[tap], xv[t], acc[t]);
-        } else {
-#pragma unroll
-          for (int cb = 0; cb < KBW; ++cb) {
-            f4 xv[PT];
-#pragma unroll
-            for (int t = 0; t < PT; ++t) xv[t] = lds_f4(img, pbase[t] + toff + 16 * cb);
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-#pragma unroll
-              for (int t = 0; t < PT; ++t) acc[t] = mfma(w[(tap * KBW + cb) * 4 + e], xv[t][e], acc[t]);
-          }
         }
+      }
+      if constexpr (CI != 4) {
+        // (tap, cb) blocks in order, software-pipelined: block b + 1's activations are read
+        // into the other register set before block b's MFMAs, so no MFMA chain waits on
+        // a whole LDS round trip (the compiler, left alone, read two blocks, ran their 40
+        // MFMAs, then read the next two)
+        constexpr int NBK = 9 * KBW;
+        auto boff = [&](int bk) { return ((bk / KBW / 3) * RP + (bk / KBW) % 3) * PI + 16 * (bk % KBW); };
+        f4 xv[2][PT];
+#pragma unroll
+        for (int t = 0; t < PT; ++t) xv[0][t] = lds_f4(img, pbase[t] + boff(0));
+#pragma unroll
+        for (int bk = 0; bk < NBK; ++bk) {
+          if (bk + 1 < NBK) {
+#pragma unroll
+            for (int t = 0; t < PT; ++t) xv[(bk + 1) & 1][t] = lds_f4(img, pbase[t] + boff(bk + 1));
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int t = 0; t < PT; ++t) acc[t] = mfma(w[bk * 4 + e], xv[bk & 1][t][e], acc[t]);
+        }
+#if HEIST_TC_SCHED
+        // the issue order, pinned: block 0's reads, then per block one read of the next block
+        // ahead of every 4 MFMAs (mask 0x100 = LDS read, 0x8 = MFMA)
+        __builtin_amdgcn_sched_group_barrier(0x100, PT, 0);
+#pragma unroll
+        for (int bk = 0; bk < NBK; ++bk)
+#pragma unroll
+          for (int t = 0; t < PT; ++t) {
+            if (bk + 1 < NBK) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+          }
+#endif
       }
     }
     if constexpr (S == 2) {  // k halves: wave s = 1 hands its partial tiles to wave s = 0 through LDS
@@ -618,34 +641,48 @@ __global__ __launch_bounds__(256) void pool_kernel(const float* __restrict__ a3,
 }
 
 // d3 [n][R][C][68] = (a3 > 0) * (adaptive_avg_pool2d's input gradient of dfeat [n][1024]), the
-// mask from conv3's forward bits m3 [n][R][C][16] (uint8 per 4 channels).
+// mask from conv3's forward bits m3 [n][R][C][16] (uint8 per 4 channels).  One workgroup per
+// sample: the sample's 1,024 pooled gradients, each divided by its window's area, go to LDS
+// as [cell][channel] (a channel quad = one ds_read_b128), then the workgroup writes the
+// sample's positions, thread = (position, channel quad), each position's windows summed in
+// (cy, cx) order (the order of torch's adaptive_avg_pool2d backward; one window per position
+// when 4 divides R and C).
 __global__ __launch_bounds__(256) void pool_bwd_mask_kernel(const float* __restrict__ dfeat, const uint8_t* __restrict__ m3,
                                                             int n, int R, int C, float* __restrict__ d3) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;  // (sample, position, channel quad)
-  if (e >= (int64_t)n * R * C * 16) return;
-  const int q = e & 15;
-  const int64_t pe = e >> 4;
-  const int p = (int)(pe % (R * C));
-  const int64_t smp = pe / (R * C);
-  const int y = p / C, x = p % C;
-  f4 gsum = {0.f, 0.f, 0.f, 0.f};
-  for (int cy = 0; cy < 4; ++cy) {
-    const int y0 = win_start(cy, R), y1 = win_end(cy, R);
-    if (y < y0 || y >= y1) continue;
-    for (int cx = 0; cx < 4; ++cx) {
-      const int x0 = win_start(cx, C), x1 = win_end(cx, C);
-      if (x < x0 || x >= x1) continue;
-      const float area = (float)((y1 - y0) * (x1 - x0));
-      const float* df = dfeat + smp * 1024 + (4 * q) * 16 + cy * 4 + cx;
+  __shared__ f4 g[16 * 16];  // [cell][channel quad]
+  const int smp = blockIdx.x, tid = threadIdx.x;
+  {
+    const int cell = tid & 15, qd = tid >> 4;  // reads dfeat[(4 qd + r) * 16 + cell]
+    const int cy = cell >> 2, cx = cell & 3;
+    const float area = (float)((win_end(cy, R) - win_start(cy, R)) * (win_end(cx, C) - win_start(cx, C)));
+    const float* df = dfeat + (int64_t)smp * 1024 + (4 * qd) * 16 + cell;
+    f4 v;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) gsum[r] += df[r * 16] / area;
-    }
+    for (int r = 0; r < 4; ++r) v[r] = df[r * 16] / area;
+    g[cell * 16 + qd] = v;
   }
-  const uint32_t bits = (uint32_t)m3[pe * 16 + q];
-  f4 v;
+  __syncthreads();
+  const int npos = R * C;
+  const int64_t base = (int64_t)smp * npos;
+  for (int it = tid; it < npos * 16; it += 256) {
+    const int q = it & 15, p = it >> 4;
+    const int y = p / C, x = p - (p / C) * C;
+    f4 gsum = {0.f, 0.f, 0.f, 0.f};
+    for (int cy = 0; cy < 4; ++cy) {
+      if (y < win_start(cy, R) || y >= win_end(cy, R)) continue;
+      for (int cx = 0; cx < 4; ++cx) {
+        if (x < win_start(cx, C) || x >= win_end(cx, C)) continue;
+        const f4 t = g[(cy * 4 + cx) * 16 + q];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = (bits >> r) & 1u ? gsum[r] : 0.f;
-  *reinterpret_cast<f4*>(d3 + pe * 68 + 4 * q) = v;
+        for (int r = 0; r < 4; ++r) gsum[r] += t[r];
+      }
+    }
+    const uint32_t bits = (uint32_t)m3[(base + p) * 16 + q];
+    f4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = (bits >> r) & 1u ? gsum[r] : 0.f;
+    *reinterpret_cast<f4*>(d3 + (base + p) * 68 + 4 * q) = v;
+  }
 }
 
 }  // namespace tc
@@ -771,9 +808,8 @@ hipError_t launch_train_pool(const float* a3, int n, int R, int C, float* feat, 
 }
 
 hipError_t launch_train_pool_bwd(const float* dfeat, const uint8_t* m3, int n, int R, int C, float* d3, hipStream_t st) {
-  const int64_t total = (int64_t)n * R * C * 16;
-  hipLaunchKernelGGL(tc::pool_bwd_mask_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, dfeat, m3, n, R,
-                     C, d3);
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(tc::pool_bwd_mask_kernel, dim3((unsigned)n), dim3(256), 0, st, dfeat, m3, n, R, C, d3);
   return hipGetLastError();
 }
 

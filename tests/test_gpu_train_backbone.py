@@ -199,6 +199,19 @@ def test_mfma_passes_match_torch(gpu_device, n):
     feat = torch.empty(n, 1024, device=dev)
     nat.check(L.heist_train_pool(P(ours(a3, 64)), n, R, C, P(feat), st), "pool")
     _close(feat, F.adaptive_avg_pool2d(a3, (4, 4)).reshape(n, -1), 1e-5, "pool")
+    # its backward with conv3's ReLU mask (written by the forward above): window / area, masked
+    dfeat = torch.randn(n, 1024, device=dev)
+    m3 = torch.empty((n, R, C, 16), dtype=torch.uint8, device=dev)
+    nat.check(L.heist_train_conv(3, 0, P(ins[3]), n, R, C, P(f), P(b[2]), P(m3), P(_tc_act(n, R, C, 64, dev)), P(q), st),
+              "conv3 mask")
+    dp = _tc_act(n, R, C, 64, dev)
+    nat.check(L.heist_train_pool_bwd(P(dfeat), P(m3), n, R, C, P(dp), st), "pool_bwd")
+    ap = a3.detach().clone().requires_grad_(True)
+    F.adaptive_avg_pool2d(ap, (4, 4)).reshape(n, -1).backward(dfeat)
+    mask3 = (m3.to(torch.int32)[..., None] >> torch.arange(4, device=dev, dtype=torch.int32) & 1).reshape(n, R, C, 64)
+    # (torch divides by the window's height, then its width: a last-bit difference)
+    _close(back(dp, 64), ap.grad * mask3.permute(0, 3, 1, 2).to(ap.grad.dtype), 1e-6, "pool backward")
+    assert torch.equal(back(dp, 64) != 0, (ap.grad * mask3.permute(0, 3, 1, 2)) != 0), "pool backward mask"
     d3 = torch.randn_like(a3) * (a3 > 0)
     gi2, gw3, gb3 = torch.ops.aten.convolution_backward(d3, a2, w[2], [64], [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
                                                         [True, True, True])

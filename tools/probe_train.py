@@ -70,6 +70,48 @@ def main():
     parts["train_iteration_overlapped"] = time.perf_counter() - t0
     res["parts_s"] = parts
     res["layouts_scored"] = int(len(done_ids))
+    # CU theft: the Architect's sequence holds 64 whole CUs while the Solver's update runs on
+    # the rest.  The update by HIP events on the main stream, alone (the Architect's sequence
+    # after it) and with the sequence launched just before it on the side stream (the
+    # iteration's order); the sequence by events on its own stream.
+    main = torch.cuda.current_stream(dev)
+    theft = {}
+    for mode in ("alone", "beside_architect", "alone", "beside_architect"):
+        ro = tr._rollout(T)
+        done = tr._score_finished()
+        k = len(tr.architect.rewards)
+        torch.cuda.synchronize()
+        side = tr.architect.side_stream()
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        pend = None
+        if mode == "beside_architect" and side is not None:
+            side.wait_stream(main)
+            for buf in (tr.architect.log_probs, tr.architect.values):
+                ts = buf.tensors() if hasattr(buf, "tensors") else [x for x in buf if torch.is_tensor(x)]
+                for t_ in ts:
+                    if t_.is_cuda:
+                        t_.record_stream(side)
+            with torch.cuda.stream(side):
+                e[2].record(side)
+                pend = tr._architect_step(defer=True, join=main)
+                e[3].record(side)
+        e[0].record(main)
+        tr.solver.update_rollout(ro, minibatch=mb)
+        e[1].record(main)
+        torch.cuda.synchronize()
+        row = {"solver_update_ms": e[0].elapsed_time(e[1]), "architect_updates": k}
+        if pend is not None:
+            pend()
+            row["architect_ms"] = e[2].elapsed_time(e[3])
+        else:
+            t0 = time.perf_counter()
+            tr._architect_step()
+            torch.cuda.synchronize()
+            row["architect_ms_serial_wall"] = (time.perf_counter() - t0) * 1e3
+        tr._arch_eps = []
+        tr._assign_layouts(done)
+        theft.setdefault(mode, []).append(row)
+    res["cu_theft"] = theft
     res["rollout_steps_per_s"] = n * T / res["rollout_s"]
     res["train_steps_per_s"] = n * T / res["iteration_s"]
     print(json.dumps(res), flush=True)

@@ -292,13 +292,16 @@ def measure_rollout(env, dev, steps=20, warmup=3, precision="bf16"):
     torch.cuda.synchronize(dev)
     dt = time.perf_counter() - t0
     tf = solver_backbone_flop(env.rows) * steps * env.n_envs / dt / 1e12  # rollout MFMA fraction
+    peak = MFMA_BF16_PEAK_TFLOPS if precision == "bf16" else MFMA_FP32_PEAK_TFLOPS
     return {"value": steps * env.n_envs / dt, "unit": "env-steps/s", "ms_per_step": dt / steps * 1e3,
-            "mfma_roofline": {"achieved": tf, "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                              "frac": tf / MFMA_BF16_PEAK_TFLOPS,
+            "mfma_roofline": {"achieved": tf, "peak": peak, "unit": "TFLOP/s", "frac": tf / peak,
+                              "peak_dtype": precision,
                               "note": "algorithmic conv-backbone flops of the policy forward per env-step"},
-            "dtype": "bf16 MFMA policy (fp32 accumulate)" if precision == "bf16" else "fp32 policy (PyTorch-ROCm)",
+            "dtype": "bf16 MFMA policy (fp32 accumulate)" if precision == "bf16" else
+                     "fp32 policy (exact-fp32 MFMA conv backbone)",
             "note": ("heist_step + fused Solver select_action (backbone + head kernels)" if precision == "bf16" else
-                     "heist_step + reference fp32 select_action (MIOpen convs, fused-gate LSTM)") +
+                     "heist_step + fp32 select_action (conv backbone on the fp32-MFMA training kernels at "
+                     "20x20, fused-gate LSTM; the fp32 matrix peak bounds it at ~3.5 M env-steps/s)") +
                     ", carried LSTM state"}
 
 
@@ -349,6 +352,7 @@ def solver_backbone_flop(R):  # conv1..3 MACs x 2 per env at R x R (algorithmic,
 
 SOLVER_BACKBONE_FLOP = solver_backbone_flop(20)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X dense bf16 (MI355X_MICROARCH.md)
+MFMA_FP32_PEAK_TFLOPS = 157.3   # MI355X fp32 matrix (v_mfma_f32_*_f32)
 
 
 def measure_policy(dev, n, iters=50, warmup=5, R=20, settle_ms=100.0):
@@ -441,9 +445,13 @@ def measure_train(cfg, dev, n_envs, rollout_len=32, minibatch=16384, update_prec
             "dtype": "rollout %s, update %s" % (rollout_precision, update_precision),
             "solver_optimizer_steps_per_iteration": outs[-1].get("solver_updates"),
             "config": "T=%d x %d envs/GPU x %d GPU%s, %s phase (budget %d), 3 epochs, minibatch %d per rank; rollout "
-                      "policy %s, PPO update %s (NHWC MIOpen convs)%s"
+                      "policy %s, PPO update %s%s"
                       % (rollout_len, n_envs, world, "s" if world > 1 else "", phase, budget, minibatch,
-                         "bf16 fused kernels" if rollout_precision == "bf16" else "fp32", update_precision,
+                         "bf16 fused kernels" if rollout_precision == "bf16" else
+                         "fp32 (conv backbone on the fp32-MFMA kernels at 20x20)", update_precision +
+                         (" (conv backbone forward + backward on the hand-written fp32-MFMA kernels, heist_train_conv*, "
+                          "at 20x20; MIOpen elsewhere)" if update_precision == "fp32" else
+                          " (autocast: NHWC MIOpen convs)"),
                          "; one flat RCCL/gloo all-reduce of the Solver gradients per optimizer step" if multi
                          else "")}
 

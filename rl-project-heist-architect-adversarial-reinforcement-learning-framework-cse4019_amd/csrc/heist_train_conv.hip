@@ -46,6 +46,10 @@
 
 #pragma clang fp contract(off)
 
+#ifndef HEIST_TC_PADW
+#define HEIST_TC_PADW 1  // conv1's activation rows written whole, pad words included (A/B: -DHEIST_TC_PADW=0)
+#endif
+
 namespace heist {
 namespace tc {
 
@@ -334,6 +338,11 @@ __global__ __launch_bounds__(kThreads, 1) void conv_a_kernel(ConvAArgs a) {
           for (int r = 0; r < 4; ++r) v[r] = (bits >> r) & 1u ? v[r] : 0.f;
         }
         *reinterpret_cast<f4*>(a.y + pos * PO + 16 * c + 4 * g) = v;
+        // conv1's forward (memory-bound) writes the position's 4 pad words as well (zeros, never
+        // read): whole 128-B lines, no read-modify-write of a partly written line (0.445 ->
+        // 0.346 ms at 16,384 samples); in the MFMA-bound passes the extra store cost 0.3-1.2 %
+        if constexpr (HEIST_TC_PADW && CI == 4)
+          if (c == NCT - 1 && g == 3) *reinterpret_cast<f4*>(a.y + pos * PO + CO) = f4{0.f, 0.f, 0.f, 0.f};
       }
     }
     __syncthreads();  // slot written; this buffer free for the unit after next
@@ -640,6 +649,24 @@ __global__ __launch_bounds__(256) void pool_kernel(const float* __restrict__ a3,
   feat[smp * 1024 + co * 16 + cell] = sum / (float)((y1 - y0) * (x1 - x0));
 }
 
+// The same for R = C = 20 (windows of 5 x 5): the window's 25 loads unrolled, all in flight
+// before the first add (the rolled loop above waits for each load before the next), summed in
+// the same row-major order.
+__global__ __launch_bounds__(256) void pool20_kernel(const float* __restrict__ a3, int n, float* __restrict__ feat) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)n * 1024) return;
+  const int co = e & 63, cell = (e >> 6) & 15;
+  const int64_t smp = e >> 10;
+  const float* s = a3 + (smp * 400 + (cell >> 2) * 5 * 20 + (cell & 3) * 5) * 68 + co;
+  float v[25];
+#pragma unroll
+  for (int i = 0; i < 25; ++i) v[i] = s[((i / 5) * 20 + i % 5) * 68];
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 25; ++i) sum += v[i];
+  feat[smp * 1024 + co * 16 + cell] = sum / 25.f;
+}
+
 // d3 [n][R][C][68] = (a3 > 0) * (adaptive_avg_pool2d's input gradient of dfeat [n][1024]), the
 // mask from conv3's forward bits m3 [n][R][C][16] (uint8 per 4 channels).  One workgroup per
 // sample: the sample's 1,024 pooled gradients, each divided by its window's area, go to LDS
@@ -650,7 +677,11 @@ __global__ __launch_bounds__(256) void pool_kernel(const float* __restrict__ a3,
 __global__ __launch_bounds__(256) void pool_bwd_mask_kernel(const float* __restrict__ dfeat, const uint8_t* __restrict__ m3,
                                                             int n, int R, int C, float* __restrict__ d3) {
   __shared__ f4 g[16 * 16];  // [cell][channel quad]
+  extern __shared__ uint4 mk[];  // the sample's mask bits, one 16-byte row per position
   const int smp = blockIdx.x, tid = threadIdx.x;
+  // the mask rows first, all loads in flight (one per position), so the store loop below
+  // waits on no global load
+  for (int p = tid; p < R * C; p += 256) mk[p] = reinterpret_cast<const uint4*>(m3)[(int64_t)smp * R * C + p];
   {
     const int cell = tid & 15, qd = tid >> 4;  // reads dfeat[(4 qd + r) * 16 + cell]
     const int cy = cell >> 2, cx = cell & 3;
@@ -677,11 +708,14 @@ __global__ __launch_bounds__(256) void pool_bwd_mask_kernel(const float* __restr
         for (int r = 0; r < 4; ++r) gsum[r] += t[r];
       }
     }
-    const uint32_t bits = (uint32_t)m3[(base + p) * 16 + q];
+    const uint32_t bits = (uint32_t)reinterpret_cast<const uint8_t*>(mk)[p * 16 + q];
     f4 v;
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = (bits >> r) & 1u ? gsum[r] : 0.f;
     *reinterpret_cast<f4*>(d3 + (base + p) * 68 + 4 * q) = v;
+    // the row's 4 pad words too, so every 128-B line of the rows is written whole (a line
+    // left partly unwritten costs the memory system a read-modify-write)
+    if (q == 15) *reinterpret_cast<f4*>(d3 + (base + p) * 68 + 64) = f4{0.f, 0.f, 0.f, 0.f};
   }
 }
 
@@ -803,13 +837,19 @@ hipError_t launch_obs_nhwc4(const float* obs, int n, int R, int C, const int64_t
 
 hipError_t launch_train_pool(const float* a3, int n, int R, int C, float* feat, hipStream_t st) {
   const int64_t total = (int64_t)n * 1024;
+  if (R == 20 && C == 20) {
+    hipLaunchKernelGGL(tc::pool20_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a3, n, feat);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(tc::pool_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a3, n, R, C, feat);
   return hipGetLastError();
 }
 
 hipError_t launch_train_pool_bwd(const float* dfeat, const uint8_t* m3, int n, int R, int C, float* d3, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(tc::pool_bwd_mask_kernel, dim3((unsigned)n), dim3(256), 0, st, dfeat, m3, n, R, C, d3);
+  if (R * C * 16 > 48 * 1024 || (reinterpret_cast<uintptr_t>(m3) & 15)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(tc::pool_bwd_mask_kernel, dim3((unsigned)n), dim3(256), (size_t)R * C * 16, st, dfeat, m3, n, R, C,
+                     d3);
   return hipGetLastError();
 }
 

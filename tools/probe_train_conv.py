@@ -87,6 +87,18 @@ def main():
     for name, (fn, fl) in passes.items():
         ms = timed(fn, dev)
         out[name] = {"ms": ms, "tflops": fl / ms / 1e9, "frac": fl / ms / 1e9 / PEAK}
+    # the adaptive pool and its backward (HBM passes: a3 read / d3 written, 68-float rows)
+    feat = torch.empty(n, 1024, device=dev)
+    dfeat = torch.rand(n, 1024, device=dev)
+    d3 = _tc_act(n, R, C, 64, dev)
+    act_bytes = n * R * C * 68 * 4
+    mem = {"pool": (lambda: nat.check(L.heist_train_pool(P(a3), n, R, C, P(feat), st), "pool"), act_bytes),
+           "pool_bwd": (lambda: nat.check(L.heist_train_pool_bwd(P(dfeat), P(mk[64]), n, R, C, P(d3), st), "pool_bwd"),
+                        act_bytes + n * R * C * 16)}
+    mem_out = {}
+    for name, (fn, b) in mem.items():
+        ms = timed(fn, dev)
+        mem_out[name] = {"ms": ms, "gbs": b / ms / 1e6}
     # MIOpen on the same shapes (channels-last fp32), the path the MFMA kernels replace
     xs = {c: torch.rand(n, c, R, C, device=dev).contiguous(memory_format=torch.channels_last) for c in (3, 32, 64)}
     gy = {c: torch.rand(n, c, R, C, device=dev).contiguous(memory_format=torch.channels_last) for c in (32, 64)}
@@ -113,7 +125,7 @@ def main():
         out[name]["miopen_frac"] = fl / ms / 1e9 / PEAK
     tot = sum(v["ms"] for v in out.values())
     tot_mi = sum(v["miopen_ms"] for v in out.values())
-    print(json.dumps({"n": n, "passes": out, "sum_ms": tot, "sum_miopen_ms": tot_mi,
+    print(json.dumps({"n": n, "passes": out, "pool_passes": mem_out, "sum_ms": tot, "sum_miopen_ms": tot_mi,
                       "flop_per_step": 3 * sum(flop.values()) - flop[1]}), flush=True)
 
 

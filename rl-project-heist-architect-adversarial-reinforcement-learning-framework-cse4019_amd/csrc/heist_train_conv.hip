@@ -362,9 +362,10 @@ __global__ __launch_bounds__(kThreads, 1) void conv_a_kernel(ConvAArgs a) {
 //   channel ci = col_ci(j, h, qq) -- a bank-conflict-free assignment: the 16 lanes of a k group
 //   read QW consecutive words each, and the next k group (the next position, 4 banks further)
 //   lands on the banks this one leaves free (ds_read_b64: 2 x 32-lane groups; ds_read_b32: 32
-//   banks).  CI == 4: wave (m, kg) takes every 4th k-step (k group kg) for all three column
-//   tiles of the 36 (tap, ci) pairs and the bias tile; the four k groups' tiles are summed in a
-//   fixed order through LDS at the chunk's end.
+//   banks).  CI == 4: wave (m, kg) takes every 4th k-step (k group kg) for both column tiles:
+//   columns 0..26 the 27 (tap, ci) pairs of the 3 real input channels, column 27 the bias
+//   (B operand 1.0), 28..31 zero; the four k groups' tiles are summed in a fixed order through
+//   LDS at the chunk's end.
 struct ConvWArgs {
   const float* dy;
   const float* x;
@@ -380,17 +381,17 @@ struct ConvWGeom {
   static constexpr int BPI = CI == 4 ? 4 : 1;           // bands per iteration (one LDS buffer)
   static constexpr int XB_F = 6 * RP * PI, DB_F = 4 * C * PD, BUF_F = BPI * (XB_F + DB_F);
   static constexpr int QW = CI == 4 ? 1 : (CI / 16) / WPM;   // input channels per lane per tap
-  static constexpr int NTW = CI == 4 ? 3 : 9 * QW;           // column tiles per wave
-  static constexpr int NT_ALL = CI == 4 ? 3 : 9 * (CI / 16); // column tiles per row tile
+  static constexpr int NTW = CI == 4 ? 2 : 9 * QW;           // column tiles per wave
+  static constexpr int NT_ALL = CI == 4 ? 2 : 9 * (CI / 16); // column tiles per row tile
   static constexpr int WSZ = MT * NT_ALL * 256 + CO;         // partial floats per chunk
   static constexpr int LDS = 2 * BUF_F * 4 + 64;
   static_assert(CI == 4 ? WPM == 4 : (CI / 16) % WPM == 0, "wave split");
   static_assert(kChunkBands % BPI == 0, "whole iterations per chunk");
-  static_assert(CI != 4 || 8 * 4 * 256 <= BPI * DB_F, "the k groups' partial tiles fit the dY images");
+  static_assert(CI != 4 || 8 * 2 * 256 <= BPI * DB_F, "the k groups' partial tiles fit the dY images");
 };
 
 // Input channel of column j of the wave's tile qq (CI >= 32, wave half h); for CI == 4 the
-// column jj = 16 tile + j is the pair (tap jj / 4, ci jj % 4).
+// column jj = 16 tile + j < 27 is the pair (tap jj / 3, ci jj % 3), 27 the bias.
 template <int CI>
 __host__ __device__ constexpr int col_ci(int j, int h, int qq) {
   return CI == 64 ? 8 * (j >> 1) + 2 * (j & 1) + 4 * h + qq : 8 * (j >> 2) + (j & 3) + 4 * h;
@@ -409,16 +410,18 @@ __global__ __launch_bounds__(kThreads, 1) void conv_w_kernel(ConvWArgs a) {
   const int m = wid % MT, h = wid / MT;  // CI == 4: h is the k group
   const int j = lane & 15, g = lane >> 4;
   const int nbands = a.n * NB, nchunks = (nbands + kChunkBands - 1) / kChunkBands;
-  const bool has_bias = CI == 4 ? true : h == 0;
+  const bool has_bias = CI == 4 ? false : h == 0;  // (CI == 4: the bias is column 27)
 
   // this lane's column offsets within a position (word units)
-  int coff[CI == 4 ? 3 : QW];
-  bool cval[3] = {true, true, true};
+  int coff[CI == 4 ? 2 : QW];
+  bool cval[2] = {true, true};
+  float cfix[2] = {0.f, 0.f};  // CI == 4: the B value of a column that is not a (tap, ci) pair
   if constexpr (CI == 4) {
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      const int jj = 16 * t + j, tap = jj / 4, ci = jj % 4;
-      cval[t] = jj < 36;
+    for (int t = 0; t < 2; ++t) {
+      const int jj = 16 * t + j, tap = jj / 3, ci = jj % 3;
+      cval[t] = jj < 27;
+      cfix[t] = jj == 27 ? 1.0f : 0.f;
       coff[t] = cval[t] ? ((tap / 3) * RP + tap % 3) * PI + ci : 0;
     }
   } else {
@@ -480,7 +483,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv_w_kernel(ConvWArgs a) {
           const int xb = (y * RP + xx) * PI;
           if constexpr (CI == 4) {
 #pragma unroll
-            for (int t = 0; t < 3; ++t) acc[t] = mfma(av, cval[t] ? lds_f1(xi, xb + coff[t]) : 0.f, acc[t]);
+            for (int t = 0; t < 2; ++t) acc[t] = mfma(av, cval[t] ? lds_f1(xi, xb + coff[t]) : cfix[t], acc[t]);
           } else {
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
@@ -501,24 +504,23 @@ __global__ __launch_bounds__(kThreads, 1) void conv_w_kernel(ConvWArgs a) {
     // this chunk's partial: tiles [m][tile][lane][4], then the bias [CO]
     float* p = a.partial + (size_t)chunk * G::WSZ;
     if constexpr (CI == 4) {
-      // the k groups' tiles (3 column tiles + the bias tile each) summed in k-group order through
-      // the dY images of the buffer this iteration read (everyone is done with it after the
-      // barrier; the next DMA into it is issued after the next iteration's first barrier)
+      // the k groups' 2 column tiles summed in k-group order through the dY images of the
+      // buffer this iteration read (everyone is done with it after the barrier; the next DMA
+      // into it is issued after the next iteration's first barrier)
       __syncthreads();
       float* scr = smem + ((it - 1) & 1) * G::BUF_F + BPI * G::XB_F;
-      float* mine = scr + (m * 4 + h) * 4 * 256;
+      float* mine = scr + (m * 4 + h) * 2 * 256;
 #pragma unroll
-      for (int t = 0; t < 3; ++t) *reinterpret_cast<f4*>(mine + t * 256 + lane * 4) = acc[t];
-      *reinterpret_cast<f4*>(mine + 3 * 256 + lane * 4) = accb;
+      for (int t = 0; t < 2; ++t) *reinterpret_cast<f4*>(mine + t * 256 + lane * 4) = acc[t];
       __syncthreads();
       if (h == 0) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          f4 v = lds_f4(scr, (m * 4 * 4 + t) * 256 + lane * 4);
+        for (int t = 0; t < 2; ++t) {
+          f4 v = lds_f4(scr, (m * 4 * 2 + t) * 256 + lane * 4);
 #pragma unroll
-          for (int k = 1; k < 4; ++k) v += lds_f4(scr, ((m * 4 + k) * 4 + t) * 256 + lane * 4);
-          if (t < 3) *reinterpret_cast<f4*>(p + ((size_t)m * 3 + t) * 256 + lane * 4) = v;
-          else if (j == 0) *reinterpret_cast<f4*>(p + MT * G::NT_ALL * 256 + 16 * m + 4 * g) = v;
+          for (int k = 1; k < 4; ++k) v += lds_f4(scr, ((m * 4 + k) * 2 + t) * 256 + lane * 4);
+          *reinterpret_cast<f4*>(p + ((size_t)m * 2 + t) * 256 + lane * 4) = v;
+          if (t == 1 && j == 11) *reinterpret_cast<f4*>(p + MT * G::NT_ALL * 256 + 16 * m + 4 * g) = v;  // column 27
         }
       }
     } else {
@@ -568,8 +570,8 @@ __global__ __launch_bounds__(256) void conv_w_reduce_kernel(const float* __restr
   }
   const int r = e & 3, lane = (e >> 2) & 63, tile = e >> 8, j = lane & 15, g = lane >> 4;
   if constexpr (CI == 4) {
-    const int m = tile / 3, t = tile % 3, jj = 16 * t + j, tap = jj / 4, ci = jj % 4;
-    if (jj < 36 && ci < ci_real) dw[((size_t)(16 * m + 4 * g + r) * ci_real + ci) * 9 + tap] = sum;
+    const int m = tile / 2, t = tile % 2, jj = 16 * t + j, tap = jj / 3, ci = jj % 3;
+    if (jj < 27 && ci < ci_real) dw[((size_t)(16 * m + 4 * g + r) * ci_real + ci) * 9 + tap] = sum;
   } else {
     constexpr int NQ = CI / 16, QW = G::QW;
     const int m = tile / (9 * NQ), rest = tile % (9 * NQ), tap = rest / NQ, nq = rest % NQ;

@@ -55,6 +55,7 @@ namespace tc {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 512;  // 8 waves, 2 per SIMD
 constexpr int kChunkBands = 40;  // bands per weight-gradient partial (8 samples of 20 rows)
@@ -76,6 +77,39 @@ __device__ __forceinline__ void lds_dma16(const void* gsrc, uint32_t lds_dst) {
 }
 
 __device__ __forceinline__ void wait_dma() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// vmcnt(0) as the builtin, which the compiler's wait insertion sees (an asm wait it does not):
+// after the prologue's global loads (weights, bias), so that it does not put a vmcnt(0) at
+// their first use INSIDE the unit loop, where it would also wait for the next unit's LDS-DMA
+// (issued just before) every iteration.  Encoding: vmcnt 0, expcnt 7, lgkmcnt 15.
+__device__ __forceinline__ void settle_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+// vmcnt(N): every vector memory op of this wave but the last N issued has completed (they
+// complete in issue order): the unit's DMA, issued before the previous unit's N epilogue
+// stores, has landed without waiting for those stores.
+template <int N>
+__device__ __forceinline__ void wait_vm_keep() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// The work queue's next unit, by one lane: the atomic in asm, so the compiler neither waits for
+// it where it is issued nor knows its result is pending; queue_value() waits (vmcnt(0): by
+// then nothing else is in flight) and hands the value over.
+__device__ __forceinline__ int queue_draw(int* queue) {
+  int v;
+  asm volatile("global_atomic_add %0, %1, %2, off sc0" : "=&v"(v) : "v"(queue), "v"(1) : "memory");
+  return v;
+}
+__device__ __forceinline__ int queue_value(int v) {
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(v)::"memory");
+  return v;
+}
+
+typedef __attribute__((address_space(8))) void* rsrc_t;
+// a raw buffer resource over `bytes` bytes at p (0 bytes: every store through it is dropped,
+// but still issued and counted -- the epilogue's store count is the same in every wave)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_over(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+constexpr int kOOB = 0x7FFFFFF0;  // a buffer offset past any resource: the store is dropped
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)p; }
 
@@ -213,6 +247,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv_a_kernel(ConvAArgs a) {
   }
   f4 bias4 = {0.f, 0.f, 0.f, 0.f};  // this lane's output channels 16 c + 4 g + r
   if constexpr (MODE == 0) bias4 = *reinterpret_cast<const f4*>(a.bias + 16 * c + 4 * g);
+  settle_vm();
 
   zero_range(smem, 2 * G::BUF_F * 4, wid, lane);  // border columns stay zero for the whole kernel
   if (tid == 0) {
@@ -241,12 +276,17 @@ __global__ __launch_bounds__(kThreads, 1) void conv_a_kernel(ConvAArgs a) {
     const int q = 16 * t + j, y = q / C, xx = q % C;
     pbase[t] = (y * RP + xx) * PI + (CI == 4 ? g : 4 * g + 16 * KBW * s);
   }
+  // epilogue stores per wave per unit, the same in every wave (dropped ones included)
+  constexpr int NST = PT * (1 + (MODE == 0 ? 1 : 0) + (MODE == 0 && CI == 4 && HEIST_TC_PADW ? 1 : 0));
   for (int it = 0; cur < nunits; ++it) {
     float* img = buf[it & 1] + bslot * G::BAND_F;
-    wait_dma();
+    // this unit's DMA, not the previous unit's epilogue stores issued after it
+    if (it == 0) wait_dma();
+    else wait_vm_keep<NST>();
     __syncthreads();  // the unit's images are in LDS; everyone is done with the other buffer
+    int drawn = 0;  // the unit after next (tid 0), published after the compute
+    if (tid == 0) drawn = queue_draw(a.queue);
     if (nxt < nunits) issue(nxt, (it + 1) & 1);
-    if (tid == 0) slot[2 + (it & 1)] = atomicAdd(a.queue, 1);
     const int gb = cur * BPU + bslot;
     f4 acc[PT];
 #pragma unroll
@@ -264,10 +304,10 @@ __global__ __launch_bounds__(kThreads, 1) void conv_a_kernel(ConvAArgs a) {
         }
       }
       if constexpr (CI != 4) {
-        // (tap, cb) blocks in order, software-pipelined: block b + 1's activations are read
-        // into the other register set before block b's MFMAs, so no MFMA chain waits on
-        // a whole LDS round trip (the compiler, left alone, read two blocks, ran their 40
-        // MFMAs, then read the next two)
+        // (tap, cb) blocks in order, block b + 1's activations read into the other register
+        // set before block b's MFMAs (the compiler reschedules them: it keeps reads 1-4 MFMAs
+        // ahead; pinning them a whole block ahead with sched_barrier or sched_group_barrier
+        // measured no faster, the SIMD's second wave hides the LDS latency, r06o / r06t)
         constexpr int NBK = 9 * KBW;
         auto boff = [&](int bk) { return ((bk / KBW / 3) * RP + (bk / KBW) % 3) * PI + 16 * (bk % KBW); };
         f4 xv[2][PT];
@@ -284,18 +324,6 @@ __global__ __launch_bounds__(kThreads, 1) void conv_a_kernel(ConvAArgs a) {
 #pragma unroll
             for (int t = 0; t < PT; ++t) acc[t] = mfma(w[bk * 4 + e], xv[bk & 1][t][e], acc[t]);
         }
-#if HEIST_TC_SCHED
-        // the issue order, pinned: block 0's reads, then per block one read of the next block
-        // ahead of every 4 MFMAs (mask 0x100 = LDS read, 0x8 = MFMA)
-        __builtin_amdgcn_sched_group_barrier(0x100, PT, 0);
-#pragma unroll
-        for (int bk = 0; bk < NBK; ++bk)
-#pragma unroll
-          for (int t = 0; t < PT; ++t) {
-            if (bk + 1 < NBK) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
-          }
-#endif
       }
     }
     if constexpr (S == 2) {  // k halves: wave s = 1 hands its partial tiles to wave s = 0 through LDS
@@ -312,16 +340,22 @@ __global__ __launch_bounds__(kThreads, 1) void conv_a_kernel(ConvAArgs a) {
 #pragma unroll
         for (int t = 0; t < PT; ++t) acc[t] += lds_f4(part, t * 256 + lane * 4);
     }
-    if (s == 0 && gb < nbands) {
+    if (tid == 0) slot[2 + (it & 1)] = queue_value(drawn);
+    {
       // D[co][pos]: lane (j, g) holds channels 16 c + 4 g + r of band position 16 t + j; the band's
-      // rows are contiguous, so band position q is image position (smp R + y0) C + q
+      // rows are contiguous, so band position q is image position (smp R + y0) C + q.  Every wave
+      // issues the same NST buffer stores: a wave with no output (s = 1, or no band) stores
+      // through empty resources (dropped), so the next unit's counted wait holds in every wave.
+      const bool out = s == 0 && gb < nbands;
       const int smp = gb / NB, y0 = (gb % NB) * 4;
-      const size_t bandpos = ((size_t)smp * R + y0) * C;
+      const size_t bandpos = out ? ((size_t)smp * R + y0) * C : 0;
+      const auto ry = rsrc_over(a.y + bandpos * PO, out ? 4 * C * PO * 4 : 0);
+      const auto rm = rsrc_over(a.mask_out ? a.mask_out + bandpos * (CO / 4) : nullptr,
+                                out && a.mask_out ? 4 * C * (CO / 4) : 0);
       const lds_u8* mk = reinterpret_cast<const lds_u8*>(as_lds(mbuf)) + ((it & 1) * BPU + bslot) * G::MASK_B;
 #pragma unroll
       for (int t = 0; t < PT; ++t) {
         const int q = 16 * t + j;
-        const size_t pos = bandpos + q;
         f4 v = acc[t];
         if constexpr (MODE == 0) {
           v += bias4;  // conv + b rounded once, then ReLU
@@ -331,18 +365,19 @@ __global__ __launch_bounds__(kThreads, 1) void conv_a_kernel(ConvAArgs a) {
             bits |= (uint32_t)(v[r] > 0.f) << r;
             v[r] = v[r] > 0.f ? v[r] : 0.f;
           }
-          if (a.mask_out) a.mask_out[pos * (CO / 4) + 4 * c + g] = (uint8_t)bits;
+          __builtin_amdgcn_raw_buffer_store_b8((uint8_t)bits, rm, q * (CO / 4) + 4 * c + g, 0, 0);
         } else {
           const uint32_t bits = (uint32_t)mk[q * (CO / 4) + 4 * c + g];
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = (bits >> r) & 1u ? v[r] : 0.f;
         }
-        *reinterpret_cast<f4*>(a.y + pos * PO + 16 * c + 4 * g) = v;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), ry, (q * PO + 16 * c + 4 * g) * 4, 0, 0);
         // conv1's forward (memory-bound) writes the position's 4 pad words as well (zeros, never
         // read): whole 128-B lines, no read-modify-write of a partly written line (0.445 ->
         // 0.346 ms at 16,384 samples); in the MFMA-bound passes the extra store cost 0.3-1.2 %
-        if constexpr (HEIST_TC_PADW && CI == 4)
-          if (c == NCT - 1 && g == 3) *reinterpret_cast<f4*>(a.y + pos * PO + CO) = f4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (MODE == 0 && CI == 4 && HEIST_TC_PADW)
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{0u, 0u, 0u, 0u}, ry,
+                                                 c == NCT - 1 && g == 3 ? (q * PO + CO) * 4 : kOOB, 0, 0);
       }
     }
     __syncthreads();  // slot written; this buffer free for the unit after next
@@ -458,6 +493,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv_w_kernel(ConvWArgs a) {
 #pragma unroll
     for (int t = 0; t < NTW; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
     accb = f4{0.f, 0.f, 0.f, 0.f};
+    int drawn = 0;  // the chunk after next (tid 0), stored to slot[2] once this chunk's k-steps are done
     for (int i = 0; i < kChunkBands; i += BPI, ++it) {
       const float* xi0 = smem + (it & 1) * G::BUF_F;
       const float* di0 = xi0 + BPI * G::XB_F;
@@ -467,8 +503,10 @@ __global__ __launch_bounds__(kThreads, 1) void conv_w_kernel(ConvWArgs a) {
       if (i + BPI < kChunkBands) {
         issue(chunk, i + BPI, (it + 1) & 1);
       } else {
+        // drawn before the DMA goes out (the compiler's wait for the atomic, vmcnt(0), would
+        // otherwise also wait for the DMA), stored after the k-steps
+        if (tid == 0) drawn = atomicAdd(a.queue, 1);
         if (nchunk < nchunks) issue(nchunk, 0, (it + 1) & 1);
-        if (tid == 0) slot[2] = atomicAdd(a.queue, 1);
       }
 #pragma unroll
       for (int bb = 0; bb < BPI; ++bb) {
@@ -501,6 +539,7 @@ __global__ __launch_bounds__(kThreads, 1) void conv_w_kernel(ConvWArgs a) {
         }
       }
     }
+    if (tid == 0) slot[2] = drawn;
     // this chunk's partial: tiles [m][tile][lane][4], then the bias [CO]
     float* p = a.partial + (size_t)chunk * G::WSZ;
     if constexpr (CI == 4) {

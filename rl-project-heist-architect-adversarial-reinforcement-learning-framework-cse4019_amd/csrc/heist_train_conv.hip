@@ -535,6 +535,9 @@ __global__ __launch_bounds__(kThreads, 1) void conv_w_kernel(ConvWArgs a) {
               }
             }
           }
+          // (behind a run-time `if`, so each k-step is its own basic block; compiled once per
+          // wave role instead -- one straight block -- conv2's ran 1 % slower and conv3's spilled,
+          // profiles/r06w_*)
           if (has_bias) accb = mfma(av, 1.0f, accb);
         }
       }

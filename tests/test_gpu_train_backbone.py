@@ -146,14 +146,16 @@ def test_mfma_backbone_matches_float64(gpu_device, n):
     assert max(errs.values()) <= 1e-4, errs
 
 
-@pytest.mark.parametrize("n", [64, 257, 2061])
+@pytest.mark.parametrize("n", [1, 3, 64, 257, 2061])
 def test_mfma_passes_match_torch(gpu_device, n):
     """Each fp32-MFMA pass alone against torch fp32 on the same inputs and masks (so a ReLU
     decision of the forward cannot differ): the three forward layers (bias + ReLU), the data
     gradients of conv3 and conv2 (with the ReLU masks of their inputs), the weight and bias
-    gradients of all three, each within 1e-5 of its max (fp32 summation order only).  n = 64
-    gives every workgroup at most one work unit; 2061 several units per workgroup (the
-    double-buffered pipeline, the k-split hand-off) and several weight-gradient chunks."""
+    gradients of all three, each within 1e-5 of its max (fp32 summation order only).  n = 1 and 3:
+    most workgroups draw no unit at all and the last unit holds one band (the dropped
+    epilogue stores of the counted-wait scheme); n = 64 gives every workgroup at most one work
+    unit; 2061 several units per workgroup (the double-buffered pipeline with its counted DMA
+    waits, the k-split hand-off) and several weight-gradient chunks."""
     from heist_amd import _native as nat
     from heist_amd.networks import _tc_act, _tc_queues
     F = torch.nn.functional

@@ -55,6 +55,10 @@
 
 #pragma clang fp contract(off)
 
+#ifndef HEIST_ARCH_XCD_BARRIER
+#define HEIST_ARCH_XCD_BARRIER 1  // the two-level grid barrier (A/B: -DHEIST_ARCH_XCD_BARRIER=0, the flat one)
+#endif
+
 namespace heist {
 namespace au {
 
@@ -72,7 +76,13 @@ constexpr int MAXNZ = 64;            // nonzeros of the input plane (the Archite
 // workspace layout (floats)
 constexpr int WS_A2 = 0, WS_GP = WS_A2 + C2 * PLANE, WS_DA3 = WS_GP + NWG * HID, WS_DA2 = WS_DA3 + C3 * PLANE,
               WS_DW3 = WS_DA2 + C2 * PLANE, WS_DW2 = WS_DW3 + NWG * DW3R, WS_NP = WS_DW2 + NWG * DW2R,
-              WS_CTR = WS_NP + NWG * REC, WS_FLOATS = WS_CTR + 64;
+              WS_XB = WS_NP + NWG * REC, WS_CTR = WS_XB + 1568, WS_FLOATS = WS_CTR + 64;
+// barrier words (unsigned; zeroed per launch).  ws + WS_CTR, the last 64 words: [0] the flat
+// barrier's counter, [1] the status word (heist.h: byte offset workspace_bytes - 252).  The
+// two-level barrier's words before them, at ws + WS_XB, each on a line of its own (16 XCD
+// slots: XCC_ID is 4 bits): [32 x] XCD x's member count, [512 + 32 x] its arrivals,
+// [1024 + 32 x] its release generation, [1536] the XCD leaders' counter
+constexpr int CW_MEMB = 0, CW_ARR = 512, CW_GEN = 1024, CW_TOP = 1536, CW_WORDS = 1568 + 64;
 
 enum { W1, B1, W2, B2, W3, B3, WF, BF, WV1, BV1, WV2, BV2, NTENS };
 // NP record slots
@@ -114,6 +124,7 @@ struct Lay {
 };
 // scal slots
 enum { S_V = 0, S_DV, S_CLIP, S_NS, S_BC2S, S_NNZ, S_TIMEOUT, S_TG, S_DB3 = 8, S_DB2 = 12, S_NWF = 16, S_NWV1,
+       S_XC = 56, S_XM, S_XN, S_HB,
        S_NBF, S_NBV1, S_NWV2, S_RED8 = 32 };
 
 // ---- memory helpers ---------------------------------------------------------------------
@@ -200,6 +211,52 @@ __device__ __forceinline__ void grid_barrier(unsigned* ctr, unsigned idx, float*
           scal[S_TIMEOUT] = 1.f;
           break;
         }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// The two-level form (MI355X_MICROARCH.md barrier-xcd): a workgroup arrives on its XCD's
+// counter; the XCD's last arriver arrives on the leaders' counter, waits for every XCD's
+// leader and releases its XCD through the XCD's generation word, which only that XCD's
+// workgroups poll (8 pollers per line instead of 64 on one).  Membership (m workgroups on
+// XCD x, nx XCDs with any) is counted once at the start of the launch.  Data hand-offs are
+// unchanged (sc1 stores drained before the arrival, sc1 loads after the release).  Same
+// bounded spin and status bit as grid_barrier.
+// (Its state -- XCD, member count, XCD count, barrier index -- sits in LDS words read by the
+// one polling thread, so it costs the kernel's long-lived registers nothing.)
+__device__ __forceinline__ void xcd_barrier(unsigned* ctr, float* scal, unsigned spin_limit,
+                                            unsigned long long* ready = nullptr) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (ready) *ready = __builtin_amdgcn_s_memrealtime();
+    unsigned* xb = ctr - (WS_CTR - WS_XB);
+    const unsigned xcc = __float_as_uint(scal[S_XC]), m = __float_as_uint(scal[S_XM]), nx = __float_as_uint(scal[S_XN]);
+    const unsigned h = __float_as_uint(scal[S_HB]);
+    scal[S_HB] = __uint_as_float(h + 1u);
+    unsigned* gen = xb + CW_GEN + 32 * xcc;
+    const unsigned old = __hip_atomic_fetch_add(xb + CW_ARR + 32 * xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (scal[S_TIMEOUT] == 0.f) {
+      unsigned spins = 0;
+      bool lost = false;
+      if (old == (h + 1u) * m - 1u) {  // the XCD's last: arrive on the leaders' counter, then release the XCD
+        __hip_atomic_fetch_add(xb + CW_TOP, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (__hip_atomic_load(xb + CW_TOP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (h + 1u) * nx) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > spin_limit) { lost = true; break; }
+        }
+        __hip_atomic_store(gen, h + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < h + 1u) {
+          __builtin_amdgcn_s_sleep(1);
+          if (++spins > spin_limit) { lost = true; break; }
+        }
+      }
+      if (lost) {
+        __hip_atomic_fetch_or(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        scal[S_TIMEOUT] = 1.f;
       }
     }
   }
@@ -623,6 +680,29 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
 
   float a2keep = 0.f;  // a2 at (channel t / NPB, band position t % NPB): P4's relu mask
   unsigned bar = 0;
+#if HEIST_ARCH_XCD_BARRIER
+  unsigned* xb = reinterpret_cast<unsigned*>(a.ws + WS_XB);
+  // the two-level barrier's membership: this workgroup's XCD, its workgroup count, the number of
+  // XCDs holding any (one flat barrier makes the counts final), in LDS for xcd_barrier
+  if (threadIdx.x == 0) {
+    const unsigned xcc = __builtin_amdgcn_s_getreg(0x1814) & 15u;  // hwreg(HW_REG_XCC_ID, 0, 4)
+    scal[S_XC] = __uint_as_float(xcc);
+    scal[S_HB] = __uint_as_float(0u);
+    __hip_atomic_fetch_add(xb + CW_MEMB + 32 * xcc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  grid_barrier(ctr, bar++, scal, a.spin_limit);
+  if (threadIdx.x == 0) {
+    unsigned nx = 0;
+    for (int x = 0; x < 16; ++x)
+      nx += __hip_atomic_load(xb + CW_MEMB + 32 * x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+    const unsigned xcc = __float_as_uint(scal[S_XC]);
+    scal[S_XM] = __uint_as_float(__hip_atomic_load(xb + CW_MEMB + 32 * xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    scal[S_XN] = __uint_as_float(nx);
+  }
+#define BARRIER(i) xcd_barrier(ctr, scal, a.spin_limit, READY(i));
+#else
+#define BARRIER(i) grid_barrier(ctr, bar++, scal, a.spin_limit, READY(i));
+#endif
   for (int s = 0; s < a.k; ++s) {
     const int t = tid_o(), wv = t >> 6, lane = t & 63, w = wg_o();
     const int cg = wg_cg(w), band = wg_band(w), y0 = band * BH;
@@ -647,7 +727,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       store_band<R, C>(a.ws + WS_A2, sm + L::own, cg, band);
     }
     STAMP(1)
-    grid_barrier(ctr, bar++, scal, a.spin_limit, READY(0));
+    BARRIER(0)
     STAMP(2)
 
     // ======== P2: conv3 own channels, pool, fc_global partial ========
@@ -718,7 +798,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       if (fhf == 0) st_sc1(a.ws + WS_GP + w * HID + fi, gp);
     }
     STAMP(3)
-    grid_barrier(ctr, bar++, scal, a.spin_limit, READY(1));
+    BARRIER(1)
     STAMP(4)
 
     // ======== P3: value head (redundant), dp / da3 / dW3 / dWf / dWv1 (owned) ========
@@ -888,7 +968,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       }
     }
     STAMP(5)
-    grid_barrier(ctr, bar++, scal, a.spin_limit, READY(2));
+    BARRIER(2)
     STAMP(6)
 
     // ======== P4: da2 own channels (conv3^T), dW2 / db2 partials ========
@@ -986,7 +1066,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       if (t < 32) st_sc1(a.ws + WS_DW2 + w * DW2R + DW2N + t, t < CPG ? x[t] : 0.f);
     }
     STAMP(7)
-    grid_barrier(ctr, bar++, scal, a.spin_limit, READY(3));
+    BARRIER(3)
     STAMP(8)
 
     // ======== P5: da1 (2 channels on the band), partial dW1 / db1, the group's weight
@@ -1098,7 +1178,7 @@ __global__ void __launch_bounds__(NT, 1) arch_update_kernel(Args a) {
       }
     }
     STAMP(9)
-    grid_barrier(ctr, bar++, scal, a.spin_limit, READY(4));
+    BARRIER(4)
     STAMP(10)
 
     // ======== P6: clip coefficient, Adam, publish ========
@@ -1318,7 +1398,7 @@ hipError_t launch_arch_update(float* const* p, float* const* m, float* const* v,
   a.eps = (float)eps;
   a.max_norm = (float)max_norm;
   a.grad_out = (float)value_coeff;
-  hipError_t e = hipMemsetAsync(a.ws + au::WS_CTR, 0, 64 * sizeof(float), st);
+  hipError_t e = hipMemsetAsync(a.ws + au::WS_XB, 0, au::CW_WORDS * sizeof(float), st);  // through the end
   if (e != hipSuccess) return e;
   switch (R) {
     case 20: return launch_sized<20>(a, st);

@@ -891,7 +891,12 @@ hipError_t launch_train_pool(const float* a3, int n, int R, int C, float* feat, 
 
 hipError_t launch_train_pool_bwd(const float* dfeat, const uint8_t* m3, int n, int R, int C, float* d3, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  if (R * C * 16 > 48 * 1024 || (reinterpret_cast<uintptr_t>(m3) & 15)) return hipErrorInvalidValue;
+  // the sample's mask rows in LDS: R * C * 16 bytes (64 x 64 at most)
+  if (R * C * 16 > 64 * 1024 || (reinterpret_cast<uintptr_t>(m3) & 15)) return hipErrorInvalidValue;
+  if (R * C * 16 > 48 * 1024) {
+    const hipError_t e = set_lds(&tc::pool_bwd_mask_kernel, R * C * 16);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(tc::pool_bwd_mask_kernel, dim3((unsigned)n), dim3(256), (size_t)R * C * 16, st, dfeat, m3, n, R, C,
                      d3);
   return hipGetLastError();

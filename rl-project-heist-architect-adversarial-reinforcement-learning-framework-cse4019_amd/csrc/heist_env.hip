@@ -21,6 +21,10 @@
 
 #pragma clang fp contract(off)
 
+#ifndef HEIST_LEAN_OCC
+#define HEIST_LEAN_OCC 4  // step_lean_kernel's waves per SIMD the compiler budgets registers for (A/B)
+#endif
+
 namespace heist {
 
 __constant__ double kSinCosTab[4 * HEIST_SINCOS_TAB_ROWS] = HEIST_SINCOS_TAB_INIT;
@@ -2357,7 +2361,7 @@ __device__ __attribute__((noinline)) void lean_generic_body(EnvParams p, int K, 
 // their visibility stores / stop-byte loads, 26 the observation stores without their LDS reads,
 // 27 the stores alone (no move, cast, detection), 28 move + patrol + stores.
 template <int R_, int C_, bool STAMP = false, int PROBE = 0>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void step_lean_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_OCC))) void step_lean_kernel(
     EnvParams p, int K, const int64_t* __restrict__ actions, float* __restrict__ obs, float* __restrict__ rew,
     double* __restrict__ rew64, uint8_t* __restrict__ done_out, int8_t* __restrict__ status_out, int auto_reset) {
   constexpr int D = lean_gap(R_, C_);

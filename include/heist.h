@@ -26,7 +26,8 @@ extern "C" {
 
 /* 2: heist_step_stamps takes the buffer size; heist_stamp_words; 3: heist_arch_update_*;
  * 4: heist_arch_update_status, the heist_*_nhwc training passes, heist_get_config's 15th word
- *    (heist_step on the lean kernel), the heist_train_* fp32-MFMA training convolutions */
+ *    (heist_step on the lean kernel), the heist_train_* fp32-MFMA training convolutions,
+ *    heist_rollout_tally */
 #define HEIST_ABI_VERSION 4
 #define HEIST_EINVAL 100000
 
@@ -260,6 +261,18 @@ int heist_arch_update_timed_out(const void* workspace, int* timed_out, heist_str
  * phase points of steps 0..15 in workgroups 0 and 63, then every workgroup's arrival (stores
  * drained) at each of the 5 grid barriers of steps 0..15 (tools/probe_arch_update.py); NULL: off. */
 int heist_arch_update_stamps(uint64_t* buf);
+
+/* The batched trainer's per-tick attempt bookkeeping over n envs (the per-episode counters of
+ * training.py:515-544 -- steps, reward, outcome per attempt -- and solver.reset() per attempt,
+ * :517), replacing ~20 tensor ops per tick: counting = valid[e] && attempts[e] <
+ * attempts_per_layout; steps += counting; reward_sum += counting ? reward64 : 0.0 (float64);
+ * an attempt that ends (counting && done) adds 1 to solve (status 2 = vault_reached), detect
+ * (status 1) or timeout (any other status) and to attempts; h, c [n][hidden] float32 (the
+ * LSTM state, layer dimension 1) are multiplied by (done ? 0 : 1).  valid, done uint8 (bool),
+ * status int8, the counters int32. */
+int heist_rollout_tally(const uint8_t* valid, int32_t* attempts, int attempts_per_layout, const uint8_t* done,
+                        const int8_t* status, const double* reward64, int32_t* steps, double* reward_sum, int32_t* solve,
+                        int32_t* detect, int32_t* timeout, float* h, float* c, int hidden, int n, heist_stream_t stream);
 
 /* Replaces SolverAgent._compute_gae + returns (agents/solver.py:142-143, :228-244) on a
  * [T][N] rollout (column e = env e's concatenated episodes).  dones [T][N] uint8.

@@ -80,6 +80,10 @@ hipError_t launch_train_pool(const float* a3, int n, int R, int C, float* feat, 
 hipError_t launch_train_pool_bwd(const float* dfeat, const uint8_t* m3, int n, int R, int C, float* d3, hipStream_t st);
 hipError_t launch_gae(const float* r, const float* v, const uint8_t* d, const float* last_value, int T, int N,
                       double gamma, double lam, float* adv, float* ret, hipStream_t st);
+hipError_t launch_rollout_tally(const uint8_t* valid, int32_t* attempts, int A, const uint8_t* done, const int8_t* status,
+                                const double* reward64, int32_t* steps, double* reward_sum, int32_t* solve,
+                                int32_t* detect, int32_t* timeout, float* h, float* c, int hidden, int n, int vault,
+                                int det, hipStream_t st);
 hipError_t launch_adv_moments(const float* x, int64_t n, int phase, double* acc, hipStream_t st);
 hipError_t launch_adv_apply(float* x, int64_t n, const double* acc, float eps, hipStream_t st);
 hipError_t launch_ppo_loss(const float* logits, const float* values, const int64_t* actions, const float* old_logp,
@@ -668,6 +672,20 @@ int heist_arch_update_timed_out(const void* workspace, int* timed_out, heist_str
   if (int rc = heist_arch_update_status(workspace, &status, stream)) return rc;
   *timed_out = status & 1;
   return 0;
+}
+
+int heist_rollout_tally(const uint8_t* valid, int32_t* attempts, int attempts_per_layout, const uint8_t* done,
+                        const int8_t* status, const double* reward64, int32_t* steps, double* reward_sum, int32_t* solve,
+                        int32_t* detect, int32_t* timeout, float* h, float* c, int hidden, int n, heist_stream_t stream) {
+  HEIST_REQUIRE(valid && attempts && done && status && reward64 && steps && reward_sum && solve && detect && timeout,
+                "heist_rollout_tally: null pointer");
+  HEIST_REQUIRE(n >= 0 && hidden >= 1 && (n == 0 || (h && c)), "heist_rollout_tally: bad sizes");
+  if (n == 0) return 0;
+  return check_hip(heist::launch_rollout_tally(valid, attempts, attempts_per_layout, done, status, reward64, steps,
+                                               reward_sum, solve, detect, timeout, h, c, hidden, n, HEIST_VAULT_REACHED,
+                                               HEIST_DETECTED,
+                                               (hipStream_t)stream),
+                   "heist_rollout_tally");
 }
 
 int heist_gae(const float* rewards, const float* values, const uint8_t* dones, const float* last_value, int T, int n,

@@ -206,6 +206,50 @@ __global__ void ppo_finalize_kernel(const double* __restrict__ partials, int nbl
 
 // ---------------------------------------------------------------------------
 
+// The rollout's per-tick attempt bookkeeping (training.py:515-544: steps and reward of the
+// running attempt, its outcome when it ends, the fresh LSTM state of the next one), one thread
+// per (env, hidden slot): slot 0 also does the env's counters.  The same arithmetic as the
+// torch expressions it replaces (heist_amd/training.py _rollout): counting = valid and
+// attempts < A; reward += (counting ? r : 0.0) in float64; an ended attempt counts by status;
+// h, c *= (done ? 0 : 1) as float multiplies (negative values become -0.0, as torch's do).
+__global__ __launch_bounds__(256) void rollout_tally_kernel(const uint8_t* __restrict__ valid, int32_t* __restrict__ attempts,
+                                                            int A, const uint8_t* __restrict__ done,
+                                                            const int8_t* __restrict__ status,
+                                                            const double* __restrict__ reward64, int32_t* __restrict__ steps,
+                                                            double* __restrict__ reward_sum, int32_t* __restrict__ solve,
+                                                            int32_t* __restrict__ detect, int32_t* __restrict__ timeout,
+                                                            float* __restrict__ h, float* __restrict__ c, int hidden, int n,
+                                                            int vault, int det) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)n * hidden) return;
+  const int e = (int)(i / hidden), k = (int)(i - (int64_t)e * hidden);
+  const bool d = done[e] != 0;
+  const float keep = d ? 0.f : 1.f;
+  h[(int64_t)e * hidden + k] = h[(int64_t)e * hidden + k] * keep;
+  c[(int64_t)e * hidden + k] = c[(int64_t)e * hidden + k] * keep;
+  if (k != 0) return;
+  const bool counting = valid[e] != 0 && attempts[e] < A;
+  steps[e] += counting ? 1 : 0;
+  reward_sum[e] = reward_sum[e] + (counting ? reward64[e] : 0.0);
+  const bool fin = counting && d;
+  const int st = (int)status[e];
+  solve[e] += (fin && st == vault) ? 1 : 0;
+  detect[e] += (fin && st == det) ? 1 : 0;
+  timeout[e] += (fin && st != vault && st != det) ? 1 : 0;
+  attempts[e] += fin ? 1 : 0;
+}
+
+hipError_t launch_rollout_tally(const uint8_t* valid, int32_t* attempts, int A, const uint8_t* done, const int8_t* status,
+                                const double* reward64, int32_t* steps, double* reward_sum, int32_t* solve,
+                                int32_t* detect, int32_t* timeout, float* h, float* c, int hidden, int n, int vault,
+                                int det, hipStream_t st) {
+  const int64_t total = (int64_t)n * hidden;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(rollout_tally_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, valid, attempts, A,
+                     done, status, reward64, steps, reward_sum, solve, detect, timeout, h, c, hidden, n, vault, det);
+  return hipGetLastError();
+}
+
 hipError_t launch_gae(const float* r, const float* v, const uint8_t* d, const float* last_value, int T, int N,
                       double gamma, double lam, float* adv, float* ret, hipStream_t st) {
   const float g = (float)gamma, gl = (float)(gamma * lam);

@@ -180,7 +180,9 @@ class SolverAgent:  # agents/solver.py:18-259
                     b = idx[start:start + bs]
                     w = int(b.numel())
                     x = states[b]
-                    if x.is_cuda:
+                    # MIOpen's convolutions want channels-last; the fp32-MFMA backbone reads the
+                    # gathered rows with their own strides (one pass to NHWC4 either way)
+                    if x.is_cuda and not (self.update_precision == "fp32" and self.network._train_conv_ok(x)):
                         x = x.contiguous(memory_format=torch.channels_last)
                     with torch.autocast("cuda", dtype=torch.bfloat16,
                                         enabled=self.update_precision == "bf16" and x.is_cuda):

@@ -320,6 +320,33 @@ class AdversarialTrainer:  # training.py:115-790
 
     # -- rollout / scoring ------------------------------------------------------------------
     @torch.no_grad()
+    def _tally(self, done, status, A, vault, det):
+        """One tick's attempt bookkeeping (training.py:515-544 per env: steps and reward of the
+        running attempt, its outcome when it ends) and the fresh LSTM state of the next attempt
+        (solver.reset(), :517): one heist_rollout_tally launch on a HIP device (the torch
+        expressions below, bit for bit, elsewhere)."""
+        n = self.n_envs
+        if self.device.type == "cuda" and self.h.is_contiguous() and self.c.is_contiguous():
+            from . import _native as nat
+            P = nat.ptr
+            nat.check(nat.lib().heist_rollout_tally(
+                P(self.b_valid), P(self.b_attempts), A, P(done), P(status), P(self.env.reward64), P(self.b_steps),
+                P(self.b_reward), P(self.b_solve), P(self.b_detect), P(self.b_timeout), P(self.h), P(self.c),
+                int(self.h.shape[-1]), n, nat.stream(self.device)), "heist_rollout_tally")
+            return
+        counting = self.b_valid & (self.b_attempts < A)
+        self.b_steps += counting.int()
+        self.b_reward += torch.where(counting, self.env.reward64, torch.zeros_like(self.b_reward))
+        fin = counting & done
+        st = status.to(torch.int32)
+        self.b_solve += (fin & (st == vault)).int()
+        self.b_detect += (fin & (st == det)).int()
+        self.b_timeout += (fin & (st != vault) & (st != det)).int()
+        self.b_attempts += fin.int()
+        keep = (~done).to(self.h.dtype).reshape(1, n, 1)  # a new attempt starts with a fresh LSTM state
+        self.h = self.h * keep
+        self.c = self.c * keep
+
     def _rollout(self, T: int) -> Rollout:
         """T ticks of all envs.  The observation each tick's action is chosen from is
         obs[t]; heist_step writes the next one straight into obs[t + 1] (the last into
@@ -343,18 +370,7 @@ class AdversarialTrainer:  # training.py:115-790
             d_buf[t] = done.to(torch.uint8)
             if self._trace is not None:
                 self._trace.append((a.clone(), env.reward64.clone(), done.clone(), status.clone()))
-            counting = self.b_valid & (self.b_attempts < A)
-            self.b_steps += counting.int()
-            self.b_reward += torch.where(counting, env.reward64, torch.zeros_like(self.b_reward))
-            fin = counting & done
-            st = status.to(torch.int32)
-            self.b_solve += (fin & (st == vault)).int()
-            self.b_detect += (fin & (st == det)).int()
-            self.b_timeout += (fin & (st != vault) & (st != det)).int()
-            self.b_attempts += fin.int()
-            keep = (~done).to(self.h.dtype).reshape(1, n, 1)  # a new attempt starts with a fresh LSTM state
-            self.h = self.h * keep
-            self.c = self.c * keep
+            self._tally(done, status, A, vault, det)
         last_value = self.solver.value(env.obs, (self.h, self.c))
         return Rollout(obs_buf, act_buf, lp_buf, v_buf, r_buf, d_buf, mask=self.b_valid.clone(),
                        last_value=last_value)
@@ -384,17 +400,7 @@ class AdversarialTrainer:  # training.py:115-790
                 bufs[k].append(x)
             if self._trace is not None:
                 self._trace.append((a.clone(), env.reward64.clone(), done.clone(), status.clone()))
-            self.b_steps += counting.int()
-            self.b_reward += torch.where(counting, env.reward64, torch.zeros_like(self.b_reward))
-            fin = counting & done
-            st = status.to(torch.int32)
-            self.b_solve += (fin & (st == vault)).int()
-            self.b_detect += (fin & (st == det)).int()
-            self.b_timeout += (fin & (st != vault) & (st != det)).int()
-            self.b_attempts += fin.int()
-            keep = (~done).to(self.h.dtype).reshape(1, n, 1)  # solver.reset() per attempt (training.py:517)
-            self.h = self.h * keep
-            self.c = self.c * keep
+            self._tally(done, status, A, vault, det)  # (counting as above; solver.reset() per attempt)
             obs = nxt.clone()
             t += 1
         st = {k: torch.stack(v) for k, v in bufs.items()}

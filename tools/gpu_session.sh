@@ -13,6 +13,7 @@
 #   bench_env         the headline only: bench.py --no-secondary --no-cpu-baseline
 #   prof              rocprofv3 kernel trace + stats of the headline (bench.py --no-secondary)
 #   pmc               PMC passes on the headline: FETCH_SIZE, WRITE_SIZE, SQ mix (+ summaries)
+#   pmc_c4            the same on BASELINE C4's env-only command (tools/probe_env_configs.py, c4)
 #   train             tools/probe_train.py (the fp32 training iteration's parts)
 #   prof_train        rocprofv3 kernel stats of tools/probe_train.py
 #   arch              tools/probe_arch_update.py (Architect update kernel, per-update time)
@@ -50,6 +51,15 @@ for step in "$@"; do
       run pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS -d "$OUT/pmc_sq" -o heist --output-format csv -- python3 $B --steps 100 --warmup 10
       python tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" --ticks 20 --profile "$TAG" --out "$OUT/traffic.json" > /dev/null
       python tools/pmc_sq.py "$OUT/pmc_sq" --ticks 20 --out "$OUT/pmc_sq.json" > /dev/null ;;
+    pmc_c4)  # the same three passes on BASELINE C4's env-only command (8192 envs, budget 40)
+      export PROBE_CONFIGS=c4
+      C4="python3 tools/probe_env_configs.py"
+      run pmc_c4_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_c4_fetch" -o heist --output-format csv -- $C4
+      run pmc_c4_write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_c4_write" -o heist --output-format csv -- $C4
+      run pmc_c4_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS -d "$OUT/pmc_c4_sq" -o heist --output-format csv -- $C4
+      unset PROBE_CONFIGS
+      python tools/pmc_traffic.py "$OUT/pmc_c4_fetch" "$OUT/pmc_c4_write" --ticks 20 --envs 8192 --workload c4 --profile "$TAG" --out "$OUT/c4_traffic.json" > /dev/null
+      python tools/pmc_sq.py "$OUT/pmc_c4_sq" --ticks 20 --out "$OUT/c4_pmc_sq.json" > /dev/null ;;
     train) run train 600 python3 tools/probe_train.py ;;
     prof_train) run prof_train 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_train" -o train --output-format csv -- python3 tools/probe_train.py ;;
     arch) run arch 300 python3 tools/probe_arch_update.py ;;

@@ -27,8 +27,8 @@ extern "C" {
 /* 2: heist_step_stamps takes the buffer size; heist_stamp_words; 3: heist_arch_update_*;
  * 4: heist_arch_update_status, the heist_*_nhwc training passes, heist_get_config's 15th word
  *    (heist_step on the lean kernel), the heist_train_* fp32-MFMA training convolutions,
- *    heist_rollout_tally */
-#define HEIST_ABI_VERSION 4
+ *    heist_rollout_tally; 5: heist_get_config's 16th word (lean_waves) */
+#define HEIST_ABI_VERSION 5
 #define HEIST_EINVAL 100000
 
 /* status_out codes of heist_step (environment.py:236-297 info["status"]). */
@@ -144,11 +144,13 @@ int64_t heist_stamp_words(heist_t h, int which);
 int heist_step_waves(heist_t h);
 
 /* The handle's effective kernel configuration, no reference counterpart (what a benchmark
- * records next to its numbers): out[0..n) with n <= 15 receives step_waves, ray_chunk,
+ * records next to its numbers): out[0..n) with n <= 16 receives step_waves, ray_chunk,
  * step_occ, vis_gap, obs_store, ray_mode, probe_mode, dispatch_order, split_obs,
  * guard_cones, multi_waves, fan_on, lean, interval_fans (the HEIST_* environment knobs as heist_create resolved them,
  * then any heist_set_* calls), step_lean (1: heist_step currently runs as a one-tick
- * heist_step_multi launch on the lean kernel; HEIST_STEP_LEAN=1 at heist_create turns it on).  probe_mode != 0 selects the profiling step kernel, whose results are
+ * heist_step_multi launch on the lean kernel; HEIST_STEP_LEAN=1 at heist_create turns it on),
+ * lean_waves (waves per env of the 32 x 32 lean kernel: 2 when the batch's doubled waves fit
+ * the chip, HEIST_LEAN_WAVES=1/2 forces).  probe_mode != 0 selects the profiling step kernel, whose results are
  * wrong by design (phases skipped). */
 int heist_get_config(heist_t h, int32_t* out, int n);
 

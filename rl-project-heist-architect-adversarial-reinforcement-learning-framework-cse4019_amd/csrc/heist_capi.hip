@@ -34,6 +34,7 @@ int vis_gap_for(int R, int C);
 int stop_map_bytes(int R, int C);
 bool env_variant_exists(int W, int U, int O, int D);
 bool multi_variant_exists(int W, int U, int O, int D);
+bool lean_two_waves(const EnvParams& p);
 hipError_t launch_cone_order(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
                              uint32_t* keys_out, hipStream_t st);
 hipError_t launch_cones(int n, int R, int C, const uint8_t* walls, const int32_t* meta, const double* params,
@@ -287,6 +288,8 @@ int heist_create(int R, int C, int max_steps, int sr, int sc, int vr, int vc, co
   p.n_cu = n_cu;
   p.prio_mode = 0;
   if (const char* m = getenv("HEIST_PRIO_MODE")) p.prio_mode = atoi(m) < 0 ? 0 : (atoi(m) > 3 ? 3 : atoi(m));
+  p.lean_waves = 0;
+  if (const char* m = getenv("HEIST_LEAN_WAVES")) p.lean_waves = atoi(m) == 1 ? 1 : (atoi(m) == 2 ? 2 : 0);
   p.split_obs = 1;
   if (const char* m = getenv("HEIST_SPLIT_OBS")) p.split_obs = atoi(m) ? 1 : 0;
   for (int k = 0; k < 8; ++k) p.tile_lut[k] = k <= 5 ? (float)k / 5.0f : 0.0f;  // environment.py:319
@@ -520,11 +523,12 @@ int heist_step_waves(heist_t h) {
 
 int heist_get_config(heist_t h, int32_t* out, int n) {
   if (int rc = check_handle(h)) return rc;
-  HEIST_REQUIRE(out != nullptr && n >= 0 && n <= 15, "heist_get_config: need out != NULL and 0 <= n <= 15");
+  HEIST_REQUIRE(out != nullptr && n >= 0 && n <= 16, "heist_get_config: need out != NULL and 0 <= n <= 16");
   const EnvParams& p = h->p;
-  const int32_t v[15] = {p.step_waves, p.ray_chunk,  p.step_occ,       p.vis_gap,   p.obs_store,  p.ray_mode,
+  const int32_t v[16] = {p.step_waves, p.ray_chunk,  p.step_occ,       p.vis_gap,   p.obs_store,  p.ray_mode,
                          p.probe_mode, p.dispatch_order, p.split_obs, p.guard_cones, p.multi_waves, p.fan_on,
-                         p.lean,       p.interval_fans,  lean_serves(h) ? 1 : 0};
+                         p.lean,       p.interval_fans,  lean_serves(h) ? 1 : 0,
+                         p.R == 32 && p.C == 32 && heist::lean_two_waves(p) ? 2 : 1};
   for (int k = 0; k < n; ++k) out[k] = v[k];
   return 0;
 }

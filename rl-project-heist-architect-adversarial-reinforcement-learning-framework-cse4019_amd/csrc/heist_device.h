@@ -149,6 +149,8 @@ struct EnvParams {
                                // the SIMDs (order_kernel); 0: env b
   int n_cu;                    // compute units of the device (the snake draft's SIMD count / 4)
   int prio_mode;               // K-tick lean kernel wave priority by cost rank (order_kernel; HEIST_PRIO_MODE)
+  int lean_waves;              // 32 x 32 lean kernel waves per env: 0 auto (2 when they fit the chip), 1, 2
+                               // (HEIST_LEAN_WAVES)
   unsigned long long* stamps;          // optional [n_envs][waves][8]: step-kernel phase stamps (s_memtime), else null
   int obs_store;              // observation stores: 0 plain, 1 write-through (sc1), 2 nt, 3 sc1 nt (HEIST_OBS_STORE)
   int ray_mode;               // 0: fp32 fast path with exact fp64 re-cast of near-tie rays; 1: exact fp64 only

@@ -2360,8 +2360,8 @@ __device__ __attribute__((noinline)) void lean_generic_body(EnvParams p, int K, 
 // DMA, 22 no visibility cast, 23 no observation stores, 24 / 25 shared-fan marches without
 // their visibility stores / stop-byte loads, 26 the observation stores without their LDS reads,
 // 27 the stores alone (no move, cast, detection), 28 move + patrol + stores.
-template <int R_, int C_, bool STAMP = false, int PROBE = 0>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_OCC))) void step_lean_kernel(
+template <int R_, int C_, bool STAMP = false, int PROBE = 0, int NW = 1>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_OCC))) void step_lean_kernel(
     EnvParams p, int K, const int64_t* __restrict__ actions, float* __restrict__ obs, float* __restrict__ rew,
     double* __restrict__ rew64, uint8_t* __restrict__ done_out, int8_t* __restrict__ status_out, int auto_reset) {
   constexpr int D = lean_gap(R_, C_);
@@ -2370,10 +2370,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_O
   constexpr int N4 = RC / 4;
   constexpr int C4 = C_ / 4;
   constexpr int Q = (N4 + 63) / 64;  // observation quads per lane (20 x 20: 2, 32 x 32: 4)
-  constexpr int kStores = 3 * Q + 4;  // a tick's stores (see 6. below)
   constexpr int OFF0 = kRing * PC + kRing;  // padded index of tile (0, 0); also a sample's offset on its own tile
   static_assert((R_ + 2 * kRing) * PC <= D, "the padded planes fit the 1024-byte gap");
   static_assert(C_ % 4 == 0 && R_ <= 64 && C_ <= 32 && (R_ + 2 * kRing) * PC <= 2048, "lean kernel geometry");
+  static_assert(NW == 1 || (NW == 2 && !STAMP && PROBE == 0 && Q % 2 == 0), "two waves: the plain form, even Q");
+  constexpr int QW = Q / NW;          // observation quads per lane this wave stores
+  constexpr int kStores = 3 * QW + 4;  // a wave's stores per tick (see 6. below)
   extern __shared__ __align__(16) unsigned char smem[];
   const int e = block_env(p);
   if (p.prio_mode && p.dispatch_order) {
@@ -2382,7 +2384,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_O
     else if (pr == 2) __builtin_amdgcn_s_setprio(2);
     else if (pr == 1) __builtin_amdgcn_s_setprio(1);
   }
-  const int lane = threadIdx.x;
+  // NW = 2 (an interval-fan env of a batch small enough that two waves per env still fit
+  // the chip): both waves keep the env's whole state (the same inputs, the same arithmetic),
+  // split the cast's pair chunks and the observation quads, and meet at LDS barriers; wave 0
+  // alone owns the cached guard cones (their LDS-DMA, staging and stamps) and the write-back
+  const int lane = NW == 1 ? (int)threadIdx.x : (int)(threadIdx.x & 63u);
+  const int wid = NW == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int tid = threadIdx.x;
   const int N = p.n_envs;
   const int mc = p.max_cams, mg = p.max_guards, n_slot = mc + mg, mp = p.max_path;
   const EnvBase eb = env_base(p, e);
@@ -2445,6 +2453,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_O
                                        su_ >= 2097153.0);
     ivl = base_ok && !fan_ok && p.interval_fans && __ballot(!ivl_cam) == 0ull;
     if (!base_ok || (!fan_ok && !ivl)) {
+      if (NW == 2 && wid != 0) return;  // the generic body is one wave's (an ended wave leaves the barriers)
       lean_generic_body<D>(p, K, actions, obs, rew, rew64, done_out, status_out, auto_reset, smem, e);
       return;
     }
@@ -2481,18 +2490,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_O
   {
     // grid (static observation channel 0) and the padded stop map, as prefetch does
     const uint32_t* g4 = reinterpret_cast<const uint32_t*>(p.grid + (size_t)e * RC);
-    for (int i = lane; i < N4; i += 64) reinterpret_cast<uint32_t*>(L.grid)[i] = g4[i];
+    for (int i = tid; i < N4; i += 64 * NW) reinterpret_cast<uint32_t*>(L.grid)[i] = g4[i];
     const uint8_t* ss = p.stop + (size_t)e * p.stop_bytes;
-    for (int i = lane; i < p.stop_bytes; i += 64) expand_stop(wall, i, ss[i]);
+    for (int i = tid; i < p.stop_bytes; i += 64 * NW) expand_stop(wall, i, ss[i]);
     const int vault = p.vr * C_ + p.vc, qv = vault >> 2;
-    for (int q = lane; q < N4; q += 64) {  // channel 2's static plane with the vault patched
+    for (int q = tid; q < N4; q += 64 * NW) {  // channel 2's static plane with the vault patched
       float4 v = reinterpret_cast<const float4*>(p.plane0)[q];
       if (q == qv) patch4(v, vault & 3, p.vault_val);
       L.plane2[q] = v;
     }
   }
-  for (int i = lane; i < mg * mp; i += 64) L.path[i] = eb.paths[i];
-  for (int k = lane; k < K; k += 64) {
+  for (int i = tid; i < mg * mp; i += 64 * NW) L.path[i] = eb.paths[i];
+  for (int k = tid; k < K; k += 64 * NW) {
     const int64_t a = actions[(size_t)k * N + e];
     L.act[k] = (uint8_t)((a < 0 || a > 4) ? 0 : a);  // unknown actions do not move (environment.py:239)
   }
@@ -2535,15 +2544,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_O
     }
     dma_cone(idx, slot, par);
   };
-  dma_next_cone(0);
+  if (wid == 0) dma_next_cone(0);
   if (ivl) {  // the interval table into the staging space (LDS-DMA, 16 B per lane per pass)
-    for (uint32_t o = 0; o < (uint32_t)sizeof(IvlTable); o += 1024u)
+    for (uint32_t o = 1024u * (uint32_t)wid; o < (uint32_t)sizeof(IvlTable); o += 1024u * NW)
       if (o + 16u * (uint32_t)lane < (uint32_t)sizeof(IvlTable))
         lds_dma16(reinterpret_cast<const unsigned char*>(&kIvlTable) + o + 16u * (uint32_t)lane, stg_a + o);
-  } else {
+  } else if (wid == 0) {
     dma_fan(0, true);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (NW == 2) __syncthreads();  // both waves' parts of the table in place
 
   // the cached guards' cone rows (staging parity par) ORed into the plane: lane 15 i + j
   // takes row j of guard slot 4 pass + i; bit dc + 7 of row dr + 7 is tile (gr + dr, gc + dc);
@@ -2665,9 +2675,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_O
   // fan widths, and an env's chain of chunks is as short as its cameras' total cut count
   // allows (about 92 % of the pairs of the synthetic mix hold a ray; packing the marches
   // through an LDS queue, 64 per march, was slower: one more LDS round trip per march).
+  // NW = 2: the waves meet with their LDS operations retired (no vector-memory wait: the
+  // previous ticks' stores stay in flight)
+  auto wave_join = [&]() {
+    if constexpr (NW == 2) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  };
   auto cast_ivl = [&](int par) {
+    wave_join();  // both waves' reads of the previous plane are done
 #pragma unroll
-    for (int z = 0; z < D / 1024; ++z)  // 64 x 16 B per pass: the plane
+    for (int z = wid; z < D / 1024; z += NW)  // 64 x 16 B per pass: the plane
       reinterpret_cast<uint4*>(vis)[lane + 64 * z] = make_uint4(0u, 0u, 0u, 0u);
     // camera lanes: the start angle, the cut range, the pair count
     const double hmh = heading - fovd / 2.0;  // security.py:64, :70
@@ -2700,7 +2716,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_O
       march_fast<D, 2 * kTieMaxRange, false, false, true>(PC, own, d.x, d.y, mx, my, 2 * kTieMaxRange);
     };
     int mb = 0;  // the first camera whose pairs reach this chunk
-    for (int q0 = 0; q0 < total; q0 += 64) {
+    wave_join();  // the plane is clear
+    for (int q0 = 64 * wid; q0 < total; q0 += 64 * NW) {
       const int q = q0 + lane;
       while (__builtin_amdgcn_readlane(end_l, mb) <= q0) ++mb;
       // the camera of pair q (those before it end at or below q) and its cut
@@ -2742,13 +2759,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_O
       if (safe) march_at(cu.z >> 16, dj);
     }
     LEAN_STAMP(2);
-    stamp_cones(par);
+    if (wid == 0) stamp_cones(par);
+    wave_join();  // the plane is complete
   };
   auto cast = [&](int k, int n_uniq, int n_tie, int par, bool staged, bool staged_wide) {
-    if (ivl)
+    if (ivl) {
       cast_ivl(par);
-    else
-      cast_fan(k, n_uniq, n_tie, par, staged, staged_wide);
+    } else {  // the shared fan: wave 0's (its staging and DMA are wave 0's)
+      wave_join();
+      if (wid == 0) cast_fan(k, n_uniq, n_tie, par, staged, staged_wide);
+      wave_join();
+    }
   };
 
   constexpr uint32_t kOOB = 0x40000000u;  // a store offset past every buffer descriptor below
@@ -2761,7 +2782,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_O
     if (PROBE == 21) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(kStores) : "memory");
     int n_uniq = 0, n_tie = 0;
-    if (!ivl) {  // one LDS read for both header words
+    if (!ivl && wid == 0) {  // one LDS read for both header words
       const int2 h = *reinterpret_cast<const int2*>(&L.stg->hdr[2]);
       n_uniq = __builtin_amdgcn_readfirstlane(h.x);
       n_tie = __builtin_amdgcn_readfirstlane(h.y);
@@ -2796,8 +2817,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_O
         gd.b = np | (gd.b & 0xffff0000u);
       }
       // the slot after the guard's next move: row 15 of this tick's entry (staged a tick ago)
-      if (cached) gd.nslot = L.cone[par * 16 * mg + 8 * mg + 8 * g + 7];
-      if (k + 1 < K) dma_next_cone(par ^ 1);  // tick k + 1's entry if the env still acts then
+      if (cached && wid == 0) gd.nslot = L.cone[par * 16 * mg + 8 * mg + 8 * g + 7];
+      if (k + 1 < K && wid == 0) dma_next_cone(par ^ 1);  // tick k + 1's entry if the env still acts then
       LEAN_STAMP(1);  // 1: move, rotation, patrol
       // 3. visibility (environment.py:257-258)
       if (PROBE != 22 && PROBE != 28) cast(k, n_uniq, n_tie, par, true, staged_wide);
@@ -2805,23 +2826,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_O
     }
     // (tick k + 1's fan entry went out inside cast_fan; a frozen env keeps its plane and skips it)
     wide = n_uniq > 64;
-    // the plane's channel-1 quads (also the detection test's byte)
-    uint32_t v1[Q];
+    // the plane's channel-1 quads this wave stores (one wave: also the detection test's byte)
+    uint32_t v1[QW];
 #pragma unroll
-    for (int j = 0; j < Q; ++j) {
-      const int q = lane + 64 * j, qc = q < N4 ? q : N4 - 1, r = qc / C4;
+    for (int j = 0; j < QW; ++j) {
+      const int q = lane + 64 * (wid * QW + j), qc = q < N4 ? q : N4 - 1, r = qc / C4;
       v1[j] = *reinterpret_cast<const uint32_t*>(vis + OFF0 + r * PC + 4 * (qc - r * C4));
     }
     int done_now = s.done;
     LEAN_STAMP(4);  // 4: next fan DMA, the channel-1 quads
     if (!frozen && PROBE != 27 && PROBE != 28) {
       // 4. detection, vault, timeout (environment.py:271-297), in the reference's order
-      const int sol = s.pos_r * C_ + s.pos_c, qs = sol >> 2;
-      uint32_t vq = v1[0];  // the quad holding the solver's tile (register qs >> 6, wave-uniform)
+      bool seen;
+      if constexpr (NW == 1) {
+        const int sol = s.pos_r * C_ + s.pos_c, qs = sol >> 2;
+        uint32_t vq = v1[0];  // the quad holding the solver's tile (register qs >> 6, wave-uniform)
 #pragma unroll
-      for (int j = 1; j < Q; ++j) vq = (qs >> 6) == j ? v1[j] : vq;
-      const uint32_t qv = (uint32_t)__builtin_amdgcn_readlane((int)vq, qs & 63);
-      if ((qv >> (8 * (sol & 3))) & 0xffu) {
+        for (int j = 1; j < Q; ++j) vq = (qs >> 6) == j ? v1[j] : vq;
+        const uint32_t qv = (uint32_t)__builtin_amdgcn_readlane((int)vq, qs & 63);
+        seen = ((qv >> (8 * (sol & 3))) & 0xffu) != 0u;
+      } else {  // the quad may be the other wave's: the byte itself
+        seen = vis[OFF0 + s.pos_r * PC + s.pos_c] != 0;
+      }
+      if (seen) {
         s.detected = 1;
         reward += p.r_detect;
         s.done = 1;
@@ -2853,7 +2880,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_O
         gd.a &= ~0xffu;                        // idx 0
         gd.b = (gd.b & 0xffff0000u) | gd.pos0();  // the patrol start
       }
-      if (cached) {  // the cone of (patrol point 0, this slot), loaded now: only finishing envs pay for it
+      if (cached && wid == 0) {  // the cone of (patrol point 0, this slot), loaded now: only finishing envs pay for it
         const uint4* rsrc = reinterpret_cast<const uint4*>(eb.cones + cone_off(g, 0, gd.hslot()));
         const uint4 ra = rsrc[0], rb = rsrc[1];
         if (moved) {
@@ -2865,12 +2892,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_O
       if (moved) {  // the plane again from the reset poses (the staging holds tick k + 1's fan now)
         cast(k, n_uniq, n_tie, par, false, false);
 #pragma unroll
-        for (int j = 0; j < Q; ++j) {
-          const int q = lane + 64 * j, qc = q < N4 ? q : N4 - 1, r = qc / C4;
+        for (int j = 0; j < QW; ++j) {
+          const int q = lane + 64 * (wid * QW + j), qc = q < N4 ? q : N4 - 1, r = qc / C4;
           v1[j] = *reinterpret_cast<const uint32_t*>(vis + OFF0 + r * PC + 4 * (qc - r * C4));
         }
       }
-      if (k + 1 < K) dma_next_cone(par ^ 1);  // tick k + 1's entry from the reset pose
+      if (k + 1 < K && wid == 0) dma_next_cone(par ^ 1);  // tick k + 1's entry from the reset pose
     }
     LEAN_STAMP(6);  // 6: auto-reset
     // 6. tick k's stores (kStores, unconditional; lanes with nothing to store pass an offset
@@ -2883,8 +2910,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_O
     const int sol = s.pos_r * C_ + s.pos_c, qs = sol >> 2;
     const int vault = p.vr * C_ + p.vc;
 #pragma unroll
-    for (int j = 0; j < Q; ++j) {
-      const int q = lane + 64 * j;
+    for (int j = 0; j < QW; ++j) {
+      const int q = lane + 64 * (wid * QW + j);
       const bool in = q < N4;
       const int qc = in ? q : N4 - 1;
       const uint32_t b = PROBE == 26 ? 0x01020304u : *reinterpret_cast<const uint32_t*>(L.grid + 4 * qc);
@@ -2909,7 +2936,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_O
       obs_put(rs, pol, in ? 16 * (2 * N4 + q) : (int)kOOB, c2);
     }
     const uint32_t ko = (uint32_t)((size_t)k * N + e);
-    const int l0 = lane == 0 ? 0 : (int)kOOB;
+    const int l0 = lane == 0 && wid == 0 ? 0 : (int)kOOB;
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, (float)reward),
                                           __builtin_amdgcn_make_buffer_rsrc(rew + ko, (short)0, 4, 0x00020000), l0, 0, 0);
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, __builtin_bit_cast(uint64_t, reward)),
@@ -2934,6 +2961,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(HEIST_LEAN_O
     q[12] = (unsigned)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
   }
 #undef LEAN_STAMP
+  if (wid != 0) return;  // (its guards' heading slots are not tracked)
   if (lane == 0) p.scal[e] = s;
   if (live_cam) eb.cams[(uint32_t)lane].heading = heading;
   if (live_guard) {
@@ -3578,6 +3606,13 @@ size_t step_multi_lds(const EnvParams& p, int K) {
          align16(sizeof(TieBuckets)) + 1024 * (size_t)p.multi_waves + (p.stamps ? 80 * (size_t)p.multi_waves : 0);
 }
 
+// Two waves per env for the 32 x 32 lean kernel (HEIST_LEAN_WAVES: 0 auto, 1, 2): auto when
+// the batch's doubled waves still fit the chip at the kernel's 4 waves per SIMD.
+bool lean_two_waves(const EnvParams& p) {
+  if (p.lean_waves != 0) return p.lean_waves == 2;
+  return 2 * (size_t)p.n_envs <= 16 * (size_t)(p.n_cu > 0 ? p.n_cu : 256);
+}
+
 hipError_t launch_step_multi(const EnvParams& p, int K, const int64_t* actions, float* obs,
                              float* rew, double* rew64, uint8_t* done_out, int8_t* status_out, int auto_reset,
                              hipStream_t st) {
@@ -3627,6 +3662,9 @@ hipError_t launch_step_multi(const EnvParams& p, int K, const int64_t* actions, 
     else if (p.stamps)
       hipLaunchKernelGGL((step_lean_kernel<32, 32, true>), dim3(p.n_envs), dim3(64), lds_l, st, p, K, actions, obs, rew,
                          rew64, done_out, status_out, auto_reset);
+    else if (lean_two_waves(p))
+      hipLaunchKernelGGL((step_lean_kernel<32, 32, false, 0, 2>), dim3(p.n_envs), dim3(128), lds_l, st, p, K, actions,
+                         obs, rew, rew64, done_out, status_out, auto_reset);
     else
       hipLaunchKernelGGL((step_lean_kernel<32, 32>), dim3(p.n_envs), dim3(64), lds_l, st, p, K, actions, obs, rew,
                          rew64, done_out, status_out, auto_reset);

@@ -349,7 +349,7 @@ class HeistEnv:
 
     CONFIG_KEYS = ("step_waves", "ray_chunk", "step_occ", "vis_gap", "obs_store", "ray_mode", "probe_mode",
                    "dispatch_order", "split_obs", "guard_cones", "multi_waves", "fan_on", "lean", "interval_fans",
-                   "step_lean")
+                   "step_lean", "lean_waves")
 
     def kernel_config(self) -> dict:
         """The handle's effective kernel configuration (heist_get_config): the HEIST_* knobs as

@@ -12,7 +12,7 @@ def test_library_built_and_loads():
     if _build.needs_build():
         _build.build()
     lib = _native.lib()
-    assert lib.heist_abi_version() == 4
+    assert lib.heist_abi_version() == 5
 
 
 def test_every_header_symbol_is_exported():

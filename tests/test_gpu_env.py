@@ -869,21 +869,25 @@ def _interval_fan_layouts(n, R, budget, seed, **kw):
 
 
 @pytest.mark.parametrize("auto_reset", [True, False], ids=["auto_reset", "no_reset"])
-@pytest.mark.parametrize("R,n,budget,kw", [(20, 4096, 15, {}), (20, 512, 40, {}),
-                                           (32, 2048, 40, {"n_cams": 4, "n_guards": 3})],
-                         ids=["bench4096", "budget40", "c5_32x32"])
-def test_step_lean_interval_fans(gpu_device, monkeypatch, R, n, budget, kw, auto_reset):
+@pytest.mark.parametrize("R,n,budget,kw,waves", [(20, 4096, 15, {}, None), (20, 512, 40, {}, None),
+                                                 (32, 2048, 40, {"n_cams": 4, "n_guards": 3}, None),
+                                                 (32, 2048, 40, {"n_cams": 4, "n_guards": 3}, 1)],
+                         ids=["bench4096", "budget40", "c5_32x32", "c5_32x32_one_wave"])
+def test_step_lean_interval_fans(gpu_device, monkeypatch, R, n, budget, kw, waves, auto_reset):
     """step_lean_kernel's interval fans (cameras the shared fan does not serve: the synthetic
     mix) == single ticks of the step kernel, == the generic K-tick body (HEIST_INTERVAL_FANS=0),
     and 32 envs == the C oracle (reward, done, status, observation bytes) on every tick; short
     episodes, launches of 1, 20, 63 and 70 ticks; 20 x 20 and BASELINE C5's 32 x 32 (2048 envs,
     exactly 4 cameras + 3 guards, budget 40: four observation quads per lane, 19 stores per
-    row).  Cameras forced onto the default heading, cuts, axes and wide fovs
-    (_interval_fan_layouts).  Reference environment.py:216-299, security.py:53-101."""
+    row; at 2,048 envs two waves per env, HEIST_LEAN_WAVES=1 the one-wave form).  Cameras forced
+    onto the default heading, cuts, axes and wide fovs (_interval_fan_layouts).  Reference
+    environment.py:216-299, security.py:53-101."""
     cfg = EnvironmentConfig(grid_rows=R, grid_cols=R, max_steps=40, architect_budget=budget)
     lays = _interval_fan_layouts(n, R, budget, 300 + budget + R, **kw)
     envs = []
     monkeypatch.setenv("HEIST_MULTI_WAVES", "1")
+    if waves is not None:
+        monkeypatch.setenv("HEIST_LEAN_WAVES", str(waves))
     for i, ivl in enumerate(("1", "0", "1")):
         monkeypatch.setenv("HEIST_INTERVAL_FANS", ivl)
         env = (HeistEnv if i < 2 else _step_kernel_env)(n, cfg, max_cams=max(1, budget // 3),
@@ -896,6 +900,8 @@ def test_step_lean_interval_fans(gpu_device, monkeypatch, R, n, budget, kw, auto
     assert torch.equal(va, vb) and torch.equal(va, vc)
     assert a.kernel_config()["interval_fans"] == 1 and c.kernel_config()["interval_fans"] == 0
     assert a.kernel_config()["lean"] == 1 and a.kernel_config()["multi_waves"] == 1
+    if R == 32 and torch.cuda.get_device_properties(gpu_device).multi_processor_count >= 256:
+        assert a.kernel_config()["lean_waves"] == (waves or 2)
     valid = va.cpu().numpy().astype(bool)
     pick = np.random.default_rng(budget).choice(np.nonzero(valid)[0], 32, replace=False)
     pick_t = torch.from_numpy(pick).to(gpu_device)
@@ -974,6 +980,60 @@ def test_step_lean_interval_fans_narrow_fovs(gpu_device, monkeypatch, R, n, budg
                 assert (float(r64[k, i]), bool(done[k, i]), int(status[k, i])) == (r_, d_, s_), (k0 + k, i)
                 assert obs[k, i].cpu().numpy().tobytes() == o_env.state_tensor().tobytes(), (k0 + k, i)
         k0 += kk
+
+
+@pytest.mark.parametrize("waves", [1, 2])
+def test_step_lean_32x32_shared_fan_and_interval_mix(gpu_device, monkeypatch, waves):
+    """The 32 x 32 lean kernel with one and two waves per env on a batch that mixes envs the
+    shared fan serves (every camera the batch's first camera's twin: in the two-wave form wave
+    0 casts them) with interval-fan envs (the casts split over the waves) and envs the generic
+    body takes (a 4-degree fov: wave 1 leaves): K-tick launches with auto-reset == single ticks
+    of the step kernel, and 12 envs == the C oracle, over 60 ticks."""
+    n, R, budget = 512, 32, 40
+    cfg = EnvironmentConfig(grid_rows=R, grid_cols=R, max_steps=30, architect_budget=budget)
+    rng = np.random.default_rng(29 + waves)
+    lays = []
+    for walls, cams, guards in synthetic_layouts(n, R, R, budget, seed=131, n_cams=4, n_guards=3):
+        cams = [dict(c) for c in cams]
+        u = rng.random()
+        for c in cams:
+            if u < 0.5:  # the shared fan's source camera's twin
+                c.update(fov_angle=60.0, heading=30.0, rotation_speed=15.0)
+            elif u < 0.6:
+                c.update(fov_angle=4.0)
+        lays.append((walls, cams, guards))
+    first = lays[0][1][0]
+    first.update(fov_angle=60.0, heading=30.0, rotation_speed=15.0)
+    monkeypatch.setenv("HEIST_LEAN_WAVES", str(waves))
+    a = HeistEnv(n, cfg, max_cams=13, max_guards=8, max_path=16, device=gpu_device)
+    monkeypatch.delenv("HEIST_LEAN_WAVES")
+    b = _step_kernel_env(n, cfg, max_cams=13, max_guards=8, max_path=16, device=gpu_device)
+    va, vb = a.set_layouts(lays, budget=budget), b.set_layouts(lays, budget=budget)
+    assert torch.equal(va, vb)
+    a.reset()
+    b.reset()
+    assert a.kernel_config()["lean"] == 1 and a.kernel_config()["lean_waves"] == waves
+    pick = np.random.default_rng(5).choice(np.nonzero(va.cpu().numpy().astype(bool))[0], 12, replace=False)
+    oracles = _oracle_envs(cfg, [lays[i] for i in pick], budget)
+    g = torch.Generator(device="cpu").manual_seed(97)
+    acts = torch.randint(0, 5, (60, n), generator=g).to(gpu_device)
+    k0 = 0
+    for kk in (1, 20, 39):
+        obs, rew, done, status, r64 = a.step_multi(acts[k0:k0 + kk], reward64=True)
+        for k in range(kk):
+            o, r, d, s = b.step(acts[k0 + k])
+            assert torch.equal(obs[k], o) and torch.equal(r64[k], b.reward64), k0 + k
+            assert torch.equal(done[k], d) and torch.equal(status[k], s), k0 + k
+            for i, o_env in zip(pick, oracles):
+                r_, d_, s_ = o_env.step(int(acts[k0 + k, i]))
+                if d_:
+                    o_env.reset()
+                assert (float(r64[k, i]), bool(done[k, i]), int(status[k, i])) == (r_, d_, s_), (k0 + k, i)
+                assert obs[k, i].cpu().numpy().tobytes() == o_env.state_tensor().tobytes(), (k0 + k, i)
+        k0 += kk
+    sa, sb = a.export(grid=True), b.export(grid=True)
+    for key in sb:
+        assert torch.equal(sa[key], sb[key]), key
 
 
 def test_step_lean_interval_fans_on_architect_layouts(gpu_device, monkeypatch):

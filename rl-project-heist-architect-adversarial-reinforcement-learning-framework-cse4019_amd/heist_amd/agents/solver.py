@@ -174,7 +174,9 @@ class SolverAgent:  # agents/solver.py:18-259
             idx = torch.as_tensor(perm_fn(n), device=self.device) if n else None
             for k in range(n_mb):
                 start = k * bs
-                self.optimizer.zero_grad(set_to_none=False)
+                # grads written by the backward, not accumulated into zeros: every parameter is in
+                # the loss graph, so this only saves a fill and an add per parameter and step
+                self.optimizer.zero_grad(set_to_none=True)
                 w = 0
                 if start < n:
                     b = idx[start:start + bs]

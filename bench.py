@@ -335,11 +335,12 @@ def measure_env_config(dev, R, n, budget, steps=100, warmup=10, K=1, **kw):
     ncam, ngu = float(st["n_cams"].double().mean()), float(st["n_guards"].double().mean())
     b = algorithmic_bytes_per_env_step(R, R, ncam, ngu)
     gbs = b * n / (ms * 1e-3) / 1e9
-    kname = multi_kernel_name(env.kernel_config(), R, R) if K > 1 else "heist::step_kernel"
+    kcfg = env.kernel_config()
+    kname = multi_kernel_name(kcfg, R, R) if K > 1 else "heist::step_kernel"
     env.close()
     return {"value": n / (ms * 1e-3), "unit": "env-steps/s", "kernel_ms": ms, "envs": n, "grid": "%dx%d" % (R, R),
             "budget": budget, "mean_cameras": ncam, "mean_guards": ngu, "ticks_per_launch": K,
-            "shared_fan_frac": fan,
+            "shared_fan_frac": fan, "waves_per_env": kcfg["lean_waves"] if R == 32 and kcfg["lean"] else 1,
             "ray_samples_per_env_step": samples, "ray_samples_per_s": samples * n / (ms * 1e-3),
             "kernel": kname,
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

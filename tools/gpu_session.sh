@@ -14,6 +14,7 @@
 #   prof              rocprofv3 kernel trace + stats of the headline (bench.py --no-secondary)
 #   pmc               PMC passes on the headline: FETCH_SIZE, WRITE_SIZE, SQ mix (+ summaries)
 #   pmc_c4            the same on BASELINE C4's env-only command (tools/probe_env_configs.py, c4)
+#   pmc_c5            the same on BASELINE C5's (2048 envs of 32 x 32)
 #   train             tools/probe_train.py (the fp32 training iteration's parts)
 #   prof_train        rocprofv3 kernel stats of tools/probe_train.py
 #   arch              tools/probe_arch_update.py (Architect update kernel, per-update time)
@@ -60,6 +61,15 @@ for step in "$@"; do
       unset PROBE_CONFIGS
       python tools/pmc_traffic.py "$OUT/pmc_c4_fetch" "$OUT/pmc_c4_write" --ticks 20 --envs 8192 --workload c4 --profile "$TAG" --out "$OUT/c4_traffic.json" > /dev/null
       python tools/pmc_sq.py "$OUT/pmc_c4_sq" --ticks 20 --out "$OUT/c4_pmc_sq.json" > /dev/null ;;
+    pmc_c5)  # the same three passes on BASELINE C5's env-only command (2048 envs of 32 x 32, two waves per env)
+      export PROBE_CONFIGS=c5
+      C5="python3 tools/probe_env_configs.py"
+      run pmc_c5_fetch 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_c5_fetch" -o heist --output-format csv -- $C5
+      run pmc_c5_write 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_c5_write" -o heist --output-format csv -- $C5
+      run pmc_c5_sq 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS -d "$OUT/pmc_c5_sq" -o heist --output-format csv -- $C5
+      unset PROBE_CONFIGS
+      python tools/pmc_traffic.py "$OUT/pmc_c5_fetch" "$OUT/pmc_c5_write" --ticks 20 --envs 2048 --workload c5 --profile "$TAG" --out "$OUT/c5_traffic.json" > /dev/null
+      python tools/pmc_sq.py "$OUT/pmc_c5_sq" --ticks 20 --out "$OUT/c5_pmc_sq.json" > /dev/null ;;
     train) run train 600 python3 tools/probe_train.py ;;
     prof_train) run prof_train 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_train" -o train --output-format csv -- python3 tools/probe_train.py ;;
     arch) run arch 300 python3 tools/probe_arch_update.py ;;

@@ -27,7 +27,7 @@ extern "C" {
 /* 2: heist_step_stamps takes the buffer size; heist_stamp_words; 3: heist_arch_update_*;
  * 4: heist_arch_update_status, the heist_*_nhwc training passes, heist_get_config's 15th word
  *    (heist_step on the lean kernel), the heist_train_* fp32-MFMA training convolutions,
- *    heist_rollout_tally; 5: heist_get_config's 16th word (lean_waves) */
+ *    heist_rollout_tally; 5: heist_get_config's 16th word (lean_waves), heist_lstm_cell */
 #define HEIST_ABI_VERSION 5
 #define HEIST_EINVAL 100000
 
@@ -272,6 +272,15 @@ int heist_arch_update_stamps(uint64_t* buf);
  * (status 1) or timeout (any other status) and to attempts; h, c [n][hidden] float32 (the
  * LSTM state, layer dimension 1) are multiplied by (done ? 0 : 1).  valid, done uint8 (bool),
  * status int8, the counters int32. */
+/* The Solver's LSTM cell after its gate GEMMs (reference networks.py:90-100, nn.LSTM one time
+ * step, gate order i, f, g, o; replaces the ten pointwise torch kernels of
+ * SolverNetwork.lstm_step in the rollout): gates = gates_x + gates_h ([n][4 hidden] float32
+ * each), c_out = sigmoid(f) * c + sigmoid(i) * tanh(g), h_out = sigmoid(o) * tanh(c_out)
+ * ([n][hidden]), every operation rounded to float32 in that order (bit-identical to torch's
+ * kernels). */
+int heist_lstm_cell(const float* gates_x, const float* gates_h, const float* c, float* h_out, float* c_out, int hidden,
+                    int n, heist_stream_t stream);
+
 int heist_rollout_tally(const uint8_t* valid, int32_t* attempts, int attempts_per_layout, const uint8_t* done,
                         const int8_t* status, const double* reward64, int32_t* steps, double* reward_sum, int32_t* solve,
                         int32_t* detect, int32_t* timeout, float* h, float* c, int hidden, int n, heist_stream_t stream);

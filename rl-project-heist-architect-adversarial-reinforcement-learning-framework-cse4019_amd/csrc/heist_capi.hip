@@ -85,6 +85,8 @@ hipError_t launch_rollout_tally(const uint8_t* valid, int32_t* attempts, int A, 
                                 const double* reward64, int32_t* steps, double* reward_sum, int32_t* solve,
                                 int32_t* detect, int32_t* timeout, float* h, float* c, int hidden, int n, int vault,
                                 int det, hipStream_t st);
+hipError_t launch_lstm_cell(const float* gx, const float* gh, const float* c, float* h1, float* c1, int H, int n,
+                            hipStream_t st);
 hipError_t launch_adv_moments(const float* x, int64_t n, int phase, double* acc, hipStream_t st);
 hipError_t launch_adv_apply(float* x, int64_t n, const double* acc, float eps, hipStream_t st);
 hipError_t launch_ppo_loss(const float* logits, const float* values, const int64_t* actions, const float* old_logp,
@@ -690,6 +692,15 @@ int heist_rollout_tally(const uint8_t* valid, int32_t* attempts, int attempts_pe
                                                HEIST_DETECTED,
                                                (hipStream_t)stream),
                    "heist_rollout_tally");
+}
+
+int heist_lstm_cell(const float* gates_x, const float* gates_h, const float* c, float* h_out, float* c_out, int hidden,
+                    int n, heist_stream_t stream) {
+  HEIST_REQUIRE(n >= 0 && hidden >= 1, "heist_lstm_cell: bad sizes");
+  if (n == 0) return 0;
+  HEIST_REQUIRE(gates_x && gates_h && c && h_out && c_out, "heist_lstm_cell: null pointer");
+  return check_hip(heist::launch_lstm_cell(gates_x, gates_h, c, h_out, c_out, hidden, n, (hipStream_t)stream),
+                   "heist_lstm_cell");
 }
 
 int heist_gae(const float* rewards, const float* values, const uint8_t* dones, const float* last_value, int T, int n,

@@ -250,6 +250,38 @@ hipError_t launch_rollout_tally(const uint8_t* valid, int32_t* attempts, int A, 
   return hipGetLastError();
 }
 
+// The Solver's LSTM cell after its two gate GEMMs (networks.py:90-100 nn.LSTM, one time step,
+// gate order i, f, g, o), one thread per (row, hidden unit): gates = gx + gh, then
+// c1 = sigmoid(f) c + sigmoid(i) tanh(g), h1 = sigmoid(o) tanh(c1) -- each product and sum
+// rounded to fp32 as the ten torch kernels it replaces round them (sigmoid as 1 / (1 + exp(-x)),
+// torch's form), so the result is theirs bit for bit.
+__device__ __forceinline__ float sigmoid_f(float x) { return 1.0f / (1.0f + expf(-x)); }
+__global__ __launch_bounds__(256) void lstm_cell_kernel(const float* __restrict__ gx, const float* __restrict__ gh,
+                                                        const float* __restrict__ c, float* __restrict__ h1,
+                                                        float* __restrict__ c1, int H, int n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)n * H) return;
+  const int64_t b = i / H;
+  const int j = (int)(i - b * H);
+  const float* x = gx + b * 4 * H;
+  const float* y = gh + b * 4 * H;
+  const float gi = x[j] + y[j], gf = x[H + j] + y[H + j], gg = x[2 * H + j] + y[2 * H + j],
+              go = x[3 * H + j] + y[3 * H + j];
+  const float t1 = sigmoid_f(gf) * c[i];
+  const float t2 = sigmoid_f(gi) * tanhf(gg);
+  const float cc = t1 + t2;
+  c1[i] = cc;
+  h1[i] = sigmoid_f(go) * tanhf(cc);
+}
+
+hipError_t launch_lstm_cell(const float* gx, const float* gh, const float* c, float* h1, float* c1, int H, int n,
+                            hipStream_t st) {
+  const int64_t total = (int64_t)n * H;
+  if (total <= 0) return hipSuccess;
+  hipLaunchKernelGGL(lstm_cell_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, gx, gh, c, h1, c1, H, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_gae(const float* r, const float* v, const uint8_t* d, const float* last_value, int T, int N,
                       double gamma, double lam, float* adv, float* ret, hipStream_t st) {
   const float g = (float)gamma, gl = (float)(gamma * lam);

@@ -60,6 +60,7 @@ SIGNATURES = {
     "heist_relu_bwd_nhwc": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
     "heist_arch_update_stamps": (_i, [_vp]),
     "heist_gae": (_i, [_vp, _vp, _vp, _vp, _i, _i, _d, _d, _vp, _vp, _vp]),
+    "heist_lstm_cell": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _vp]),
     "heist_rollout_tally": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp]),
     "heist_adv_moments": (_i, [_vp, _i64, _i, _vp, _vp]),
     "heist_adv_apply": (_i, [_vp, _i64, _vp, _f, _vp]),

@@ -278,8 +278,19 @@ class SolverNetwork(nn.Module):  # networks.py:13-131
     def lstm_step(self, x: torch.Tensor, hidden: Tuple[torch.Tensor, torch.Tensor]):
         """One LSTM time step with nn.LSTM's gate order (i, f, g, o)."""
         h, c = hidden[0][0], hidden[1][0]
-        gates = F.linear(x, self.lstm.weight_ih_l0, self.lstm.bias_ih_l0) + \
-            F.linear(h, self.lstm.weight_hh_l0, self.lstm.bias_hh_l0)
+        gx = F.linear(x, self.lstm.weight_ih_l0, self.lstm.bias_ih_l0)
+        gh = F.linear(h, self.lstm.weight_hh_l0, self.lstm.bias_hh_l0)
+        if (not torch.is_grad_enabled() and gx.is_cuda and gx.dtype == torch.float32 and gh.dtype == torch.float32
+                and c.dtype == torch.float32):
+            # inference (the rollout): the pointwise part as one HIP kernel (heist_lstm_cell),
+            # the ten torch kernels' roundings in their order
+            from . import _native as nat
+            gx, gh, c = gx.contiguous(), gh.contiguous(), c.contiguous()
+            h1, c1 = torch.empty_like(c), torch.empty_like(c)
+            nat.check(nat.lib().heist_lstm_cell(nat.ptr(gx), nat.ptr(gh), nat.ptr(c), nat.ptr(h1), nat.ptr(c1),
+                                                c.shape[1], c.shape[0], nat.stream(gx.device)), "heist_lstm_cell")
+            return h1, (h1.unsqueeze(0), c1.unsqueeze(0))
+        gates = gx + gh
         i, f, g, o = gates.chunk(4, dim=1)
         c1 = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(g)
         h1 = torch.sigmoid(o) * torch.tanh(c1)

@@ -234,10 +234,10 @@ class SolverAgent:  # agents/solver.py:18-259
         else:
             logits, value, hidden = self.network(obs, hidden)
         logp_all = F.log_softmax(logits.float(), dim=-1)
-        action = torch.multinomial(logp_all.exp(), 1, generator=generator).reshape(-1)
+        probs = logp_all.exp()
+        action = torch.multinomial(probs, 1, generator=generator).reshape(-1)
         # Categorical(probs).log_prob = log(clamp(p / sum p, eps, 1 - eps))
-        p = logp_all.exp()
-        p = p / p.sum(-1, keepdim=True)
+        p = probs / probs.sum(-1, keepdim=True)
         eps = torch.finfo(p.dtype).eps
         logp = torch.log(p.gather(1, action[:, None]).clamp(eps, 1 - eps)).reshape(-1)
         return action, logp, value.reshape(-1).float(), hidden

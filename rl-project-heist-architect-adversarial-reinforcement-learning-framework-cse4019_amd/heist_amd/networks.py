@@ -127,6 +127,59 @@ def _tc_mask(n, R, C, ch, dev) -> torch.Tensor:
     return torch.empty((n, R, C, ch // 4), dtype=torch.uint8, device=dev)
 
 
+def _wgrad_splitk(g: torch.Tensor, x: torch.Tensor, chunks: int = 16) -> torch.Tensor:
+    """dW = g^T x over many rows and few outputs (the Solver's fc / LSTM / head weight
+    gradients over a 16,384-row minibatch): the rows in `chunks` slices as one batched GEMM, the
+    partials summed in slice order -- one GEMM of this shape fills a fraction of the chip
+    (480 -> 172 us for the update's five, profiles/r06zs_dw_splitk.log); the result differs from
+    the single GEMM's only by the order of the fp32 sums."""
+    m = g.shape[0]
+    step = m // chunks
+    main = step * chunks
+    gb = g[:main].reshape(chunks, step, g.shape[1])
+    xb = x[:main].reshape(chunks, step, x.shape[1])
+    dw = torch.bmm(gb.transpose(1, 2), xb).sum(0)
+    if main < m:
+        dw = dw + g[main:].t() @ x[main:]
+    return dw
+
+
+class _LinearSplitK(torch.autograd.Function):
+    """F.linear whose weight gradient is _wgrad_splitk (input gradient and bias gradient as
+    autograd forms them: g @ W, g summed over rows)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        return F.linear(x, w, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, w = ctx.saved_tensors
+        g = g.contiguous()
+        dx = g @ w if ctx.needs_input_grad[0] else None
+        dw = _wgrad_splitk(g, x.contiguous()) if ctx.needs_input_grad[1] else None
+        db = g.sum(0) if ctx.has_bias and ctx.needs_input_grad[2] else None
+        return dx, dw, db
+
+
+def _linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> torch.Tensor:
+    """F.linear; in an fp32 training forward on a HIP device over >= 4,096 rows, with the
+    split-K weight gradient (HEIST_SPLITK_WGRAD=0 turns it off)."""
+    import os
+    if (torch.is_grad_enabled() and w.requires_grad and x.is_cuda and x.dim() == 2 and x.shape[0] >= 4096
+            and x.dtype == torch.float32 and w.dtype == torch.float32 and not torch.is_autocast_enabled("cuda")
+            and os.environ.get("HEIST_SPLITK_WGRAD", "1") != "0"):
+        return _LinearSplitK.apply(x, w, b)
+    return F.linear(x, w, b)
+
+
+def _mlp_head(seq: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
+    """Linear, ReLU, Linear (the policy / value heads) with _linear for the first layer."""
+    return seq[2](F.relu(_linear(x, seq[0].weight, seq[0].bias)))
+
+
 class _BackboneMFMA32(torch.autograd.Function):
     """SolverNetwork's conv stack (networks.py:93-100) forward and backward on the hand-written
     fp32-MFMA kernels (csrc/heist_train_conv.hip, heist_train_* in include/heist.h): conv1-3
@@ -264,22 +317,22 @@ class SolverNetwork(nn.Module):  # networks.py:13-131
         if self._train_conv_ok(state):
             x = _BackboneMFMA32.apply(state, self.conv1.weight, self.conv1.bias, self.conv2.weight, self.conv2.bias,
                                       self.conv3.weight, self.conv3.bias)
-            return F.relu(self.fc_spatial(x))
+            return F.relu(_linear(x, self.fc_spatial.weight, self.fc_spatial.bias))
         if self._fused_tail_ok(state):
             x = _BackboneF32.apply(state, self.conv1.weight, self.conv1.bias, self.conv2.weight, self.conv2.bias,
                                    self.conv3.weight, self.conv3.bias)
-            return F.relu(self.fc_spatial(x))
+            return F.relu(_linear(x, self.fc_spatial.weight, self.fc_spatial.bias))
         x = F.relu(self.conv1(state))
         x = F.relu(self.conv2(x))
         x = F.relu(self.conv3(x))
         x = self.pool(x)
-        return F.relu(self.fc_spatial(x.reshape(state.shape[0], -1)))
+        return F.relu(_linear(x.reshape(state.shape[0], -1), self.fc_spatial.weight, self.fc_spatial.bias))
 
     def lstm_step(self, x: torch.Tensor, hidden: Tuple[torch.Tensor, torch.Tensor]):
         """One LSTM time step with nn.LSTM's gate order (i, f, g, o)."""
         h, c = hidden[0][0], hidden[1][0]
-        gx = F.linear(x, self.lstm.weight_ih_l0, self.lstm.bias_ih_l0)
-        gh = F.linear(h, self.lstm.weight_hh_l0, self.lstm.bias_hh_l0)
+        gx = _linear(x, self.lstm.weight_ih_l0, self.lstm.bias_ih_l0)
+        gh = _linear(h, self.lstm.weight_hh_l0, self.lstm.bias_hh_l0)
         if (not torch.is_grad_enabled() and gx.is_cuda and gx.dtype == torch.float32 and gh.dtype == torch.float32
                 and c.dtype == torch.float32):
             # inference (the rollout): the pointwise part as one HIP kernel (heist_lstm_cell),
@@ -303,7 +356,7 @@ class SolverNetwork(nn.Module):  # networks.py:13-131
         if hidden is None:
             hidden = self._init_hidden(b, state.device)
         out, new_hidden = self.lstm_step(spatial, hidden)
-        return self.policy_head(out), self.value_head(out), new_hidden
+        return _mlp_head(self.policy_head, out), _mlp_head(self.value_head, out), new_hidden
 
     # -- fused backbone (heist_solver_features, bf16 MFMA) -----------------------------
     def fused_supported(self, state: torch.Tensor) -> bool:

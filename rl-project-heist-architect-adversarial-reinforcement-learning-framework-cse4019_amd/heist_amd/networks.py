@@ -176,8 +176,8 @@ def _linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor]) -> torc
 
 
 def _mlp_head(seq: nn.Sequential, x: torch.Tensor) -> torch.Tensor:
-    """Linear, ReLU, Linear (the policy / value heads) with _linear for the first layer."""
-    return seq[2](F.relu(_linear(x, seq[0].weight, seq[0].bias)))
+    """Linear, ReLU, Linear (the policy / value heads) on _linear."""
+    return _linear(F.relu(_linear(x, seq[0].weight, seq[0].bias)), seq[2].weight, seq[2].bias)
 
 
 class _BackboneMFMA32(torch.autograd.Function):
